@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Headline benchmark: frames/sec of the 7x512x512 -> 1x512x512 U-Net training
+step (forward + CustomLoss + backward + grad all-reduce + clip + AdamW) on
+MI355X, data-parallel over N GPUs (one process per GPU, RCCL over xGMI).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Workload (BASELINE.json configs[1]): batch 8 per GPU, 7x512x512 fp32
+synthetic G-buffers (x ~ N(0,1), labels integers(0,256)/255), random-init
+weights of the reference architecture, dropout 0.2 (train mode), inputs
+resident in HBM and requiring grad like the reference's batches
+(setdata.py:325-326). Weak scaling: per-GPU batch fixed as N grows.
+
+Rank 0 prints ONE JSON line with the metric, a roofline object for the
+dominant kernel (conv6.conv.0 forward: 3x3, 1024->1024 at 64x64, the largest
+MFMA launch) timed with HIP events on its launch stream during the timed
+steps, and a CPU baseline (the oracle restatement on the host cores).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pcss-unet_amd"))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (spec)
+HBM_PEAK_GBS = 8000.0
+
+
+def conv_flops(B, H, W, cin, cout, k):
+    return 2.0 * B * H * W * cin * cout * k * k
+
+
+def unet_fwd_flops(in_ch, H, W):
+    """sum over the 17 convs of 2*H*W*Cin*Cout*k^2 per frame."""
+    R = (H // 2, W // 2)
+    ch = {2: (4 * in_ch, 64), 3: (64, 128), 4: (128, 512), 5: (512, 1024),
+          6: (1024, 512), 7: (512, 128), 8: (128, 64), 9: (64, 16)}
+    res = {2: R, 3: (R[0] // 2, R[1] // 2), 4: (R[0] // 4, R[1] // 4), 5: (R[0] // 8, R[1] // 8),
+           6: (R[0] // 4, R[1] // 4), 7: (R[0] // 2, R[1] // 2), 8: R, 9: R}
+    f = 0.0
+    for k, (ci, co) in ch.items():
+        h, w = res[k]
+        f += conv_flops(1, h, w, ci, ci, 3) + conv_flops(1, h, w, ci, co, 1)
+    f += conv_flops(1, R[0], R[1], 16, 4, 1)
+    return f
+
+
+def cpu_baseline(in_ch, H, W, frames=1, reps=3):
+    """Oracle restatement (same ATen ops as the reference) fp32 fwd+bwd on the
+    host cores: frames/s on a bounded sample (`frames` frames x `reps`)."""
+    from oracle import unet_ref as O
+    from oracle.weights import make_state, synthetic_batch
+    cores = len(os.sched_getaffinity(0))
+    torch.set_num_threads(min(cores, 64))
+    sd = O.torch_state(make_state(in_ch, 42), requires_grad=True)
+    x_np, y_np = synthetic_batch(frames, in_ch, H, W)
+    y = torch.from_numpy(y_np)
+
+    def step():
+        x = torch.from_numpy(x_np).requires_grad_(True)
+        out, _ = O.forward(sd, x, True, None, 0.0)
+        O.custom_loss(out, y, 0.9).backward()
+
+    step()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        step()
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"value": frames / t, "unit": "frames/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"{frames} frame(s) {in_ch}x{H}x{W} fp32 train step (fwd+L1+bwd), "
+                      f"oracle/unet_ref.py on PyTorch CPU, median of {reps} after 1 warmup, "
+                      f"{ts and round(sum(ts), 2)} s timed"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch")
+    ap.add_argument("--in-ch", type=int, default=7)
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+
+    import nsm_amd
+    from nsm_amd import ops as nops
+
+    torch.manual_seed(1234 + rank)
+    B, C, H, W = args.batch, args.in_ch, args.res, args.res
+    model = nsm_amd.Unet(in_ch=C, dropout_rate=0.2).to(dev).train()
+    if world > 1:  # identical initial weights on every rank (DDP semantics)
+        with torch.no_grad():
+            for p in model.parameters():
+                dist.broadcast(p, 0)
+    opt = nsm_amd.FlatAdamW(model.parameters(), lr=7e-4, weight_decay=1e-3, max_grad_norm=1.0,
+                            world_size=world)
+    crit = nsm_amd.CustomLoss(dev, alpha=0.9)
+    g = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(B, C, H, W, device=dev, generator=g).requires_grad_(True)
+    y = (torch.randint(0, 256, (B, 1, H, W), device=dev, generator=g).float() / 255.0)
+
+    def step():
+        out = model(x)
+        loss = crit(out, y, x)
+        loss.backward()
+        if world > 1:
+            nsm_amd.allreduce_grads(model.parameters())
+        opt.step()
+        opt.zero_grad()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    probe_tag = "conv6.conv.0.fwd"
+    nops.PROBES[probe_tag] = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    evs = nops.PROBES.pop(probe_tag)
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else float("nan")
+
+    frames = world * B * args.steps
+    value = frames / elapsed
+    Rh = H // 2
+    k_flops = conv_flops(B, Rh // 4, Rh // 4, 1024, 1024, 3)
+    achieved = k_flops / (kern_ms * 1e-3) / 1e12
+    step_flops = 3 * unet_fwd_flops(C, H, W) * B
+    res = {
+        "metric": "frames/sec 7x512x512 U-Net fwd+bwd (train step)",
+        "value": round(value, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (x~N(0,1), labels integers(0,256)/255), random-init weights",
+        "config": {"workload": f"configs[1]: batch={B}/GPU {C}x{H}x{W} fp32 train step "
+                               "(fwd + 0.9*L1 + bwd + RCCL grad all-reduce + clip + AdamW)",
+                   "global_batch": world * B, "in_ch": C, "res": [H, W],
+                   "parallelism": f"dp{world}"},
+        "model_tflops_per_s": round(step_flops * args.steps / elapsed / 1e12 / world, 2),
+        "roofline": {"kernel": f"{probe_tag} (nsm gemm_f32 implicit-GEMM 3x3, "
+                               f"M={B * (Rh // 4) ** 2} N=1024 K=9216)",
+                     "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+                     "avg_launch_ms": round(kern_ms, 4), "launches": len(evs),
+                     "algorithmic_flops_per_launch": k_flops, "traffic": None},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(C, H, W)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

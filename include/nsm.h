@@ -1,0 +1,159 @@
+/*
+ * nsm.h — C ABI of libnsm.so, the MI355X-native (gfx950 / CDNA4) hot path of
+ * the Neural-Shadow-Mapping U-Net of SDU-Gary/PCSS-Unet.
+ *
+ * The reference exposes no FFI: its boundary is the Python nn.Module /
+ * loss-callable surface. Each entry point below replaces the
+ * ATen op(s) the reference dispatches at the cited line; the Python host
+ * (pcss-unet_amd/nsm_amd) binds them with ctypes underneath a drop-in
+ * `Unetmodel.Unet` / `customLoss.CustomLoss` / `pert_loss.PerturbationLoss`.
+ *
+ * Conventions (all entry points):
+ *   - extern "C", POD arguments only: device pointers, int / int64 sizes,
+ *     float hyper-parameters, and the HIP stream as `void*` (hipStream_t).
+ *   - Activations are NHWC fp32, channel count padded to a multiple of 32
+ *     ("cp"); padded channels are kept exactly zero by zero weights/affine.
+ *   - Caller owns all memory (PyTorch caching allocator); the library never
+ *     allocates or synchronises; every launch is asynchronous on `stream`
+ *     and hipGraph-capturable.
+ *   - Return 0 on success, else NSM_E_* ; message via nsm_get_last_error().
+ */
+#ifndef NSM_H_
+#define NSM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NSM_OK 0
+#define NSM_E_ARG 1 /* bad shape / pointer / alignment */
+#define NSM_E_HIP 2 /* HIP launch error */
+#define NSM_E_WS 3  /* workspace too small */
+
+#define NSM_PACK_FWD 0   /* w[co][ci][k][k] -> [co_p][tap][ci_p]            */
+#define NSM_PACK_DGRAD 1 /* w[co][ci][k][k] -> [ci_p][tap'][co_p], tap'=k*k-1-tap */
+
+/* ---- library ----------------------------------------------------------- */
+int nsm_version(void);
+int nsm_get_last_error(char* buf, size_t n);
+
+/* ---- parameter layout ------------------------------------------------------
+ * Replaces the implicit weight layout of nn.Conv2d (Unetmodel.py:21,26) with
+ * the MFMA operand layout; nsm_pad_vec pads bias / BN affine to cp. */
+int nsm_pack_conv_weight(const float* w, int cout, int cin, int ksize, int cout_p, int cin_p,
+                         int mode, float* out, void* stream);
+int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
+
+/* ---- convolution as MFMA implicit GEMM (fp32 in, fp32 accumulate) ----------
+ * nsm_conv_fwd: y[p][co] = bias[co] + sum_{tap,ci} pro(x[p+off(tap)][ci]) * W
+ *   Replaces F.conv2d 3x3 pad 1 / 1x1 of DoubleConv (Unetmodel.py:21,26) and,
+ *   with NSM_PACK_DGRAD weights and bias=NULL, its input-gradient (autograd
+ *   ConvolutionBackward dgrad).  Optional prologue (1x1 only, pro_scale!=NULL):
+ *   pro(v) = lrelu(v*scale[ci]+shift[ci], slope) * mask[b*cin_p+ci] — the
+ *   BN-apply + LeakyReLU + Dropout2d between the two convs
+ *   (Unetmodel.py:22-24) fused into the operand load. mask may be NULL. */
+int nsm_conv_fwd(const float* x, int ldx, int B, int H, int W, int cin_p, const float* wpk,
+                 const float* bias, int cout_p, int ksize, float* y, int ldy, const float* pro_scale,
+                 const float* pro_shift, const float* pro_mask, float slope, void* stream);
+
+/* nsm_conv_wgrad: dw[co][ci][kh][kw] (real cout x cin, reference layout) =
+ *   sum_p dy[p][co] * pro(x[p+off(tap)][ci]); deterministic split-K over
+ *   pixels through `ws` (nsm_conv_wgrad_ws() floats). Replaces the weight
+ *   gradient of ConvolutionBackward for Unetmodel.py:21,26. If dbias != NULL
+ *   it is left untouched (bias grads come from nsm_bn_bwd_finalize). */
+size_t nsm_conv_wgrad_ws(int B, int H, int W, int cin_p, int cout_p, int ksize);
+int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx, int B, int H, int W,
+                   int cin_p, int cout_p, int ksize, const float* pro_scale, const float* pro_shift,
+                   const float* pro_mask, float slope, float* ws, size_t ws_floats, int cin, int cout,
+                   float* dw, void* stream);
+
+/* ---- BatchNorm2d(eps, momentum) train/eval (Unetmodel.py:22,27) ----------- */
+int nsm_reduce_chunks(int M, int C); /* partial-buffer rows for the two below */
+/* per-channel chunk partials {sum, M2 about chunk mean}: partial[nchunk][2][C] */
+int nsm_bn_stats(const float* y, int ld, int M, int C, float* partial, int nchunk, void* stream);
+/* merge partials; batch mean/biased var normalise; unbiased var feeds running
+ * stats, applied n_updates times (2 for conv5: checkpoint recompute,
+ * Unetmodel.py:114-116); num_batches_tracked += n_updates.
+ * Emits scale=gamma*invstd, shift=beta-mean*scale, mean, invstd. */
+int nsm_bn_finalize_train(const float* partial, int nchunk, int M, int C, int c_real,
+                          const float* gamma, const float* beta, float* run_mean, float* run_var,
+                          int64_t* num_batches, float momentum, float eps, int n_updates,
+                          float* mean, float* invstd, float* scale, float* shift, void* stream);
+int nsm_bn_finalize_eval(const float* run_mean, const float* run_var, const float* gamma,
+                         const float* beta, int C, int c_real, float eps, float* mean,
+                         float* invstd, float* scale, float* shift, void* stream);
+/* out = lrelu(y*scale+shift, slope) (+ res): BN apply + LeakyReLU
+ * (Unetmodel.py:27-28) fused with the additive skip (Unetmodel.py:125,131,137) */
+int nsm_bn_act(const float* y, int ldy, int M, int C, const float* scale, const float* shift,
+               float slope, const float* res, int ldres, float* out, int ldo, void* stream);
+/* backward of  z = lrelu(mask * ... ) chains around a train-mode BN:
+ *   dz = g * mask[b][c] * lrelu'(y*scale+shift); partial {sum dz, sum dz*xhat}. */
+int nsm_bn_bwd_reduce(const float* g, int ldg, const float* y, int ldy, int M, int C, int HW,
+                      const float* scale, const float* shift, float slope, const float* mask,
+                      const float* mean, const float* invstd, float* partial, int nchunk,
+                      void* stream);
+/* dgamma, dbeta (real channels), bias grad of the producing conv
+ * (analytically 0 in train mode), coef[3][C] for nsm_bn_bwd_apply. */
+int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int C, int c_real,
+                        const float* gamma, const float* invstd, float* dgamma, float* dbeta,
+                        float* dbias_prev, float* coef, void* stream);
+/* dy = coef0*dz + coef1*(y-mean) + coef2 */
+int nsm_bn_bwd_apply(const float* g, int ldg, const float* y, int ldy, int M, int C, int HW,
+                     const float* scale, const float* shift, float slope, const float* mask,
+                     const float* mean, const float* coef, float* dy, int lddy, void* stream);
+
+/* ---- resampling -------------------------------------------------------------
+ * AvgPool2d(2) (Unetmodel.py:40,43,46): floor mode. bwd: dx = skip + dy/4. */
+int nsm_avgpool2_fwd(const float* x, int B, int H, int W, int C, float* y, void* stream);
+int nsm_avgpool2_bwd_add(const float* dy, int B, int H, int W, int C, const float* skip,
+                         float* dx, void* stream);
+/* bilinear, align_corners=True: nn.Upsample(x2) and _upsample_and_match
+ * (Unetmodel.py:51-60,118-119). bwd is a deterministic gather. */
+int nsm_resize_fwd(const float* x, int B, int Hi, int Wi, int C, float* y, int Ho, int Wo,
+                   void* stream);
+int nsm_resize_bwd(const float* dy, int B, int Hi, int Wi, int C, float* dx, int Ho, int Wo,
+                   void* stream);
+
+/* ---- model boundary ---------------------------------------------------------
+ * pixel_unshuffle(2) + NCHW->NHWC + channel pad (Unetmodel.py:65-67,101) */
+int nsm_input_prep(const float* x, int B, int C, int H, int W, float* out, int cp, void* stream);
+int nsm_input_grad(const float* dX, int B, int C, int H, int W, int cp, float* dx, void* stream);
+/* conv10 1x1 16->4 + pixel_shuffle(2) + sigmoid (Unetmodel.py:63,143-148) */
+int nsm_head_fwd(const float* z, int ldz, int B, int Rh, int Rw, const float* w10,
+                 const float* b10, float* out, void* stream);
+int nsm_head_bwd_blocks(int B, int Rh, int Rw);
+int nsm_head_bwd(const float* gout, const float* out, const float* z, int ldz, int B, int Rh,
+                 int Rw, const float* w10, float* dz, float* partial, float* dw10, float* db10,
+                 void* stream);
+
+/* ---- losses -----------------------------------------------------------------
+ * nn.L1Loss (customLoss.py:96,134) scaled by alpha (customLoss.py:160);
+ * bwd: grad = alpha * sign(o-t) / n * (*gscale) (+ grad if accumulate). */
+int nsm_loss_blocks(int64_t n);
+int nsm_l1_loss_fwd(const float* o, const float* t, int64_t n, float alpha, float* partial,
+                    float* out, void* stream);
+int nsm_l1_loss_bwd(const float* o, const float* t, int64_t n, float alpha, const float* gscale,
+                    float* grad, int accumulate, void* stream);
+/* PerturbationLoss.perturb_input (pert_loss.py:26-59):
+ * per-channel unbiased std over the batch of NCHW x -> std[C] */
+int nsm_channel_std(const float* x, int B, int C, int H, int W, float* partial, float* std,
+                    void* stream);
+/* out = x + noise * std[c] * factor */
+int nsm_perturb(const float* x, const float* noise, const float* std, int B, int C, int H,
+                int W, float factor, float* out, void* stream);
+
+/* ---- train-step tail (main.py:405,421: clip_grad_norm_ + AdamW) ----------- */
+int nsm_sumsq(const float* g, int64_t n, float* partial, float* out, void* stream);
+/* coef = inv_world * min(1, max_norm / (sqrt(sumsq)*inv_world + 1e-6)) */
+int nsm_clip_coef(const float* sumsq, float inv_world, float max_norm, float* coef, void* stream);
+int nsm_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
+                   float beta2, float eps, float weight_decay, int step, const float* gcoef,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSM_H_ */

@@ -1,0 +1,661 @@
+// MFMA implicit-GEMM convolutions for gfx950 (CDNA4), fp32 in / fp32 accumulate.
+//
+// One kernel template, three problems (NHWC activations, p = flattened pixel):
+//   fwd   : y[p][co]  = sum_{tap,ci} x[p+off(tap)][ci] * Wf[co][tap][ci]       M=pixels N=co   K=9*ci
+//   dgrad : dx[p][ci] = sum_{tap,co} dy[p+off(tap)][co] * Wd[ci][tap'][co]     (same kernel, flipped taps)
+//   wgrad : dW[co][tap,ci] = sum_p dy[p][co] * x[p+off(tap)][ci]                M=co N=tap*ci K=pixels (split-K)
+//
+// Matrix core: v_mfma_f32_32x32x2_f32 (exact f32 fmaf chain, 64 FLOP/clk/SIMD,
+// the fp32 peak of the chip). Each lane feeds ONE f32 of A and of B per MFMA:
+// lane l supplies A[m=l&31][kk=l>>5] and B[kk=l>>5][n=l&31]. The K order inside
+// a BK=32 slab is permuted so a lane's 16 k-values are contiguous in LDS:
+// (half h, group j, step q) -> physical k = 16h + 4j + q. Both operands use the
+// same permutation, so the contraction is unchanged (only fp rounding order).
+//
+// Operand LDS images (per pipeline stage):
+//   MK: [rows][BK+4]  k contiguous, read with ds_read_b128 (4 k-steps per read);
+//       the +4 pad makes the 16-lane groups of ds_read_b128 conflict-free.
+//   KM: [BK][rows+4]  rows contiguous, read with ds_read_b32 (one k-step);
+//       32 consecutive lanes -> 32 consecutive dwords: conflict-free.
+// Global -> LDS staging goes through registers (float4 per lane, coalesced
+// along channels), double-buffered: the next slab's global loads are issued
+// before the current slab's MFMAs, and written to the other LDS stage after.
+#include "nsm_common.h"
+
+namespace nsm {
+
+constexpr int BK = 32;
+constexpr int LDK = BK + 4;
+
+// ---------------------------------------------------------------------------
+// Operand loaders. R = rows of the operand tile (BM or BN), NT = threads.
+// ---------------------------------------------------------------------------
+struct ConvActP {  // im2col of NHWC activations; rows = pixels, K = (tap, channel)
+  const float* x;
+  int ld, cin, H, W, M, ksize;
+  FastDiv fdW, fdH;
+  const float* scale;  // prologue (1x1 fwd only): lrelu(v*scale+shift)*mask
+  const float* shift;
+  const float* mask;
+  int mask_ld;
+  float slope;
+};
+
+template <int R, int NT, bool PRO>
+struct ConvActLoader {  // MK image
+  static constexpr bool KM = false;
+  static constexpr int NPT = R * (BK / 4) / NT;
+  static constexpr int RSTEP = NT / (BK / 4);
+  static constexpr int LDS_FLOATS = R * LDK;
+  static_assert(NPT >= 1 && NPT * RSTEP == R, "loader shape");
+  int pix[NPT];
+  int py[NPT], px[NPT], pb[NPT];
+  int kc, row0, tap, c0;
+
+  __device__ void init(const ConvActP& p, int m0, int kbeg, int tid) {
+    kc = (tid & 7) * 4;
+    row0 = tid >> 3;
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      int q = m0 + row0 + i * RSTEP;
+      bool v = q < p.M;
+      q = v ? q : 0;
+      int t = (int)fdiv((uint32_t)q, p.fdW);
+      int xx = q - t * p.W;
+      int b = (int)fdiv((uint32_t)t, p.fdH);
+      int yy = t - b * p.H;
+      pix[i] = q;
+      px[i] = xx;
+      py[i] = v ? yy : -0x40000000;  // invalid rows never pass the bounds test
+      pb[i] = b;
+    }
+    tap = kbeg / p.cin;
+    c0 = kbeg - tap * p.cin;
+  }
+  __device__ void load(const ConvActP& p, f32x4* r) const {
+    int dy = 0, dx = 0;
+    if (p.ksize == 3) {
+      dy = tap / 3 - 1;
+      dx = tap - (tap / 3) * 3 - 1;
+    }
+    const int c = c0 + kc;
+    f32x4 sc, sh;
+    if constexpr (PRO) {
+      sc = *(const f32x4*)(p.scale + c);
+      sh = *(const f32x4*)(p.shift + c);
+    }
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      int yy = py[i] + dy, xx = px[i] + dx;
+      bool ok = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (ok) {
+        const float* a = p.x + (size_t)(pix[i] + dy * p.W + dx) * p.ld + c;
+        v = *(const f32x4*)a;
+        if constexpr (PRO) {
+          v.x = lrelu(v.x * sc.x + sh.x, p.slope);
+          v.y = lrelu(v.y * sc.y + sh.y, p.slope);
+          v.z = lrelu(v.z * sc.z + sh.z, p.slope);
+          v.w = lrelu(v.w * sc.w + sh.w, p.slope);
+          if (p.mask) {
+            f32x4 mk = *(const f32x4*)(p.mask + (size_t)pb[i] * p.mask_ld + c);
+            v *= mk;
+          }
+        }
+      }
+      r[i] = v;
+    }
+  }
+  __device__ void advance(const ConvActP& p) {
+    c0 += BK;
+    if (c0 >= p.cin) {
+      c0 = 0;
+      ++tap;
+    }
+  }
+  __device__ void store(float* S, const f32x4* r) const {
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) *(f32x4*)&S[(row0 + i * RSTEP) * LDK + kc] = r[i];
+  }
+};
+
+struct RowsKP {  // dense rows with contiguous K (packed weights); rows >= nrows are zero
+  const float* w;
+  int ldw, nrows;
+};
+
+template <int R, int NT>
+struct RowsKLoader {  // MK / NK image
+  static constexpr bool KM = false;
+  static constexpr int NPT = R * (BK / 4) / NT;
+  static constexpr int RSTEP = NT / (BK / 4);
+  static constexpr int LDS_FLOATS = R * LDK;
+  static_assert(NPT >= 1 && NPT * RSTEP == R, "loader shape");
+  int kc, row0, k0, n0;
+
+  __device__ void init(const RowsKP& p, int n0_, int kbeg, int tid) {
+    kc = (tid & 7) * 4;
+    row0 = tid >> 3;
+    k0 = kbeg;
+    n0 = n0_;
+  }
+  __device__ void load(const RowsKP& p, f32x4* r) const {
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      int n = n0 + row0 + i * RSTEP;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (n < p.nrows) v = *(const f32x4*)(p.w + (size_t)n * p.ldw + k0 + kc);
+      r[i] = v;
+    }
+  }
+  __device__ void advance(const RowsKP&) { k0 += BK; }
+  __device__ void store(float* S, const f32x4* r) const {
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) *(f32x4*)&S[(row0 + i * RSTEP) * LDK + kc] = r[i];
+  }
+};
+
+struct PixRowsP {  // rows = pixels (the GEMM K of wgrad), columns contiguous channels
+  const float* x;
+  int ld, ncols;   // channel stride, valid columns (cp)
+  int cin;         // channels per tap (N split into taps) — 0: no tap split
+  int H, W, M, ksize;
+  FastDiv fdW, fdH;
+  const float* scale;  // prologue (1x1 wgrad B operand: recomputed BN+LReLU+dropout)
+  const float* shift;
+  const float* mask;
+  int mask_ld;
+  float slope;
+};
+
+template <int R, int NT, bool SHIFT, bool PRO>
+struct PixRowsLoader {  // KM / KN image
+  static constexpr bool KM = true;
+  static constexpr int C4 = R / 4;
+  static constexpr int KSTEP = NT / C4;
+  static constexpr int NPT = BK / KSTEP;
+  static constexpr int LDS_FLOATS = BK * (R + 4);
+  static_assert(NPT >= 1 && NPT * KSTEP == BK && KSTEP * C4 == NT, "loader shape");
+  int col, c4o, krow0, k0, kend, dy, dx;
+  bool colok;
+  f32x4 sc, sh;
+
+  __device__ void init(const PixRowsP& p, int off, int kbeg, int kend_, int tid) {
+    int c4 = tid % C4;
+    c4o = c4 * 4;
+    krow0 = tid / C4;
+    int tap = 0, c = off;
+    if (p.cin > 0) {
+      tap = off / p.cin;
+      c = off - tap * p.cin;
+    }
+    col = c + c4 * 4;
+    colok = col < p.ncols && (p.cin == 0 || c + c4 * 4 < p.cin);
+    dy = dx = 0;
+    if (SHIFT && p.ksize == 3) {
+      dy = tap / 3 - 1;
+      dx = tap % 3 - 1;
+    }
+    k0 = kbeg;
+    kend = kend_;
+    if constexpr (PRO) {
+      sc = colok ? *(const f32x4*)(p.scale + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+      sh = colok ? *(const f32x4*)(p.shift + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __device__ void load(const PixRowsP& p, f32x4* r) const {
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      int q = k0 + krow0 + i * KSTEP;
+      bool ok = colok && q < kend;
+      int b = 0;
+      int src = q;
+      if (SHIFT || PRO) {
+        int qq = ok ? q : 0;
+        int t = (int)fdiv((uint32_t)qq, p.fdW);
+        int xx = qq - t * p.W;
+        b = (int)fdiv((uint32_t)t, p.fdH);
+        int yy = t - b * p.H;
+        if (SHIFT) {
+          ok = ok && (unsigned)(yy + dy) < (unsigned)p.H && (unsigned)(xx + dx) < (unsigned)p.W;
+          src = q + dy * p.W + dx;
+        }
+      }
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (ok) {
+        v = *(const f32x4*)(p.x + (size_t)src * p.ld + col);
+        if constexpr (PRO) {
+          v.x = lrelu(v.x * sc.x + sh.x, p.slope);
+          v.y = lrelu(v.y * sc.y + sh.y, p.slope);
+          v.z = lrelu(v.z * sc.z + sh.z, p.slope);
+          v.w = lrelu(v.w * sc.w + sh.w, p.slope);
+          if (p.mask) v *= *(const f32x4*)(p.mask + (size_t)b * p.mask_ld + col);
+        }
+      }
+      r[i] = v;
+    }
+  }
+  __device__ void advance(const PixRowsP&) { k0 += BK; }
+  __device__ void store(float* S, const f32x4* r) const {
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) *(f32x4*)&S[(krow0 + i * KSTEP) * (R + 4) + c4o] = r[i];
+  }
+};
+
+// ---------------------------------------------------------------------------
+// Fragment reads (see the K permutation in the file header).
+// ---------------------------------------------------------------------------
+template <bool KM, int R>
+__device__ __forceinline__ void read_frag(const float* S, int rb, int lane, int j, float* f) {
+  const int r = lane & 31, h = lane >> 5;
+  if constexpr (!KM) {
+    f32x4 v = *(const f32x4*)&S[(rb + r) * LDK + h * 16 + 4 * j];
+    f[0] = v.x;
+    f[1] = v.y;
+    f[2] = v.z;
+    f[3] = v.w;
+  } else {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) f[q] = S[(h * 16 + 4 * j + q) * (R + 4) + rb + r];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Epilogues. acc[tm][tn] register i holds C[row][col] with
+//   col = lane & 31, row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5).
+// ---------------------------------------------------------------------------
+struct EpiStoreP {
+  float* y;
+  int ldy;
+  const float* bias;
+};
+struct EpiStore {
+  using P = EpiStoreP;
+  template <int TM, int TN>
+  __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], int mb, int nb, int lane, int M,
+                               int N, int) {
+    const int col = lane & 31, h = lane >> 5;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      int n = nb + tn * 32 + col;
+      if (n >= N) continue;
+      float bv = e.bias ? e.bias[n] : 0.f;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          int m = mb + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (m < M) e.y[(size_t)m * e.ldy + n] = acc[tm][tn][i] + bv;
+        }
+      }
+    }
+  }
+};
+
+struct EpiSlabP {
+  float* ws;
+};
+struct EpiSlab {
+  using P = EpiSlabP;
+  template <int TM, int TN>
+  __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], int mb, int nb, int lane, int M,
+                               int N, int split) {
+    const int col = lane & 31, h = lane >> 5;
+    float* out = e.ws + (size_t)split * M * N;
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      int n = nb + tn * 32 + col;
+      if (n >= N) continue;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          int m = mb + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (m < M) out[(size_t)m * N + n] = acc[tm][tn][i];
+        }
+      }
+    }
+  }
+};
+
+// ---------------------------------------------------------------------------
+// The GEMM kernel: block tile BM x BN, WM x WN waves, each wave TM x TN 32x32
+// MFMA tiles; grid (ceil(M/BM), ceil(N/BN), splits); split z covers
+// K range [z*kchunk, min(K,(z+1)*kchunk)).
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, class AL, class BL, class EP, class AP, class BP>
+__global__ void __launch_bounds__(WM * WN * 64)
+    gemm_f32_kernel(AP ap, BP bp, typename EP::P ep, int M, int N, int K, int kchunk) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  constexpr int A_SZ = AL::LDS_FLOATS, B_SZ = BL::LDS_FLOATS, STAGE = A_SZ + B_SZ;
+  __shared__ __attribute__((aligned(16))) float lds[2 * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, split = blockIdx.z;
+  const int kbeg = split * kchunk;
+  const int kend = min(K, kbeg + kchunk);
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  AL a;
+  BL b;
+  if constexpr (AL::KM) a.init(ap, m0, kbeg, kend, tid);
+  else a.init(ap, m0, kbeg, tid);
+  if constexpr (BL::KM) b.init(bp, n0, kbeg, kend, tid);
+  else b.init(bp, n0, kbeg, tid);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  f32x4 ar[AL::NPT], br[BL::NPT];
+  if (nk > 0) {
+    a.load(ap, ar);
+    b.load(bp, br);
+    a.store(lds, ar);
+    b.store(lds + A_SZ, br);
+  }
+  __syncthreads();
+
+  const int arb = wm * TM * 32, brb = wn * TN * 32;
+  for (int it = 0; it < nk; ++it) {
+    const float* As = lds + (it & 1) * STAGE;
+    const float* Bs = As + A_SZ;
+    const bool more = it + 1 < nk;
+    if (more) {
+      a.advance(ap);
+      b.advance(bp);
+      a.load(ap, ar);
+      b.load(bp, br);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float fa[TM][4], fb[TN][4];
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm) read_frag<AL::KM, BM>(As, arb + tm * 32, lane, j, fa[tm]);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) read_frag<BL::KM, BN>(Bs, brb + tn * 32, lane, j, fb[tn]);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int tn = 0; tn < TN; ++tn)
+            acc[tm][tn] =
+                __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm][q], fb[tn][q], acc[tm][tn], 0, 0, 0);
+    }
+    if (more) {
+      float* An = lds + ((it + 1) & 1) * STAGE;
+      a.store(An, ar);
+      b.store(An + A_SZ, br);
+    }
+    __syncthreads();
+  }
+  EP::template apply<TM, TN>(ep, acc, m0 + arb, n0 + brb, lane, M, N, split);
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, bool PRO>
+static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const EpiStoreP& ep, int M, int N,
+                           int K, hipStream_t s) {
+  constexpr int NT = WM * WN * 64;
+  using AL = ConvActLoader<BM, NT, PRO>;
+  using BL = RowsKLoader<BN, NT>;
+  dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 1);
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiStore, ConvActP, RowsKP>), grid,
+                     dim3(NT), 0, s, ap, bp, ep, M, N, K, K);
+  NSM_LAUNCH_CHECK("conv_fwd");
+  return 0;
+}
+
+template <bool PRO>
+static int dispatch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const EpiStoreP& ep, int M,
+                             int N, int K, hipStream_t s) {
+  // Tile choice: 128x128 (2x2 waves of 64x64) wherever N allows; narrower N
+  // tiles for the 32/64-channel layers; BM=64 when the grid would not cover
+  // the 256 CUs twice.
+  long long mb128 = ceil_div(M, 128);
+  if (N >= 128) {
+    if (mb128 * ceil_div(N, 128) >= 512)
+      return launch_conv_fwd<128, 128, 2, 2, PRO>(ap, bp, ep, M, N, K, s);
+    return launch_conv_fwd<64, 128, 2, 2, PRO>(ap, bp, ep, M, N, K, s);
+  }
+  if (N >= 64) {
+    if (mb128 * ceil_div(N, 64) >= 512)
+      return launch_conv_fwd<128, 64, 2, 2, PRO>(ap, bp, ep, M, N, K, s);
+    return launch_conv_fwd<64, 64, 2, 2, PRO>(ap, bp, ep, M, N, K, s);
+  }
+  if (mb128 >= 512) return launch_conv_fwd<128, 32, 4, 1, PRO>(ap, bp, ep, M, N, K, s);
+  return launch_conv_fwd<64, 32, 2, 1, PRO>(ap, bp, ep, M, N, K, s);
+}
+
+template <int BM, int BN, int WM, int WN, bool SHIFT, bool PRO>
+static int launch_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& ep, int M, int N,
+                        int K, int kchunk, int splits, hipStream_t s) {
+  constexpr int NT = WM * WN * 64;
+  using AL = PixRowsLoader<BM, NT, false, false>;
+  using BL = PixRowsLoader<BN, NT, SHIFT, PRO>;
+  dim3 grid(ceil_div(M, BM), ceil_div(N, BN), splits);
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlab, PixRowsP, PixRowsP>), grid,
+                     dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk);
+  NSM_LAUNCH_CHECK("conv_wgrad");
+  return 0;
+}
+
+template <bool SHIFT, bool PRO>
+static int dispatch_wgrad(int BM, int BN, const PixRowsP& ap, const PixRowsP& bp,
+                          const EpiSlabP& ep, int M, int N, int K, int kchunk, int splits,
+                          hipStream_t s) {
+#define NSM_WG(bm, bn, wm, wn) \
+  if (BM == bm && BN == bn)    \
+    return launch_wgrad<bm, bn, wm, wn, SHIFT, PRO>(ap, bp, ep, M, N, K, kchunk, splits, s);
+  NSM_WG(128, 128, 2, 2)
+  NSM_WG(128, 64, 2, 2)
+  NSM_WG(128, 32, 4, 1)
+  NSM_WG(64, 128, 2, 2)
+  NSM_WG(64, 64, 2, 2)
+  NSM_WG(64, 32, 2, 1)
+  NSM_WG(32, 128, 1, 4)
+  NSM_WG(32, 64, 1, 2)
+  NSM_WG(32, 32, 1, 1)
+#undef NSM_WG
+  return fail(NSM_E_ARG, "wgrad: no tile %dx%d", BM, BN);
+}
+
+struct WgradPlan {
+  int BM, BN, splits, kchunk;
+  size_t ws_floats;
+};
+
+static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksize) {
+  WgradPlan pl;
+  const int M = cout_p, N = ksize * ksize * cin_p;
+  const long long K = (long long)B * H * W;
+  pl.BM = cout_p >= 128 ? 128 : (cout_p >= 64 ? 64 : 32);
+  pl.BN = cin_p >= 128 ? 128 : (cin_p >= 64 ? 64 : 32);
+  long long tiles = (long long)ceil_div(M, pl.BM) * ceil_div(N, pl.BN);
+  long long want = (2048 + tiles - 1) / tiles;
+  long long maxs = (K + 255) / 256;  // at least 256 pixels (8 K-slabs) per split
+  long long sp = want < maxs ? want : maxs;
+  if (sp < 1) sp = 1;
+  long long kc = (K + sp - 1) / sp;
+  kc = (kc + BK - 1) / BK * BK;
+  sp = (K + kc - 1) / kc;
+  pl.splits = (int)sp;
+  pl.kchunk = (int)kc;
+  pl.ws_floats = (size_t)sp * M * N;
+  return pl;
+}
+
+// dw[co][ci][tap] (real dims) = sum_s ws[s][co][tap*cin_p + ci]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, int cin_p,
+                                    int taps, int cin, int cout, float* __restrict__ dw) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  int total = cout * taps * cin;
+  if (idx >= total) return;
+  int ci = idx % cin;
+  int t = idx / cin;
+  int tap = t % taps;
+  int co = t / taps;
+  const float* src = ws + (size_t)co * N + tap * cin_p + ci;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += src[(size_t)k * M * N];
+  dw[((size_t)co * cin + ci) * taps + tap] = s;
+}
+
+__global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int taps,
+                                   int cout_p, int cin_p, int mode, float* __restrict__ out) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  int total = cout_p * cin_p * taps;
+  if (idx >= total) return;
+  if (mode == NSM_PACK_FWD) {  // out[co][tap][ci]
+    int ci = idx % cin_p;
+    int t = idx / cin_p;
+    int tap = t % taps;
+    int co = t / taps;
+    out[idx] = (co < cout && ci < cin) ? w[((size_t)co * cin + ci) * taps + tap] : 0.f;
+  } else {  // out[ci][tap'][co] = w[co][ci][taps-1-tap']
+    int co = idx % cout_p;
+    int t = idx / cout_p;
+    int tap = t % taps;
+    int ci = t / taps;
+    out[idx] =
+        (co < cout && ci < cin) ? w[((size_t)co * cin + ci) * taps + (taps - 1 - tap)] : 0.f;
+  }
+}
+
+__global__ void pad_vec_kernel(const float* __restrict__ v, int n, int n_p, float* __restrict__ out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n_p) out[i] = i < n ? v[i] : 0.f;
+}
+
+}  // namespace nsm
+
+using namespace nsm;
+
+extern "C" int nsm_pack_conv_weight(const float* w, int cout, int cin, int ksize, int cout_p,
+                                    int cin_p, int mode, float* out, void* stream) {
+  NSM_CHECK_ARG(w && out && cout > 0 && cin > 0 && cout_p >= cout && cin_p >= cin,
+                "pack_conv_weight: bad args");
+  NSM_CHECK_ARG(ksize == 1 || ksize == 3, "pack_conv_weight: ksize %d", ksize);
+  int taps = ksize * ksize;
+  int total = cout_p * cin_p * taps;
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(ceil_div(total, 256)), dim3(256), 0,
+                     as_stream(stream), w, cout, cin, taps, cout_p, cin_p, mode, out);
+  NSM_LAUNCH_CHECK("pack_conv_weight");
+  return 0;
+}
+
+extern "C" int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream) {
+  NSM_CHECK_ARG(v && out && n_p >= n, "pad_vec: bad args");
+  hipLaunchKernelGGL(pad_vec_kernel, dim3(ceil_div(n_p, 256)), dim3(256), 0, as_stream(stream), v,
+                     n, n_p, out);
+  NSM_LAUNCH_CHECK("pad_vec");
+  return 0;
+}
+
+extern "C" int nsm_conv_fwd(const float* x, int ldx, int B, int H, int W, int cin_p,
+                            const float* wpk, const float* bias, int cout_p, int ksize, float* y,
+                            int ldy, const float* pro_scale, const float* pro_shift,
+                            const float* pro_mask, float slope, void* stream) {
+  NSM_CHECK_ARG(x && wpk && y, "conv_fwd: null pointer");
+  NSM_CHECK_ARG(B > 0 && H > 0 && W > 0, "conv_fwd: bad shape");
+  NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0, "conv_fwd: channels must be multiples of 32");
+  NSM_CHECK_ARG(ldx >= cin_p && ldx % 4 == 0 && ldy >= cout_p, "conv_fwd: bad leading dims");
+  NSM_CHECK_ARG(ksize == 1 || ksize == 3, "conv_fwd: ksize %d", ksize);
+  NSM_CHECK_ARG(!pro_scale || (pro_shift && ksize == 1), "conv_fwd: prologue needs 1x1 + shift");
+  NSM_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)wpk % 16) == 0, "conv_fwd: 16B alignment");
+  long long Ml = (long long)B * H * W;
+  NSM_CHECK_ARG(Ml < (1ll << 30), "conv_fwd: too many pixels");
+  ConvActP ap;
+  ap.x = x;
+  ap.ld = ldx;
+  ap.cin = cin_p;
+  ap.H = H;
+  ap.W = W;
+  ap.M = (int)Ml;
+  ap.ksize = ksize;
+  ap.fdW = make_fastdiv(W);
+  ap.fdH = make_fastdiv(H);
+  ap.scale = pro_scale;
+  ap.shift = pro_shift;
+  ap.mask = pro_mask;
+  ap.mask_ld = cin_p;
+  ap.slope = slope;
+  int K = ksize * ksize * cin_p;
+  RowsKP bp{wpk, K, cout_p};
+  EpiStoreP ep{y, ldy, bias};
+  hipStream_t s = as_stream(stream);
+  if (pro_scale) return dispatch_conv_fwd<true>(ap, bp, ep, (int)Ml, cout_p, K, s);
+  return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s);
+}
+
+extern "C" size_t nsm_conv_wgrad_ws(int B, int H, int W, int cin_p, int cout_p, int ksize) {
+  return plan_wgrad(B, H, W, cin_p, cout_p, ksize).ws_floats;
+}
+
+extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx, int B, int H,
+                              int W, int cin_p, int cout_p, int ksize, const float* pro_scale,
+                              const float* pro_shift, const float* pro_mask, float slope,
+                              float* ws, size_t ws_floats, int cin, int cout, float* dw,
+                              void* stream) {
+  NSM_CHECK_ARG(dy && x && ws && dw, "conv_wgrad: null pointer");
+  NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0, "conv_wgrad: channels must be x32");
+  NSM_CHECK_ARG(ksize == 1 || ksize == 3, "conv_wgrad: ksize %d", ksize);
+  NSM_CHECK_ARG(lddy >= cout_p && ldx >= cin_p && lddy % 4 == 0 && ldx % 4 == 0,
+                "conv_wgrad: bad leading dims");
+  NSM_CHECK_ARG(!pro_scale || (pro_shift && ksize == 1), "conv_wgrad: prologue needs 1x1");
+  NSM_CHECK_ARG(cin <= cin_p && cout <= cout_p, "conv_wgrad: real dims exceed padded");
+  WgradPlan pl = plan_wgrad(B, H, W, cin_p, cout_p, ksize);
+  NSM_CHECK_ARG(cin_p % pl.BN == 0, "conv_wgrad: N tile straddles taps");
+  if (ws_floats < pl.ws_floats)
+    return fail(NSM_E_WS, "conv_wgrad: workspace %zu < %zu floats", ws_floats, pl.ws_floats);
+  const int M = cout_p, N = ksize * ksize * cin_p;
+  const long long Kl = (long long)B * H * W;
+  NSM_CHECK_ARG(Kl < (1ll << 30), "conv_wgrad: too many pixels");
+  PixRowsP ap{};
+  ap.x = dy;
+  ap.ld = lddy;
+  ap.ncols = cout_p;
+  ap.cin = 0;
+  ap.H = H;
+  ap.W = W;
+  ap.M = (int)Kl;
+  ap.ksize = 1;
+  ap.fdW = make_fastdiv(W);
+  ap.fdH = make_fastdiv(H);
+  PixRowsP bp = ap;
+  bp.x = x;
+  bp.ld = ldx;
+  bp.ncols = cin_p;
+  bp.cin = cin_p;
+  bp.ksize = ksize;
+  bp.scale = pro_scale;
+  bp.shift = pro_shift;
+  bp.mask = pro_mask;
+  bp.mask_ld = cin_p;
+  bp.slope = slope;
+  EpiSlabP ep{ws};
+  hipStream_t s = as_stream(stream);
+  int rc;
+  if (ksize == 3)
+    rc = dispatch_wgrad<true, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
+  else if (pro_scale)
+    rc = dispatch_wgrad<false, true>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
+  else
+    rc = dispatch_wgrad<false, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
+  if (rc) return rc;
+  int taps = ksize * ksize;
+  int total = cout * taps * cin;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, s, ws, pl.splits,
+                     M, N, cin_p, taps, cin, cout, dw);
+  NSM_LAUNCH_CHECK("conv_wgrad reduce");
+  return 0;
+}

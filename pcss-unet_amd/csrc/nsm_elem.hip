@@ -1,0 +1,1011 @@
+// Memory-bound kernels of the U-Net hot path on gfx950: BatchNorm statistics /
+// apply / backward, LeakyReLU, Dropout2d masks, AvgPool2d, bilinear resampling
+// (align_corners=True), pixel (un)shuffle at the model boundary, the conv10 +
+// pixel_shuffle + sigmoid head, the L1 / perturbation losses and the AdamW tail.
+//
+// All activations are NHWC fp32 with a padded channel count C (multiple of 4,
+// 32 in practice), so every lane moves float4 (16 B) and a wave moves 1 KiB
+// per instruction. Cross-block reductions are deterministic: each block writes
+// a partial row, a tiny finalize kernel merges rows in a fixed order (double).
+#include "nsm_common.h"
+
+namespace nsm {
+
+// ---------------------------------------------------------------------------
+// Column reductions over an [M][C] NHWC matrix: block = 256 threads laid out
+// as rl row-lanes x cl float4 channel-lanes; grid = (gx channel groups, nchunk).
+// ---------------------------------------------------------------------------
+static inline int gcd_i(int a, int b) {
+  while (b) {
+    int t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+struct ColRed {
+  int cl, rl, gx, nchunk, rpc;
+};
+static ColRed colred_plan(int M, int C) {
+  ColRed r;
+  r.cl = gcd_i(C / 4, 64);
+  r.rl = 256 / r.cl;
+  r.gx = (C / 4) / r.cl;
+  long long want = (M + 63) / 64;
+  long long cap = 2048 / r.gx;
+  if (cap < 1) cap = 1;
+  r.nchunk = (int)(want < cap ? want : cap);
+  if (r.nchunk < 1) r.nchunk = 1;
+  r.rpc = ceil_div(M, r.nchunk);
+  return r;
+}
+
+// reduce red[rl][cl] (f32x4) over rl; result valid in red[0][tc] for all tc.
+__device__ __forceinline__ void col_tree_reduce(f32x4* red, int cl, int rl, int tid) {
+  for (int s = rl / 2; s > 0; s >>= 1) {
+    __syncthreads();
+    int tr = tid / cl;
+    if (tr < s) red[tid] += red[tid + s * cl];
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) bn_stats_kernel(const float* __restrict__ y, int ld, int M,
+                                                       int C, int cl, int rl, int rpc,
+                                                       float* __restrict__ partial) {
+  __shared__ f32x4 red[256];
+  const int tid = threadIdx.x, tc = tid % cl, tr = tid / cl;
+  const int c = (blockIdx.x * cl + tc) * 4;
+  const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  for (int r = r0 + tr; r < r1; r += rl) s += *(const f32x4*)(y + (size_t)r * ld + c);
+  red[tid] = s;
+  col_tree_reduce(red, cl, rl, tid);
+  const float n = (float)max(r1 - r0, 1);
+  const f32x4 sum = red[tc];
+  const f32x4 mean = sum / n;
+  __syncthreads();
+  f32x4 s2 = {0.f, 0.f, 0.f, 0.f};
+  for (int r = r0 + tr; r < r1; r += rl) {
+    f32x4 d = *(const f32x4*)(y + (size_t)r * ld + c) - mean;
+    s2 += d * d;
+  }
+  red[tid] = s2;
+  col_tree_reduce(red, cl, rl, tid);
+  if (tr == 0) {
+    float* pr = partial + (size_t)blockIdx.y * 2 * C;
+    *(f32x4*)(pr + c) = sum;
+    *(f32x4*)(pr + C + c) = red[tc];
+  }
+}
+
+__global__ void bn_finalize_train_kernel(const float* __restrict__ partial, int nchunk, int rpc,
+                                         int M, int C, int c_real, const float* __restrict__ gamma,
+                                         const float* __restrict__ beta, float* run_mean,
+                                         float* run_var, int64_t* num_batches, float momentum,
+                                         float eps, int n_updates, float* mean_o, float* invstd_o,
+                                         float* scale_o, float* shift_o) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && num_batches) *num_batches += n_updates;
+  if (c >= C) return;
+  double tot = 0.0;
+  for (int k = 0; k < nchunk; ++k) tot += partial[(size_t)k * 2 * C + c];
+  const double mean = tot / M;
+  double m2 = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    int r0 = k * rpc, r1 = min(M, r0 + rpc);
+    int nk = r1 - r0;
+    if (nk <= 0) continue;
+    double mk = partial[(size_t)k * 2 * C + c] / nk;
+    double d = mk - mean;
+    m2 += partial[(size_t)k * 2 * C + C + c] + nk * d * d;
+  }
+  const float var_b = (float)(m2 / M);
+  const float var_u = M > 1 ? (float)(m2 / (M - 1)) : var_b;
+  const float mf = (float)mean;
+  const float inv = 1.0f / sqrtf(var_b + eps);
+  const float sc = gamma[c] * inv;
+  mean_o[c] = mf;
+  invstd_o[c] = inv;
+  scale_o[c] = sc;
+  shift_o[c] = beta[c] - mf * sc;
+  if (c < c_real && run_mean) {
+    float rm = run_mean[c], rv = run_var[c];
+    for (int u = 0; u < n_updates; ++u) {
+      rm = momentum * mf + (1.f - momentum) * rm;
+      rv = momentum * var_u + (1.f - momentum) * rv;
+    }
+    run_mean[c] = rm;
+    run_var[c] = rv;
+  }
+}
+
+__global__ void bn_finalize_eval_kernel(const float* __restrict__ rm, const float* __restrict__ rv,
+                                        const float* __restrict__ gamma,
+                                        const float* __restrict__ beta, int C, int c_real, float eps,
+                                        float* mean_o, float* invstd_o, float* scale_o,
+                                        float* shift_o) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float m = c < c_real ? rm[c] : 0.f;
+  float v = c < c_real ? rv[c] : 1.f;
+  float inv = 1.0f / sqrtf(v + eps);
+  float sc = gamma[c] * inv;
+  mean_o[c] = m;
+  invstd_o[c] = inv;
+  scale_o[c] = sc;
+  shift_o[c] = beta[c] - m * sc;
+}
+
+__global__ void bn_act_kernel(const float* __restrict__ y, int ldy, int M, int C4,
+                              const float* __restrict__ scale, const float* __restrict__ shift,
+                              float slope, const float* __restrict__ res, int ldres,
+                              float* __restrict__ out, int ldo) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)M * C4;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int p = (int)(i / C4), c = (int)(i - (long long)p * C4) * 4;
+    f32x4 v = *(const f32x4*)(y + (size_t)p * ldy + c);
+    f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
+    f32x4 o;
+    o.x = lrelu(v.x * sc.x + sh.x, slope);
+    o.y = lrelu(v.y * sc.y + sh.y, slope);
+    o.z = lrelu(v.z * sc.z + sh.z, slope);
+    o.w = lrelu(v.w * sc.w + sh.w, slope);
+    if (res) o += *(const f32x4*)(res + (size_t)p * ldres + c);
+    *(f32x4*)(out + (size_t)p * ldo + c) = o;
+  }
+}
+
+// dz = g * mask[b][c] * lrelu'(y*scale+shift)
+__device__ __forceinline__ f32x4 bn_dz(const f32x4 g, const f32x4 v, const f32x4 sc,
+                                       const f32x4 sh, float slope, const float* mask, int b,
+                                       int C, int c) {
+  f32x4 d;
+  d.x = g.x * lrelu_grad(v.x * sc.x + sh.x, slope);
+  d.y = g.y * lrelu_grad(v.y * sc.y + sh.y, slope);
+  d.z = g.z * lrelu_grad(v.z * sc.z + sh.z, slope);
+  d.w = g.w * lrelu_grad(v.w * sc.w + sh.w, slope);
+  // Dropout2d sits AFTER the LeakyReLU (Unetmodel.py:23-24): d(out)/d(z) =
+  // mask * lrelu'(z); multiplication order does not matter for the value.
+  if (mask) d *= *(const f32x4*)(mask + (size_t)b * C + c);
+  return d;
+}
+
+__global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
+    const float* __restrict__ g, int ldg, const float* __restrict__ y, int ldy, int M, int C,
+    FastDiv fdHW, const float* __restrict__ scale, const float* __restrict__ shift, float slope,
+    const float* __restrict__ mask, const float* __restrict__ mean,
+    const float* __restrict__ invstd, int cl, int rl, int rpc, float* __restrict__ partial) {
+  __shared__ f32x4 red[256];
+  const int tid = threadIdx.x, tc = tid % cl, tr = tid / cl;
+  const int c = (blockIdx.x * cl + tc) * 4;
+  const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
+  const f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
+  const f32x4 mu = *(const f32x4*)(mean + c), is = *(const f32x4*)(invstd + c);
+  f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  for (int r = r0 + tr; r < r1; r += rl) {
+    f32x4 v = *(const f32x4*)(y + (size_t)r * ldy + c);
+    f32x4 gg = *(const f32x4*)(g + (size_t)r * ldg + c);
+    int b = mask ? (int)fdiv((uint32_t)r, fdHW) : 0;
+    f32x4 dz = bn_dz(gg, v, sc, sh, slope, mask, b, C, c);
+    s1 += dz;
+    s2 += dz * ((v - mu) * is);
+  }
+  red[tid] = s1;
+  col_tree_reduce(red, cl, rl, tid);
+  f32x4 t1 = red[tc];
+  __syncthreads();
+  red[tid] = s2;
+  col_tree_reduce(red, cl, rl, tid);
+  if (tr == 0) {
+    float* pr = partial + (size_t)blockIdx.y * 2 * C;
+    *(f32x4*)(pr + c) = t1;
+    *(f32x4*)(pr + C + c) = red[tc];
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nchunk, int M, int C,
+                                       int c_real, const float* __restrict__ gamma,
+                                       const float* __restrict__ invstd, float* dgamma,
+                                       float* dbeta, float* dbias_prev, float* coef) {
+  int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double S1 = 0.0, S2 = 0.0;
+  for (int k = 0; k < nchunk; ++k) {
+    S1 += partial[(size_t)k * 2 * C + c];
+    S2 += partial[(size_t)k * 2 * C + C + c];
+  }
+  const float gm = gamma[c], is = invstd[c];
+  const double mdz = S1 / M, mdzx = S2 / M;
+  const float k1 = gm * is;
+  const float k2 = (float)(-(double)gm * is * is * mdzx);
+  const float k3 = (float)(-(double)k1 * mdz);
+  coef[c] = k1;
+  coef[C + c] = k2;
+  coef[2 * C + c] = k3;
+  if (c < c_real) {
+    if (dgamma) dgamma[c] = (float)S2;
+    if (dbeta) dbeta[c] = (float)S1;
+    // sum_p dy = k1*S1 + k2*sum(y-mean) + k3*M == 0 analytically (pre-BN bias)
+    if (dbias_prev) dbias_prev[c] = (float)((double)k1 * S1 + (double)k3 * M);
+  }
+}
+
+__global__ void bn_bwd_apply_kernel(const float* __restrict__ g, int ldg,
+                                    const float* __restrict__ y, int ldy, int M, int C,
+                                    FastDiv fdHW, const float* __restrict__ scale,
+                                    const float* __restrict__ shift, float slope,
+                                    const float* __restrict__ mask, const float* __restrict__ mean,
+                                    const float* __restrict__ coef, float* __restrict__ dy,
+                                    int lddy) {
+  const int C4 = C / 4;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  long long total = (long long)M * C4;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int p = (int)(i / C4), c = (int)(i - (long long)p * C4) * 4;
+    f32x4 v = *(const f32x4*)(y + (size_t)p * ldy + c);
+    f32x4 gg = *(const f32x4*)(g + (size_t)p * ldg + c);
+    f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
+    int b = mask ? (int)fdiv((uint32_t)p, fdHW) : 0;
+    f32x4 dz = bn_dz(gg, v, sc, sh, slope, mask, b, C, c);
+    f32x4 k1 = *(const f32x4*)(coef + c), k2 = *(const f32x4*)(coef + C + c),
+          k3 = *(const f32x4*)(coef + 2 * C + c), mu = *(const f32x4*)(mean + c);
+    *(f32x4*)(dy + (size_t)p * lddy + c) = k1 * dz + k2 * (v - mu) + k3;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// AvgPool2d(2), floor mode
+// ---------------------------------------------------------------------------
+__global__ void avgpool2_fwd_kernel(const float* __restrict__ x, int B, int H, int W, int C4,
+                                    float* __restrict__ y) {
+  const int Ho = H / 2, Wo = W / 2;
+  long long total = (long long)B * Ho * Wo * C4;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C4);
+    long long t = i / C4;
+    int ox = (int)(t % Wo);
+    t /= Wo;
+    int oy = (int)(t % Ho);
+    int b = (int)(t / Ho);
+    const float* base = x + (((size_t)b * H + 2 * oy) * W + 2 * ox) * (C4 * 4) + c * 4;
+    size_t rs = (size_t)W * C4 * 4, cs = (size_t)C4 * 4;
+    f32x4 s = *(const f32x4*)base;
+    s += *(const f32x4*)(base + cs);
+    s += *(const f32x4*)(base + rs);
+    s += *(const f32x4*)(base + rs + cs);
+    *(f32x4*)(y + (size_t)i * 4) = s * 0.25f;
+  }
+}
+
+__global__ void avgpool2_bwd_add_kernel(const float* __restrict__ dy, int B, int H, int W, int C4,
+                                        const float* __restrict__ skip, float* __restrict__ dx) {
+  const int Ho = H / 2, Wo = W / 2;
+  long long total = (long long)B * H * W * C4;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C4);
+    long long t = i / C4;
+    int xx = (int)(t % W);
+    t /= W;
+    int yy = (int)(t % H);
+    int b = (int)(t / H);
+    f32x4 v = skip ? *(const f32x4*)(skip + (size_t)i * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    int oy = yy >> 1, ox = xx >> 1;
+    if (oy < Ho && ox < Wo)
+      v += *(const f32x4*)(dy + ((((size_t)b * Ho + oy) * Wo + ox) * C4 + c) * 4) * 0.25f;
+    *(f32x4*)(dx + (size_t)i * 4) = v;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Bilinear resize, align_corners=True (ATen upsample_bilinear2d semantics:
+// scale=(in-1)/(out-1) in fp32, src=scale*dst, i0=floor, i1=i0+(i0<in-1),
+// l1=src-i0, l0=1-l1).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void lin_idx(float scale, int dst, int in, int& i0, int& i1, float& l0,
+                                        float& l1) {
+  // __fmul_rn: keep src rounded to fp32 as ATen does; letting the compiler
+  // contract scale*dst - i0 into one FMA shifts lambda by up to ~1e-5.
+  float src = __fmul_rn(scale, (float)dst);
+  i0 = min((int)src, in - 1);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+}
+
+static inline float ac_scale(int in, int out) {
+  return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+}
+
+template <bool VEC>
+__global__ void resize_fwd_kernel(const float* __restrict__ x, int B, int Hi, int Wi, int C,
+                                  float* __restrict__ y, int Ho, int Wo, float sh, float sw) {
+  const int CV = VEC ? C / 4 : C;
+  long long total = (long long)B * Ho * Wo * CV;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % CV);
+    long long t = i / CV;
+    int ox = (int)(t % Wo);
+    t /= Wo;
+    int oy = (int)(t % Ho);
+    int b = (int)(t / Ho);
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    lin_idx(sh, oy, Hi, y0, y1, ly0, ly1);
+    lin_idx(sw, ox, Wi, x0, x1, lx0, lx1);
+    const size_t rb = (size_t)b * Hi;
+    if constexpr (VEC) {
+      const float* p00 = x + ((rb + y0) * Wi + x0) * C + c * 4;
+      const float* p01 = x + ((rb + y0) * Wi + x1) * C + c * 4;
+      const float* p10 = x + ((rb + y1) * Wi + x0) * C + c * 4;
+      const float* p11 = x + ((rb + y1) * Wi + x1) * C + c * 4;
+      f32x4 v = ly0 * (lx0 * *(const f32x4*)p00 + lx1 * *(const f32x4*)p01) +
+                ly1 * (lx0 * *(const f32x4*)p10 + lx1 * *(const f32x4*)p11);
+      *(f32x4*)(y + (size_t)i * 4) = v;
+    } else {
+      float v = ly0 * (lx0 * x[((rb + y0) * Wi + x0) * C + c] + lx1 * x[((rb + y0) * Wi + x1) * C + c]) +
+                ly1 * (lx0 * x[((rb + y1) * Wi + x0) * C + c] + lx1 * x[((rb + y1) * Wi + x1) * C + c]);
+      y[i] = v;
+    }
+  }
+}
+
+// weight of output index `o` on input index `i` (0 if none)
+__device__ __forceinline__ float lin_w(float scale, int o, int in, int i) {
+  int i0, i1;
+  float l0, l1;
+  lin_idx(scale, o, in, i0, i1, l0, l1);
+  return (i0 == i ? l0 : 0.f) + (i1 == i ? l1 : 0.f);
+}
+
+__device__ __forceinline__ void cand_range(float scale, int i, int out, int& lo, int& hi) {
+  if (scale <= 0.f) {
+    lo = 0;
+    hi = out - 1;
+    return;
+  }
+  lo = max(0, (int)floorf((float)(i - 1) / scale) - 1);
+  hi = min(out - 1, (int)ceilf((float)(i + 1) / scale) + 1);
+}
+
+template <bool VEC>
+__global__ void resize_bwd_kernel(const float* __restrict__ dy, int B, int Hi, int Wi, int C,
+                                  float* __restrict__ dx, int Ho, int Wo, float sh, float sw) {
+  const int CV = VEC ? C / 4 : C;
+  long long total = (long long)B * Hi * Wi * CV;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % CV);
+    long long t = i / CV;
+    int ix = (int)(t % Wi);
+    t /= Wi;
+    int iy = (int)(t % Hi);
+    int b = (int)(t / Hi);
+    int ylo, yhi, xlo, xhi;
+    cand_range(sh, iy, Ho, ylo, yhi);
+    cand_range(sw, ix, Wo, xlo, xhi);
+    float wxs[16];
+    int nx = 0, xs0 = xlo;
+    for (int ox = xlo; ox <= xhi && nx < 16; ++ox) wxs[nx++] = lin_w(sw, ox, Wi, ix);
+    f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
+    float acc = 0.f;
+    for (int oy = ylo; oy <= yhi; ++oy) {
+      float wy = lin_w(sh, oy, Hi, iy);
+      if (wy == 0.f) continue;
+      const float* row = dy + ((size_t)b * Ho + oy) * Wo * C;
+      for (int k = 0; k < nx; ++k) {
+        float w = wxs[k];
+        if (w == 0.f) continue;
+        if constexpr (VEC)
+          acc4 += (wy * w) * *(const f32x4*)(row + (size_t)(xs0 + k) * C + c * 4);
+        else
+          acc += (wy * w) * row[(size_t)(xs0 + k) * C + c];
+      }
+    }
+    if constexpr (VEC)
+      *(f32x4*)(dx + (size_t)i * 4) = acc4;
+    else
+      dx[i] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Model boundary: pixel_unshuffle(2) + NCHW->NHWC (+ zero channel pad), and its
+// inverse for the input gradient.
+// ---------------------------------------------------------------------------
+__global__ void input_prep_kernel(const float* __restrict__ x, int B, int C, int H, int W,
+                                  float* __restrict__ out, int cp) {
+  const int Rh = H / 2, Rw = W / 2;
+  long long total = (long long)B * Rh * Rw * cp;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int ch = (int)(i % cp);
+    long long t = i / cp;
+    int rx = (int)(t % Rw);
+    t /= Rw;
+    int ry = (int)(t % Rh);
+    int b = (int)(t / Rh);
+    float v = 0.f;
+    if (ch < 4 * C) {
+      int c = ch >> 2, di = (ch >> 1) & 1, dj = ch & 1;
+      v = x[(((size_t)b * C + c) * H + 2 * ry + di) * W + 2 * rx + dj];
+    }
+    out[i] = v;
+  }
+}
+
+__global__ void input_grad_kernel(const float* __restrict__ dX, int B, int C, int H, int W, int cp,
+                                  float* __restrict__ dx) {
+  const int Rh = H / 2, Rw = W / 2;
+  long long total = (long long)B * C * H * W;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int xx = (int)(i % W);
+    long long t = i / W;
+    int yy = (int)(t % H);
+    t /= H;
+    int c = (int)(t % C);
+    int b = (int)(t / C);
+    int ch = 4 * c + 2 * (yy & 1) + (xx & 1);
+    dx[i] = dX[(((size_t)b * Rh + (yy >> 1)) * Rw + (xx >> 1)) * cp + ch];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Head: conv10 (1x1, 16->4, bias) -> pixel_shuffle(2) -> sigmoid
+// ---------------------------------------------------------------------------
+__global__ void head_fwd_kernel(const float* __restrict__ z, int ldz, int B, int Rh, int Rw,
+                                const float* __restrict__ w10, const float* __restrict__ b10,
+                                float* __restrict__ out) {
+  __shared__ float w[68];
+  if (threadIdx.x < 64) w[threadIdx.x] = w10[threadIdx.x];
+  if (threadIdx.x < 4) w[64 + threadIdx.x] = b10[threadIdx.x];
+  __syncthreads();
+  long long npix = (long long)B * Rh * Rw;
+  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < npix;
+       p += (long long)gridDim.x * blockDim.x) {
+    float zz[16];
+    const float* zr = z + (size_t)p * ldz;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v = *(const f32x4*)(zr + 4 * q);
+      zz[4 * q] = v.x;
+      zz[4 * q + 1] = v.y;
+      zz[4 * q + 2] = v.z;
+      zz[4 * q + 3] = v.w;
+    }
+    int rx = (int)(p % Rw);
+    long long t = p / Rw;
+    int ry = (int)(t % Rh);
+    int b = (int)(t / Rh);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float acc = 0.f;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) acc += w[j * 16 + c] * zz[c];
+      acc += w[64 + j];
+      float s = 1.f / (1.f + expf(-acc));
+      int di = j >> 1, dj = j & 1;
+      out[((size_t)b * 2 * Rh + 2 * ry + di) * (2 * Rw) + 2 * rx + dj] = s;
+    }
+  }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__global__ void __launch_bounds__(256) head_bwd_kernel(
+    const float* __restrict__ gout, const float* __restrict__ out, const float* __restrict__ z,
+    int ldz, int B, int Rh, int Rw, const float* __restrict__ w10, float* __restrict__ dz,
+    float* __restrict__ partial) {
+  __shared__ float w[64];
+  __shared__ float red[4][68];
+  if (threadIdx.x < 64) w[threadIdx.x] = w10[threadIdx.x];
+  __syncthreads();
+  float accw[68];
+#pragma unroll
+  for (int k = 0; k < 68; ++k) accw[k] = 0.f;
+  long long npix = (long long)B * Rh * Rw;
+  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < npix;
+       p += (long long)gridDim.x * blockDim.x) {
+    int rx = (int)(p % Rw);
+    long long t = p / Rw;
+    int ry = (int)(t % Rh);
+    int b = (int)(t / Rh);
+    float d[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int di = j >> 1, dj = j & 1;
+      size_t o = ((size_t)b * 2 * Rh + 2 * ry + di) * (2 * Rw) + 2 * rx + dj;
+      float ov = out[o];
+      d[j] = gout[o] * (1.f - ov) * ov;  // ATen sigmoid_backward
+    }
+    const float* zr = z + (size_t)p * ldz;
+    float* dzr = dz + (size_t)p * ldz;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      f32x4 v = *(const f32x4*)(zr + 4 * q);
+      float zv[4] = {v.x, v.y, v.z, v.w};
+      f32x4 g;
+      float gv[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        int c = 4 * q + e;
+        gv[e] = d[0] * w[c] + d[1] * w[16 + c] + d[2] * w[32 + c] + d[3] * w[48 + c];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) accw[j * 16 + c] += d[j] * zv[e];
+      }
+      g.x = gv[0];
+      g.y = gv[1];
+      g.z = gv[2];
+      g.w = gv[3];
+      *(f32x4*)(dzr + 4 * q) = g;
+    }
+    for (int c = 16; c < ldz; c += 4) *(f32x4*)(dzr + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) accw[64 + j] += d[j];
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < 68; ++k) {
+    float s = wave_sum(accw[k]);
+    if (lane == 0) red[wv][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < 68) {
+    float s = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+    partial[(size_t)blockIdx.x * 68 + threadIdx.x] = s;
+  }
+}
+
+// out[j] = sum_b partial[b][j]  (j < width) -> dw10 [64] then db10 [4]
+__global__ void head_reduce_kernel(const float* __restrict__ partial, int nblk, float* dw10,
+                                   float* db10) {
+  int j = threadIdx.x;
+  if (j >= 68) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += partial[(size_t)b * 68 + j];
+  if (j < 64)
+    dw10[j] = (float)s;
+  else
+    db10[j - 64] = (float)s;
+}
+
+// ---------------------------------------------------------------------------
+// Losses
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float block_sum256(float v, float* sh) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) sh[wv] = v;
+  __syncthreads();
+  float r = 0.f;
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) r += sh[k];
+  }
+  return r;
+}
+
+__global__ void __launch_bounds__(256) l1_partial_kernel(const float* __restrict__ o,
+                                                         const float* __restrict__ t, int64_t n,
+                                                         float* __restrict__ partial) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    s += fabsf(o[i] - t[i]);
+  float r = block_sum256(s, sh);
+  if (threadIdx.x == 0) partial[blockIdx.x] = r;
+}
+
+__global__ void finalize_mean_kernel(const float* __restrict__ partial, int nblk, double scale,
+                                     float* out) {
+  // one wave; fixed-order double accumulation
+  __shared__ double sh[64];
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += 64) s += partial[b];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+    for (int k = 0; k < 64; ++k) tot += sh[k];
+    out[0] = (float)(tot * scale);
+  }
+}
+
+__global__ void l1_bwd_kernel(const float* __restrict__ o, const float* __restrict__ t, int64_t n,
+                              float alpha, const float* __restrict__ gscale, float* grad,
+                              int accumulate) {
+  const float gs = gscale ? gscale[0] : 1.f;
+  const float mag = (alpha * gs) / (float)n;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float d = o[i] - t[i];
+    float s = d > 0.f ? mag : (d < 0.f ? -mag : 0.f);
+    grad[i] = accumulate ? grad[i] + s : s;
+  }
+}
+
+__global__ void __launch_bounds__(1024) channel_std_kernel(const float* __restrict__ x, int B, int C,
+                                                           int HW, float* __restrict__ std_o) {
+  // one block per channel, double accumulation, two passes (torch.std, unbiased)
+  __shared__ double sh[16];
+  const int c = blockIdx.x;
+  const long long n = (long long)B * HW;
+  double s = 0.0;
+  for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+    long long b = i / HW, r = i - b * HW;
+    s += x[((size_t)b * C + c) * HW + r];
+  }
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  double tot = 0.0;
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) tot += sh[k];
+  const double mean = tot / n;
+  __syncthreads();
+  double s2 = 0.0;
+  for (long long i = threadIdx.x; i < n; i += blockDim.x) {
+    long long b = i / HW, r = i - b * HW;
+    double d = x[((size_t)b * C + c) * HW + r] - mean;
+    s2 += d * d;
+  }
+  for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s2;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t2 = 0.0;
+    for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t2 += sh[k];
+    std_o[c] = (float)sqrt(t2 / (double)(n > 1 ? n - 1 : 1));
+  }
+}
+
+__global__ void perturb_kernel(const float* __restrict__ x, const float* __restrict__ noise,
+                               const float* __restrict__ stdv, int C, int HW, long long total,
+                               float factor, float* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)((i / HW) % C);
+    out[i] = x[i] + (noise[i] * stdv[c]) * factor;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Train-step tail: global grad norm, clip coefficient, AdamW (torch semantics)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) sumsq_partial_kernel(const float* __restrict__ g, int64_t n,
+                                                            float* __restrict__ partial) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float v = g[i];
+    s += v * v;
+  }
+  float r = block_sum256(s, sh);
+  if (threadIdx.x == 0) partial[blockIdx.x] = r;
+}
+
+__global__ void clip_coef_kernel(const float* __restrict__ sumsq, float inv_world, float max_norm,
+                                 float* coef) {
+  float norm = sqrtf(sumsq[0]) * inv_world;
+  float c = max_norm / (norm + 1e-6f);
+  coef[0] = inv_world * fminf(c, 1.f);
+}
+
+__global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                             float* __restrict__ m, float* __restrict__ v, int64_t n, float decay,
+                             float beta1, float beta2, float eps, float step_size,
+                             float bc2_sqrt, const float* __restrict__ gcoef) {
+  const float gc = gcoef ? gcoef[0] : 1.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * gc;
+    float pi = p[i] * decay;
+    float mi = m[i];
+    mi = mi + (1.f - beta1) * (gi - mi);
+    float vi = v[i] * beta2 + (1.f - beta2) * gi * gi;
+    float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+
+static inline int grid_for(long long work, int per_block = 256, int cap = 8192) {
+  long long g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace nsm
+
+using namespace nsm;
+
+// ============================== C ABI ======================================
+extern "C" int nsm_reduce_chunks(int M, int C) {
+  if (M <= 0 || C <= 0 || C % 4) return 0;
+  return colred_plan(M, C).nchunk;
+}
+
+extern "C" int nsm_bn_stats(const float* y, int ld, int M, int C, float* partial, int nchunk,
+                            void* stream) {
+  NSM_CHECK_ARG(y && partial && M > 0 && C % 4 == 0 && ld % 4 == 0, "bn_stats: bad args");
+  ColRed r = colred_plan(M, C);
+  NSM_CHECK_ARG(nchunk == r.nchunk, "bn_stats: nchunk %d != %d", nchunk, r.nchunk);
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(r.gx, r.nchunk), dim3(256), 0, as_stream(stream), y, ld,
+                     M, C, r.cl, r.rl, r.rpc, partial);
+  NSM_LAUNCH_CHECK("bn_stats");
+  return 0;
+}
+
+extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int M, int C, int c_real,
+                                     const float* gamma, const float* beta, float* run_mean,
+                                     float* run_var, int64_t* num_batches, float momentum,
+                                     float eps, int n_updates, float* mean, float* invstd,
+                                     float* scale, float* shift, void* stream) {
+  NSM_CHECK_ARG(partial && gamma && beta && mean && invstd && scale && shift, "bn_finalize: null");
+  NSM_CHECK_ARG(M > 1, "bn_finalize: Expected more than 1 value per channel when training");
+  ColRed r = colred_plan(M, C);
+  NSM_CHECK_ARG(nchunk == r.nchunk, "bn_finalize: nchunk mismatch");
+  hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(ceil_div(C, 256)), dim3(256), 0,
+                     as_stream(stream), partial, nchunk, r.rpc, M, C, c_real, gamma, beta, run_mean,
+                     run_var, num_batches, momentum, eps, n_updates, mean, invstd, scale, shift);
+  NSM_LAUNCH_CHECK("bn_finalize_train");
+  return 0;
+}
+
+extern "C" int nsm_bn_finalize_eval(const float* run_mean, const float* run_var,
+                                    const float* gamma, const float* beta, int C, int c_real,
+                                    float eps, float* mean, float* invstd, float* scale,
+                                    float* shift, void* stream) {
+  NSM_CHECK_ARG(run_mean && run_var && gamma && beta && scale && shift, "bn_finalize_eval: null");
+  hipLaunchKernelGGL(bn_finalize_eval_kernel, dim3(ceil_div(C, 256)), dim3(256), 0,
+                     as_stream(stream), run_mean, run_var, gamma, beta, C, c_real, eps, mean, invstd,
+                     scale, shift);
+  NSM_LAUNCH_CHECK("bn_finalize_eval");
+  return 0;
+}
+
+extern "C" int nsm_bn_act(const float* y, int ldy, int M, int C, const float* scale,
+                          const float* shift, float slope, const float* res, int ldres, float* out,
+                          int ldo, void* stream) {
+  NSM_CHECK_ARG(y && scale && shift && out && C % 4 == 0, "bn_act: bad args");
+  long long work = (long long)M * (C / 4);
+  hipLaunchKernelGGL(bn_act_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), y, ldy,
+                     M, C / 4, scale, shift, slope, res, ldres, out, ldo);
+  NSM_LAUNCH_CHECK("bn_act");
+  return 0;
+}
+
+extern "C" int nsm_bn_bwd_reduce(const float* g, int ldg, const float* y, int ldy, int M, int C,
+                                 int HW, const float* scale, const float* shift, float slope,
+                                 const float* mask, const float* mean, const float* invstd,
+                                 float* partial, int nchunk, void* stream) {
+  NSM_CHECK_ARG(g && y && scale && shift && mean && invstd && partial && C % 4 == 0,
+                "bn_bwd_reduce: bad args");
+  ColRed r = colred_plan(M, C);
+  NSM_CHECK_ARG(nchunk == r.nchunk, "bn_bwd_reduce: nchunk mismatch");
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(r.gx, r.nchunk), dim3(256), 0, as_stream(stream),
+                     g, ldg, y, ldy, M, C, make_fastdiv(HW), scale, shift, slope, mask, mean,
+                     invstd, r.cl, r.rl, r.rpc, partial);
+  NSM_LAUNCH_CHECK("bn_bwd_reduce");
+  return 0;
+}
+
+extern "C" int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int C, int c_real,
+                                   const float* gamma, const float* invstd, float* dgamma,
+                                   float* dbeta, float* dbias_prev, float* coef, void* stream) {
+  NSM_CHECK_ARG(partial && gamma && invstd && coef, "bn_bwd_finalize: bad args");
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 256)), dim3(256), 0,
+                     as_stream(stream), partial, nchunk, M, C, c_real, gamma, invstd, dgamma, dbeta,
+                     dbias_prev, coef);
+  NSM_LAUNCH_CHECK("bn_bwd_finalize");
+  return 0;
+}
+
+extern "C" int nsm_bn_bwd_apply(const float* g, int ldg, const float* y, int ldy, int M, int C,
+                                int HW, const float* scale, const float* shift, float slope,
+                                const float* mask, const float* mean, const float* coef, float* dy,
+                                int lddy, void* stream) {
+  NSM_CHECK_ARG(g && y && scale && shift && mean && coef && dy && C % 4 == 0,
+                "bn_bwd_apply: bad args");
+  long long work = (long long)M * (C / 4);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), g,
+                     ldg, y, ldy, M, C, make_fastdiv(HW), scale, shift, slope, mask, mean, coef, dy,
+                     lddy);
+  NSM_LAUNCH_CHECK("bn_bwd_apply");
+  return 0;
+}
+
+extern "C" int nsm_avgpool2_fwd(const float* x, int B, int H, int W, int C, float* y,
+                                void* stream) {
+  NSM_CHECK_ARG(x && y && C % 4 == 0 && H >= 2 && W >= 2, "avgpool2_fwd: bad args");
+  long long work = (long long)B * (H / 2) * (W / 2) * (C / 4);
+  hipLaunchKernelGGL(avgpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), x,
+                     B, H, W, C / 4, y);
+  NSM_LAUNCH_CHECK("avgpool2_fwd");
+  return 0;
+}
+
+extern "C" int nsm_avgpool2_bwd_add(const float* dy, int B, int H, int W, int C,
+                                    const float* skip, float* dx, void* stream) {
+  NSM_CHECK_ARG(dy && dx && C % 4 == 0, "avgpool2_bwd: bad args");
+  long long work = (long long)B * H * W * (C / 4);
+  hipLaunchKernelGGL(avgpool2_bwd_add_kernel, dim3(grid_for(work)), dim3(256), 0,
+                     as_stream(stream), dy, B, H, W, C / 4, skip, dx);
+  NSM_LAUNCH_CHECK("avgpool2_bwd");
+  return 0;
+}
+
+extern "C" int nsm_resize_fwd(const float* x, int B, int Hi, int Wi, int C, float* y, int Ho,
+                              int Wo, void* stream) {
+  NSM_CHECK_ARG(x && y && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0,
+                "resize_fwd: bad args");
+  float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
+  bool vec = C % 4 == 0;
+  long long work = (long long)B * Ho * Wo * (vec ? C / 4 : C);
+  if (vec)
+    hipLaunchKernelGGL(resize_fwd_kernel<true>, dim3(grid_for(work)), dim3(256), 0,
+                       as_stream(stream), x, B, Hi, Wi, C, y, Ho, Wo, sh, sw);
+  else
+    hipLaunchKernelGGL(resize_fwd_kernel<false>, dim3(grid_for(work)), dim3(256), 0,
+                       as_stream(stream), x, B, Hi, Wi, C, y, Ho, Wo, sh, sw);
+  NSM_LAUNCH_CHECK("resize_fwd");
+  return 0;
+}
+
+extern "C" int nsm_resize_bwd(const float* dy, int B, int Hi, int Wi, int C, float* dx, int Ho,
+                              int Wo, void* stream) {
+  NSM_CHECK_ARG(dy && dx && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0,
+                "resize_bwd: bad args");
+  float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
+  // the gather visits at most 16 candidate columns per input column
+  NSM_CHECK_ARG(sw == 0.f || (2.f / sw + 4.f) < 16.f, "resize_bwd: scale too small");
+  bool vec = C % 4 == 0;
+  long long work = (long long)B * Hi * Wi * (vec ? C / 4 : C);
+  if (vec)
+    hipLaunchKernelGGL(resize_bwd_kernel<true>, dim3(grid_for(work)), dim3(256), 0,
+                       as_stream(stream), dy, B, Hi, Wi, C, dx, Ho, Wo, sh, sw);
+  else
+    hipLaunchKernelGGL(resize_bwd_kernel<false>, dim3(grid_for(work)), dim3(256), 0,
+                       as_stream(stream), dy, B, Hi, Wi, C, dx, Ho, Wo, sh, sw);
+  NSM_LAUNCH_CHECK("resize_bwd");
+  return 0;
+}
+
+extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, float* out, int cp,
+                              void* stream) {
+  NSM_CHECK_ARG(x && out && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C, "input_prep: bad args");
+  long long work = (long long)B * (H / 2) * (W / 2) * cp;
+  hipLaunchKernelGGL(input_prep_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), x,
+                     B, C, H, W, out, cp);
+  NSM_LAUNCH_CHECK("input_prep");
+  return 0;
+}
+
+extern "C" int nsm_input_grad(const float* dX, int B, int C, int H, int W, int cp, float* dx,
+                              void* stream) {
+  NSM_CHECK_ARG(dX && dx && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C, "input_grad: bad args");
+  long long work = (long long)B * C * H * W;
+  hipLaunchKernelGGL(input_grad_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), dX,
+                     B, C, H, W, cp, dx);
+  NSM_LAUNCH_CHECK("input_grad");
+  return 0;
+}
+
+extern "C" int nsm_head_fwd(const float* z, int ldz, int B, int Rh, int Rw, const float* w10,
+                            const float* b10, float* out, void* stream) {
+  NSM_CHECK_ARG(z && w10 && b10 && out && ldz >= 16 && ldz % 4 == 0, "head_fwd: bad args");
+  long long npix = (long long)B * Rh * Rw;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(npix)), dim3(256), 0, as_stream(stream), z, ldz,
+                     B, Rh, Rw, w10, b10, out);
+  NSM_LAUNCH_CHECK("head_fwd");
+  return 0;
+}
+
+extern "C" int nsm_head_bwd_blocks(int B, int Rh, int Rw) {
+  return grid_for((long long)B * Rh * Rw, 256, 1024);
+}
+
+extern "C" int nsm_head_bwd(const float* gout, const float* out, const float* z, int ldz, int B,
+                            int Rh, int Rw, const float* w10, float* dz, float* partial,
+                            float* dw10, float* db10, void* stream) {
+  NSM_CHECK_ARG(gout && out && z && w10 && dz && partial && dw10 && db10 && ldz % 4 == 0,
+                "head_bwd: bad args");
+  int nblk = nsm_head_bwd_blocks(B, Rh, Rw);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(nblk), dim3(256), 0, s, gout, out, z, ldz, B, Rh, Rw,
+                     w10, dz, partial);
+  NSM_LAUNCH_CHECK("head_bwd");
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(1), dim3(128), 0, s, partial, nblk, dw10, db10);
+  NSM_LAUNCH_CHECK("head_reduce");
+  return 0;
+}
+
+extern "C" int nsm_loss_blocks(int64_t n) { return grid_for(n, 1024, 1024); }
+
+extern "C" int nsm_l1_loss_fwd(const float* o, const float* t, int64_t n, float alpha,
+                               float* partial, float* out, void* stream) {
+  NSM_CHECK_ARG(o && t && partial && out && n > 0, "l1_loss_fwd: bad args");
+  int nb = nsm_loss_blocks(n);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(l1_partial_kernel, dim3(nb), dim3(256), 0, s, o, t, n, partial);
+  hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(64), 0, s, partial, nb,
+                     (double)alpha / (double)n, out);
+  NSM_LAUNCH_CHECK("l1_loss_fwd");
+  return 0;
+}
+
+extern "C" int nsm_l1_loss_bwd(const float* o, const float* t, int64_t n, float alpha,
+                               const float* gscale, float* grad, int accumulate, void* stream) {
+  NSM_CHECK_ARG(o && t && grad && n > 0, "l1_loss_bwd: bad args");
+  hipLaunchKernelGGL(l1_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), o, t, n,
+                     alpha, gscale, grad, accumulate);
+  NSM_LAUNCH_CHECK("l1_loss_bwd");
+  return 0;
+}
+
+extern "C" int nsm_channel_std(const float* x, int B, int C, int H, int W, float* partial,
+                               float* std_o, void* stream) {
+  (void)partial;
+  NSM_CHECK_ARG(x && std_o && B * H * W > 0, "channel_std: bad args");
+  hipLaunchKernelGGL(channel_std_kernel, dim3(C), dim3(1024), 0, as_stream(stream), x, B, C, H * W,
+                     std_o);
+  NSM_LAUNCH_CHECK("channel_std");
+  return 0;
+}
+
+extern "C" int nsm_perturb(const float* x, const float* noise, const float* stdv, int B, int C,
+                           int H, int W, float factor, float* out, void* stream) {
+  NSM_CHECK_ARG(x && noise && stdv && out, "perturb: bad args");
+  long long total = (long long)B * C * H * W;
+  hipLaunchKernelGGL(perturb_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x,
+                     noise, stdv, C, H * W, total, factor, out);
+  NSM_LAUNCH_CHECK("perturb");
+  return 0;
+}
+
+extern "C" int nsm_sumsq(const float* g, int64_t n, float* partial, float* out, void* stream) {
+  NSM_CHECK_ARG(g && partial && out && n > 0, "sumsq: bad args");
+  int nb = nsm_loss_blocks(n);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(nb), dim3(256), 0, s, g, n, partial);
+  hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(64), 0, s, partial, nb, 1.0, out);
+  NSM_LAUNCH_CHECK("sumsq");
+  return 0;
+}
+
+extern "C" int nsm_clip_coef(const float* sumsq, float inv_world, float max_norm, float* coef,
+                             void* stream) {
+  NSM_CHECK_ARG(sumsq && coef, "clip_coef: bad args");
+  hipLaunchKernelGGL(clip_coef_kernel, dim3(1), dim3(1), 0, as_stream(stream), sumsq, inv_world,
+                     max_norm, coef);
+  NSM_LAUNCH_CHECK("clip_coef");
+  return 0;
+}
+
+extern "C" int nsm_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr,
+                              float beta1, float beta2, float eps, float weight_decay, int step,
+                              const float* gcoef, void* stream) {
+  NSM_CHECK_ARG(p && g && m && v && n > 0 && step >= 1, "adamw: bad args");
+  double bc1 = 1.0 - pow((double)beta1, step);
+  double bc2 = 1.0 - pow((double)beta2, step);
+  float step_size = (float)(lr / bc1);
+  float bc2_sqrt = (float)sqrt(bc2);
+  float decay = 1.f - lr * weight_decay;
+  hipLaunchKernelGGL(adamw_kernel, dim3(grid_for(n)), dim3(256), 0, as_stream(stream), p, g, m, v,
+                     n, decay, beta1, beta2, eps, step_size, bc2_sqrt, gcoef);
+  NSM_LAUNCH_CHECK("adamw");
+  return 0;
+}

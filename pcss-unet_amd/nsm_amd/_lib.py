@@ -1,0 +1,111 @@
+"""ctypes binding of libnsm.so (the C ABI declared in include/nsm.h).
+
+This is the ONLY way the host reaches the GPU kernels. There is no fallback:
+if the shared library is missing or fails to load, importing this module
+raises, and every op raises on a non-ROCm device.
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NSM_LIB", os.path.join(_HERE, "libnsm.so"))
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+L = ctypes.c_int64
+F = ctypes.c_float
+Z = ctypes.c_size_t
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "nsm_version": (I, []),
+    "nsm_get_last_error": (I, [ctypes.c_char_p, Z]),
+    "nsm_pack_conv_weight": (I, [P, I, I, I, I, I, I, P, P]),
+    "nsm_pad_vec": (I, [P, I, I, P, P]),
+    "nsm_conv_fwd": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P]),
+    "nsm_conv_wgrad_ws": (Z, [I, I, I, I, I, I]),
+    "nsm_conv_wgrad": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
+    "nsm_reduce_chunks": (I, [I, I]),
+    "nsm_bn_stats": (I, [P, I, I, I, P, I, P]),
+    "nsm_bn_finalize_train": (I, [P, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P]),
+    "nsm_bn_finalize_eval": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
+    "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, P]),
+    "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, P]),
+    "nsm_bn_bwd_finalize": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
+    "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, P]),
+    "nsm_avgpool2_fwd": (I, [P, I, I, I, I, P, P]),
+    "nsm_avgpool2_bwd_add": (I, [P, I, I, I, I, P, P, P]),
+    "nsm_resize_fwd": (I, [P, I, I, I, I, P, I, I, P]),
+    "nsm_resize_bwd": (I, [P, I, I, I, I, P, I, I, P]),
+    "nsm_input_prep": (I, [P, I, I, I, I, P, I, P]),
+    "nsm_input_grad": (I, [P, I, I, I, I, I, P, P]),
+    "nsm_head_fwd": (I, [P, I, I, I, I, P, P, P, P]),
+    "nsm_head_bwd_blocks": (I, [I, I, I]),
+    "nsm_head_bwd": (I, [P, P, P, I, I, I, I, P, P, P, P, P, P]),
+    "nsm_loss_blocks": (I, [L]),
+    "nsm_l1_loss_fwd": (I, [P, P, L, F, P, P, P]),
+    "nsm_l1_loss_bwd": (I, [P, P, L, F, P, P, I, P]),
+    "nsm_channel_std": (I, [P, I, I, I, I, P, P, P]),
+    "nsm_perturb": (I, [P, P, P, I, I, I, I, F, P, P]),
+    "nsm_sumsq": (I, [P, L, P, P, P]),
+    "nsm_clip_coef": (I, [P, F, F, P, P]),
+    "nsm_adamw_step": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P]),
+}
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libnsm.so not found at {LIB_PATH}: build it with `make -C pcss-unet_amd/csrc` "
+            "(or __graft_entry__.build()). There is no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+class NsmError(RuntimeError):
+    pass
+
+
+def last_error():
+    buf = ctypes.create_string_buffer(512)
+    lib.nsm_get_last_error(buf, 512)
+    return buf.value.decode(errors="replace")
+
+
+def call(name, *args):
+    """Invoke a C-ABI entry point; raise NsmError with the library's message."""
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        raise NsmError(f"{name} failed (code {rc}): {last_error()}")
+    return rc
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def require_gpu(t, what="tensor"):
+    if not t.is_cuda:
+        raise NsmError(f"{what} must be on a ROCm GPU device (got {t.device}); "
+                       "the nsm_amd path has no CPU implementation")
+    return t
+
+
+def symbols():
+    return list(_SIGS)

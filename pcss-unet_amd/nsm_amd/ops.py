@@ -1,0 +1,234 @@
+"""Tensor-level wrappers over the libnsm C ABI (one function per entry point).
+
+Activations are NHWC fp32 2-D views `[pixels, channels_padded]`; every
+wrapper allocates its outputs with the PyTorch caching allocator and launches
+on the current HIP stream. No host synchronisation anywhere.
+"""
+import torch
+
+from ._lib import call, ptr, stream
+
+F32 = torch.float32
+PACK_FWD, PACK_DGRAD = 0, 1
+
+
+def pad32(c):
+    return (c + 31) // 32 * 32
+
+
+def empty(*shape, device):
+    return torch.empty(*shape, dtype=F32, device=device)
+
+
+# ---- parameters ------------------------------------------------------------
+def pack_conv_weight(w, cout_p, cin_p, mode):
+    cout, cin, k, _ = w.shape
+    taps = k * k
+    out = empty(cout_p * taps * cin_p, device=w.device)
+    call("nsm_pack_conv_weight", ptr(w), cout, cin, k, cout_p, cin_p, mode, ptr(out), stream())
+    return out
+
+
+def pad_vec(v, n_p):
+    if v.numel() == n_p:
+        return v
+    out = empty(n_p, device=v.device)
+    call("nsm_pad_vec", ptr(v), v.numel(), n_p, ptr(out), stream())
+    return out
+
+
+# ---- convolution -----------------------------------------------------------
+# Kernel probes: {tag: [(start_event, end_event), ...]} — bench.py registers a
+# tag to time one specific launch with HIP events on the launch stream.
+PROBES = {}
+
+
+def _probe(tag):
+    lst = PROBES.get(tag) if tag is not None else None
+    if lst is None:
+        return None
+    a = torch.cuda.Event(enable_timing=True)
+    b = torch.cuda.Event(enable_timing=True)
+    a.record()
+    lst.append((a, b))
+    return b
+
+
+def conv_fwd(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None):
+    """x: [B*H*W, cin_p]; returns y [B*H*W, cout_p]. pro=(scale, shift, mask|None)."""
+    M, cin_p = x.shape
+    y = out if out is not None else empty(M, cout_p, device=x.device)
+    sc = sh = mk = None
+    slope = 0.2
+    if pro is not None:
+        sc, sh, mk = pro
+    ev = _probe(tag)
+    call("nsm_conv_fwd", ptr(x), x.stride(0), B, H, W, cin_p, ptr(wpk), ptr(bias), cout_p, ksize,
+         ptr(y), y.stride(0), ptr(sc), ptr(sh), ptr(mk), slope, stream())
+    if ev is not None:
+        ev.record()
+    return y
+
+
+def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None):
+    """dw (reference layout [cout, cin, k, k], contiguous) <- sum_p dy (x) x."""
+    cout_p, cin_p = dy.shape[1], x.shape[1]
+    n = int(call_ws(B, H, W, cin_p, cout_p, ksize))
+    ws = empty(max(n, 1), device=dy.device)
+    sc = sh = mk = None
+    if pro is not None:
+        sc, sh, mk = pro
+    ev = _probe(tag)
+    call("nsm_conv_wgrad", ptr(dy), dy.stride(0), ptr(x), x.stride(0), B, H, W, cin_p, cout_p, ksize,
+         ptr(sc), ptr(sh), ptr(mk), 0.2, ptr(ws), n, cin, cout, ptr(dw), stream())
+    if ev is not None:
+        ev.record()
+
+
+def call_ws(B, H, W, cin_p, cout_p, ksize):
+    from ._lib import lib
+    return lib.nsm_conv_wgrad_ws(B, H, W, cin_p, cout_p, ksize)
+
+
+# ---- batch norm ------------------------------------------------------------
+def reduce_chunks(M, C):
+    from ._lib import lib
+    return lib.nsm_reduce_chunks(M, C)
+
+
+class BNState:
+    """Per-BN tensors the backward needs (all [C_padded])."""
+    __slots__ = ("scale", "shift", "mean", "invstd", "partial", "nchunk", "gamma")
+
+    def __init__(self, C, device):
+        self.scale = empty(C, device=device)
+        self.shift = empty(C, device=device)
+        self.mean = empty(C, device=device)
+        self.invstd = empty(C, device=device)
+        self.partial = None
+        self.nchunk = 0
+        self.gamma = None
+
+
+def bn_train(y, bn_mod, c_real, momentum, eps, n_updates=1):
+    """Batch statistics of y [M, C] + running-stat update (in place on the
+    module's buffers) -> BNState with scale/shift for the fused apply."""
+    M, C = y.shape
+    st = BNState(C, y.device)
+    st.nchunk = reduce_chunks(M, C)
+    st.partial = empty(st.nchunk * 2 * C, device=y.device)
+    call("nsm_bn_stats", ptr(y), y.stride(0), M, C, ptr(st.partial), st.nchunk, stream())
+    st.gamma = pad_vec(bn_mod.weight.detach(), C)
+    beta = pad_vec(bn_mod.bias.detach(), C)
+    rm = bn_mod.running_mean if bn_mod.track_running_stats else None
+    rv = bn_mod.running_var if bn_mod.track_running_stats else None
+    nbt = bn_mod.num_batches_tracked if bn_mod.track_running_stats else None
+    call("nsm_bn_finalize_train", ptr(st.partial), st.nchunk, M, C, c_real, ptr(st.gamma), ptr(beta),
+         ptr(rm), ptr(rv), ptr(nbt), momentum, eps, n_updates, ptr(st.mean), ptr(st.invstd),
+         ptr(st.scale), ptr(st.shift), stream())
+    return st
+
+
+def bn_running_update(st, M, C, bn_mod, c_real, momentum, eps, n_updates=1):
+    """Re-apply the running-stat update from saved partials (the conv5
+    checkpoint recompute in the reference's backward)."""
+    scratch = BNState(C, st.partial.device)
+    beta = pad_vec(bn_mod.bias.detach(), C)
+    call("nsm_bn_finalize_train", ptr(st.partial), st.nchunk, M, C, c_real, ptr(st.gamma), ptr(beta),
+         ptr(bn_mod.running_mean), ptr(bn_mod.running_var), ptr(bn_mod.num_batches_tracked),
+         momentum, eps, n_updates, ptr(scratch.mean), ptr(scratch.invstd), ptr(scratch.scale),
+         ptr(scratch.shift), stream())
+
+
+def bn_eval(bn_mod, C, c_real, eps, device):
+    st = BNState(C, device)
+    st.gamma = pad_vec(bn_mod.weight.detach(), C)
+    beta = pad_vec(bn_mod.bias.detach(), C)
+    call("nsm_bn_finalize_eval", ptr(bn_mod.running_mean), ptr(bn_mod.running_var), ptr(st.gamma),
+         ptr(beta), C, c_real, eps, ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift),
+         stream())
+    return st
+
+
+def bn_act(y, st, slope=0.2, res=None, out=None):
+    M, C = y.shape
+    o = out if out is not None else empty(M, C, device=y.device)
+    call("nsm_bn_act", ptr(y), y.stride(0), M, C, ptr(st.scale), ptr(st.shift), slope, ptr(res),
+         res.stride(0) if res is not None else 0, ptr(o), o.stride(0), stream())
+    return o
+
+
+def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2):
+    """Backward through lrelu(.)*mask after a train-mode BN: returns dy
+    (grad wrt the BN input) and writes dgamma/dbeta/dbias_prev (real chans)."""
+    M, C = y.shape
+    partial = empty(st.nchunk * 2 * C, device=y.device)
+    call("nsm_bn_bwd_reduce", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
+         ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(st.invstd), ptr(partial), st.nchunk,
+         stream())
+    coef = empty(3 * C, device=y.device)
+    call("nsm_bn_bwd_finalize", ptr(partial), st.nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
+         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
+    dy = empty(M, C, device=y.device)
+    call("nsm_bn_bwd_apply", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
+         ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy), dy.stride(0), stream())
+    return dy
+
+
+# ---- resampling --------------------------------------------------------------
+def avgpool2(x, B, H, W):
+    C = x.shape[1]
+    y = empty(B * (H // 2) * (W // 2), C, device=x.device)
+    call("nsm_avgpool2_fwd", ptr(x), B, H, W, C, ptr(y), stream())
+    return y
+
+
+def avgpool2_bwd_add(dy, B, H, W, skip):
+    C = dy.shape[1]
+    dx = empty(B * H * W, C, device=dy.device)
+    call("nsm_avgpool2_bwd_add", ptr(dy), B, H, W, C, ptr(skip), ptr(dx), stream())
+    return dx
+
+
+def resize(x, B, Hi, Wi, Ho, Wo):
+    C = x.shape[-1]
+    y = empty(B * Ho * Wo, C, device=x.device)
+    call("nsm_resize_fwd", ptr(x), B, Hi, Wi, C, ptr(y), Ho, Wo, stream())
+    return y
+
+
+def resize_bwd(dy, B, Hi, Wi, Ho, Wo):
+    C = dy.shape[-1]
+    dx = empty(B * Hi * Wi, C, device=dy.device)
+    call("nsm_resize_bwd", ptr(dy), B, Hi, Wi, C, ptr(dx), Ho, Wo, stream())
+    return dx
+
+
+# ---- boundary ----------------------------------------------------------------
+def input_prep(x, cp):
+    B, C, H, W = x.shape
+    out = empty(B * (H // 2) * (W // 2), cp, device=x.device)
+    call("nsm_input_prep", ptr(x), B, C, H, W, ptr(out), cp, stream())
+    return out
+
+
+def input_grad(dX, B, C, H, W):
+    dx = empty(B, C, H, W, device=dX.device)
+    call("nsm_input_grad", ptr(dX), B, C, H, W, dX.shape[1], ptr(dx), stream())
+    return dx
+
+
+def head_fwd(z, B, Rh, Rw, w10, b10):
+    out = empty(B, 1, 2 * Rh, 2 * Rw, device=z.device)
+    call("nsm_head_fwd", ptr(z), z.stride(0), B, Rh, Rw, ptr(w10), ptr(b10), ptr(out), stream())
+    return out
+
+
+def head_bwd(gout, out, z, B, Rh, Rw, w10, dw10, db10):
+    from ._lib import lib
+    nblk = lib.nsm_head_bwd_blocks(B, Rh, Rw)
+    partial = empty(nblk * 68, device=z.device)
+    dz = empty(*z.shape, device=z.device)
+    call("nsm_head_bwd", ptr(gout), ptr(out), ptr(z), z.stride(0), B, Rh, Rw, ptr(w10), ptr(dz),
+         ptr(partial), ptr(dw10), ptr(db10), stream())
+    return dz

@@ -1,0 +1,292 @@
+"""Drop-in `Unet` / `DoubleConv` whose forward and backward run entirely on the
+libnsm HIP kernels (MI355X / gfx950).
+
+Surface parity with `/root/reference/Unetmodel.py`:
+  * `DoubleConv(in_ch, out_ch, dropout_rate=0.2, dilation=1)` (:17-33) and
+    `Unet(in_ch=4, out_ch=1, dropout_rate=0.2)` (:35-63) own the same
+    sub-modules, so `state_dict()` keys/shapes/dtypes, `named_parameters()`
+    order (66 tensors) and `named_modules()` match the reference exactly.
+    The nn.Conv2d / nn.BatchNorm2d children are parameter holders only.
+  * `forward(x[B,C,H,W]) -> [B,1,H-H%2,W-W%2]` in (0,1) (:90-149), including
+    the odd-size bilinear guard, pixel_unshuffle, the conv5 checkpoint's
+    double BN running-stat update (train + backward), the up9 blur
+    (up x2 then resize back), additive skips, pixel_shuffle + sigmoid.
+  * `rearrange_to_channels` / `reconstruct_from_channels` (:65-88).
+  * `in_ch` generalises conv2 to 4*in_ch input channels (7-ch G-buffers).
+
+Execution: one torch.autograd.Function per forward. Activations live in HBM
+as NHWC fp32 `[pixels, channels padded to 32]`; every op is a libnsm kernel
+launched on the current HIP stream (see DESIGN.md for the kernel list).
+"""
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import require_gpu
+
+SLOPE = 0.2
+ENCODER = (2, 3, 4, 5)
+DECODER = (6, 7, 8, 9)
+SKIP_OF = {6: 4, 7: 3, 8: 2}          # merge_k = conv_k(...) + c_skip  (Unetmodel.py:125,131,137)
+POOL_SKIP = {4: 6, 3: 7, 2: 8}        # c_k feeds pool_k and decoder merge (6,7,8)
+
+
+class DoubleConv(nn.Module):
+    """Parameter container with the reference's layout (Unetmodel.py:17-33)."""
+
+    def __init__(self, in_ch, out_ch, dropout_rate=0.2, dilation=1):
+        super().__init__()
+        self.in_ch, self.out_ch, self.dropout_rate = in_ch, out_ch, dropout_rate
+        self.conv = nn.Sequential(
+            nn.Conv2d(in_ch, in_ch, 3, padding=1),
+            nn.BatchNorm2d(in_ch, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True),
+            nn.LeakyReLU(SLOPE, inplace=False),
+            nn.Dropout2d(p=dropout_rate),
+            nn.Conv2d(in_ch, out_ch, 1),
+            nn.BatchNorm2d(out_ch, eps=1e-5, momentum=0.1, affine=True, track_running_stats=True),
+            nn.LeakyReLU(SLOPE, inplace=False),
+        )
+
+    def forward(self, x):
+        raise RuntimeError("nsm_amd.DoubleConv is executed by Unet.forward (fused HIP path); "
+                           "call the enclosing Unet")
+
+
+class Unet(nn.Module):
+    def __init__(self, in_ch=4, out_ch=1, dropout_rate=0.2):
+        super().__init__()
+        self.in_ch = in_ch
+        self.conv2 = DoubleConv(4 * in_ch, 64, dropout_rate)
+        self.pool2 = nn.AvgPool2d(2)
+        self.conv3 = DoubleConv(64, 128, dropout_rate, dilation=2)
+        self.pool3 = nn.AvgPool2d(2)
+        self.conv4 = DoubleConv(128, 512, dropout_rate, dilation=4)
+        self.pool4 = nn.AvgPool2d(2)
+        self.conv5 = DoubleConv(512, 1024, dropout_rate)
+        self.up6 = nn.Upsample(scale_factor=2, mode="bilinear", align_corners=True)
+        self.conv6 = DoubleConv(1024, 512, dropout_rate)
+        self.up7 = nn.Upsample(scale_factor=2, mode="bilinear", align_corners=True)
+        self.conv7 = DoubleConv(512, 128, dropout_rate)
+        self.up8 = nn.Upsample(scale_factor=2, mode="bilinear", align_corners=True)
+        self.conv8 = DoubleConv(128, 64, dropout_rate)
+        self.up9 = nn.Upsample(scale_factor=2, mode="bilinear", align_corners=True)
+        self.conv9 = DoubleConv(64, 16, dropout_rate / 2)
+        self.conv10 = nn.Conv2d(16, 4, 1)
+        # parity hook: {k: [B, C_in(k)] scaled masks} consumed by the next forward
+        self._inject_masks = None
+        # when True, conv5's BNs get the reference's checkpoint-recompute update in backward
+        self.emulate_checkpoint_bn = True
+
+    # reference helpers (Unetmodel.py:65-88)
+    def rearrange_to_channels(self, x):
+        return torch.nn.functional.pixel_unshuffle(x, 2)
+
+    def reconstruct_from_channels(self, x):
+        return torch.nn.functional.pixel_shuffle(x, 2)
+
+    def block(self, k):
+        return getattr(self, f"conv{k}")
+
+    def forward(self, x):
+        require_gpu(x, "Unet input")
+        params = tuple(self.parameters())
+        for p in params[:1]:
+            require_gpu(p, "Unet parameters")
+        return _UnetFn.apply(x, self, *params)
+
+
+# ---------------------------------------------------------------------------
+# forward / backward orchestration
+# ---------------------------------------------------------------------------
+def _masks_for(mod, B, device, training):
+    masks = {}
+    inj = mod._inject_masks
+    mod._inject_masks = None
+    for k in ENCODER + DECODER:
+        blk = mod.block(k)
+        p = blk.conv[3].p
+        if not training or p == 0:
+            continue
+        ci = blk.conv[0].in_channels
+        if inj is not None and k in inj:
+            m = inj[k].to(device=device, dtype=torch.float32).reshape(B, ci)
+        else:
+            # ATen feature dropout: bernoulli(1-p) / (1-p) per (n, c)
+            m = torch.empty(B, ci, device=device).bernoulli_(1 - p).div_(1 - p)
+        cp = ops.pad32(ci)
+        if cp != ci:
+            m = torch.nn.functional.pad(m, (0, cp - ci))
+        masks[k] = m.contiguous()
+    return masks
+
+
+class _BlockSaved:
+    __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop")
+
+
+def _block_fwd(blk, X, B, H, W, training, mask, name=""):
+    c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
+    ci, co = c0.in_channels, c4.out_channels
+    cip, cop = ops.pad32(ci), ops.pad32(co)
+    assert X.shape[1] == cip, (X.shape, cip)
+    w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD)
+    b1 = ops.pad_vec(c0.bias.detach(), cip)
+    Y1 = ops.conv_fwd(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd")
+    eps1, eps2 = bn1m.eps, bn2m.eps
+    if training:
+        bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1)
+    else:
+        bn1 = ops.bn_eval(bn1m, cip, ci, eps1, X.device)
+    w2 = ops.pack_conv_weight(c4.weight.detach(), cop, cip, ops.PACK_FWD)
+    b2 = ops.pad_vec(c4.bias.detach(), cop)
+    Y2 = ops.conv_fwd(Y1, B, H, W, w2, b2, cop, 1, pro=(bn1.scale, bn1.shift, mask),
+                      tag=name + ".conv.4.fwd")
+    if training:
+        bn2 = ops.bn_train(Y2, bn2m, co, bn2m.momentum, eps2)
+    else:
+        bn2 = ops.bn_eval(bn2m, cop, co, eps2, X.device)
+    s = _BlockSaved()
+    s.X, s.Y1, s.Y2, s.bn1, s.bn2, s.mask = X, Y1, Y2, bn1, bn2, mask
+    s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
+    return s
+
+
+def _block_bwd(blk, s, G, grads, need_dx, name=""):
+    """G: grad wrt the block output z = lrelu(bn2(Y2)) [M, cop]."""
+    c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
+    ci, co = c0.in_channels, c4.out_channels
+    B, H, W = s.B, s.H, s.W
+    HW = H * W
+    g = grads
+    dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias])
+    w2d = ops.pack_conv_weight(c4.weight.detach(), s.cop, s.cip, ops.PACK_DGRAD)
+    dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
+    ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
+                   pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
+    dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias], g[c0.bias])
+    ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
+    if not need_dx:
+        return None
+    w1d = ops.pack_conv_weight(c0.weight.detach(), s.cip, s.cip, ops.PACK_DGRAD)
+    return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
+
+
+class _UnetFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, mod, *params):
+        training = mod.training
+        B, C, H, W = x.shape
+        dev = x.device
+        x32 = x.detach().to(torch.float32)
+        orig_hw = (H, W)
+        if H % 2 or W % 2:  # Unetmodel.py:94-97
+            He, We = H - H % 2, W - W % 2
+            x32 = ops.resize(x32.contiguous().view(B * C * H * W, 1), B * C, H, W, He, We).view(B, C, He, We)
+            H, W = He, We
+        x32 = x32.contiguous()
+        Rh, Rw = H // 2, W // 2
+        cin_p = ops.pad32(4 * C)
+        assert mod.conv2.conv[0].in_channels == 4 * C, (
+            f"Unet expects {mod.conv2.conv[0].in_channels // 4} input channels, got {C}")
+        X = ops.input_prep(x32, cin_p)
+        masks = _masks_for(mod, B, dev, training)
+
+        saved, c, shapes = {}, {}, {}
+        inp, h, w = X, Rh, Rw
+        for k in ENCODER:
+            s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}")
+            saved[k], shapes[k] = s, (h, w)
+            c[k] = ops.bn_act(s.Y2, s.bn2, SLOPE)
+            if k < 5:
+                inp = ops.avgpool2(c[k], B, h, w)
+                h, w = h // 2, w // 2
+        skip_shape = {6: shapes[4], 7: shapes[3], 8: shapes[2], 9: (Rh, Rw)}
+        cur, (h, w) = c[5], shapes[5]
+        ups = {}
+        for k in DECODER:
+            h2, w2 = 2 * h, 2 * w
+            up = ops.resize(cur, B, h, w, h2, w2)
+            th, tw = skip_shape[k]
+            if (th, tw) != (h2, w2):
+                up = ops.resize(up, B, h2, w2, th, tw)
+            ups[k] = (h, w, h2, w2, th, tw)
+            s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}")
+            saved[k] = s
+            res = c[SKIP_OF[k]] if k in SKIP_OF else None
+            cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
+            h, w = th, tw
+        z9 = cur
+        out = ops.head_fwd(z9, B, Rh, Rw, mod.conv10.weight.detach(), mod.conv10.bias.detach())
+
+        ctx.mod = mod
+        ctx.saved_blocks = saved
+        ctx.ups = ups
+        ctx.meta = (B, C, H, W, orig_hw, Rh, Rw, training)
+        ctx.z9 = z9
+        ctx.save_for_backward(out)
+        ctx.params = params
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        mod = ctx.mod
+        (out,) = ctx.saved_tensors
+        B, C, H, W, orig_hw, Rh, Rw, training = ctx.meta
+        if not training:
+            raise RuntimeError("nsm_amd Unet backward is implemented for train mode (as the "
+                               "reference trains); eval-mode BN backward is not on the hot path")
+        params = ctx.params
+        dev = out.device
+        total = sum(p.numel() for p in params)
+        flat = torch.empty(total, dtype=torch.float32, device=dev)
+        grads, off = {}, 0
+        views = []
+        for p in params:
+            v = flat[off:off + p.numel()].view_as(p)
+            grads[p] = v
+            views.append(v)
+            off += p.numel()
+
+        gout = gout.contiguous().to(torch.float32)
+        G = ops.head_bwd(gout, out, ctx.z9, B, Rh, Rw, mod.conv10.weight.detach(),
+                         grads[mod.conv10.weight], grads[mod.conv10.bias])
+        sb = ctx.saved_blocks
+        skip_grad = {}
+        for k in (9, 8, 7, 6):
+            s = sb[k]
+            dX = _block_bwd(mod.block(k), s, G, grads, True, f"conv{k}")
+            h, w, h2, w2, th, tw = ctx.ups[k]
+            if (th, tw) != (h2, w2):
+                dX = ops.resize_bwd(dX, B, h2, w2, th, tw)
+            dprev = ops.resize_bwd(dX, B, h, w, h2, w2)
+            # the previous merge / c5 receives dprev; merge_{k-1} = conv + c_skip
+            if k - 1 in SKIP_OF:
+                skip_grad[SKIP_OF[k - 1]] = dprev
+            G = dprev
+        # encoder: G is now d c5
+        need_x = ctx.needs_input_grad[0]
+        for k in (5, 4, 3, 2):
+            s = sb[k]
+            dX = _block_bwd(mod.block(k), s, G, grads, need_dx=(k > 2 or need_x), name=f"conv{k}")
+            if k == 5 and training and mod.emulate_checkpoint_bn:
+                # checkpoint recompute of conv5 (Unetmodel.py:114-116): 2nd BN update
+                blk = mod.block(5)
+                M = s.B * s.H * s.W
+                ops.bn_running_update(s.bn1, M, s.cip, blk.conv[1], blk.conv[0].in_channels,
+                                      blk.conv[1].momentum, blk.conv[1].eps)
+                ops.bn_running_update(s.bn2, M, s.cop, blk.conv[5], blk.conv[4].out_channels,
+                                      blk.conv[5].momentum, blk.conv[5].eps)
+            if k > 2:
+                ph, pw = sb[k - 1].H, sb[k - 1].W
+                G = ops.avgpool2_bwd_add(dX, B, ph, pw, skip_grad.get(k - 1))
+            else:
+                G = dX
+        dx = None
+        if need_x:
+            dx = ops.input_grad(G, B, C, H, W)
+            if (H, W) != tuple(orig_hw):
+                H0, W0 = orig_hw
+                dx = ops.resize_bwd(dx.view(B * C * H * W, 1), B * C, H0, W0, H, W).view(B, C, H0, W0)
+        ctx.saved_blocks = None
+        ctx.z9 = None
+        return (dx, None) + tuple(views)

@@ -1,0 +1,258 @@
+"""GPU: each libnsm kernel family against the PyTorch-CPU fp32 op it replaces
+(same seeded inputs), through the C ABI (nsm_amd.ops -> ctypes -> libnsm.so)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+torch.set_num_threads(8)
+
+
+def nhwc(x):  # [B,C,H,W] -> [B*H*W, C]
+    B, C, H, W = x.shape
+    return x.permute(0, 2, 3, 1).reshape(B * H * W, C).contiguous()
+
+
+def nchw(y, B, H, W):
+    return y.reshape(B, H, W, -1).permute(0, 3, 1, 2).contiguous()
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.fixture(scope="module")
+def ops(device):
+    from nsm_amd import ops as O
+    return O
+
+
+@pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 9, 11, 32, 64, 3), (1, 16, 16, 64, 32, 3),
+                                           (2, 8, 8, 128, 128, 3), (3, 7, 5, 32, 128, 1),
+                                           (2, 32, 32, 64, 512, 1), (1, 5, 67, 32, 32, 3)])
+def test_conv_fwd(ops, device, B, H, W, ci, co, k):
+    g = torch.Generator().manual_seed(B * 1000 + H * 10 + ci + co + k)
+    x = torch.randn(B, ci, H, W, generator=g)
+    w = torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5
+    b = torch.randn(co, generator=g)
+    ref = F.conv2d(x, w, b, padding=k // 2)
+    wp = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_FWD)
+    y = ops.conv_fwd(nhwc(x).to(device), B, H, W, wp, b.to(device), co, k)
+    out = nchw(y.cpu(), B, H, W)
+    assert (out - ref).abs().max().item() <= 2e-5 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 6, 7, 32, 64), (2, 16, 16, 128, 64)])
+def test_conv1x1_prologue(ops, device, B, H, W, ci, co):
+    g = torch.Generator().manual_seed(7)
+    y1 = torch.randn(B, ci, H, W, generator=g)
+    sc, sh = torch.rand(ci, generator=g) + 0.5, torch.randn(ci, generator=g)
+    mask = (torch.rand(B, ci, generator=g) > 0.2).float() / 0.8
+    w = torch.randn(co, ci, 1, 1, generator=g) / ci ** 0.5
+    a = F.leaky_relu(y1 * sc[None, :, None, None] + sh[None, :, None, None], 0.2) * mask[:, :, None, None]
+    ref = F.conv2d(a, w)
+    wp = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_FWD)
+    y = ops.conv_fwd(nhwc(y1).to(device), B, H, W, wp, None, co, 1,
+                     pro=(sc.to(device), sh.to(device), mask.to(device)))
+    assert (nchw(y.cpu(), B, H, W) - ref).abs().max().item() <= 2e-5 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 9, 11, 32, 64, 3), (2, 8, 8, 64, 64, 3),
+                                           (2, 12, 12, 64, 128, 1)])
+def test_conv_dgrad(ops, device, B, H, W, ci, co, k):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, ci, H, W, generator=g, requires_grad=True)
+    w = torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5
+    dy = torch.randn(B, co, H, W, generator=g)
+    F.conv2d(x, w, padding=k // 2).backward(dy)
+    wd = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_DGRAD)
+    dx = ops.conv_fwd(nhwc(dy).to(device), B, H, W, wd, None, ci, k)
+    assert rel(nchw(dx.cpu(), B, H, W), x.grad) <= 1e-5
+
+
+@pytest.mark.parametrize("B,H,W,ci,co,k,pro", [(2, 9, 11, 32, 64, 3, False), (2, 16, 16, 64, 32, 3, False),
+                                               (1, 33, 35, 128, 128, 3, False), (2, 8, 8, 32, 64, 1, True),
+                                               (2, 16, 16, 128, 512, 1, True), (2, 64, 64, 32, 32, 3, False)])
+def test_conv_wgrad(ops, device, B, H, W, ci, co, k, pro):
+    g = torch.Generator().manual_seed(13)
+    x = torch.randn(B, ci, H, W, generator=g)
+    sc, sh = torch.rand(ci, generator=g) + 0.5, torch.randn(ci, generator=g)
+    mask = (torch.rand(B, ci, generator=g) > 0.2).float() / 0.8
+    a = F.leaky_relu(x * sc[None, :, None, None] + sh[None, :, None, None], 0.2) * mask[:, :, None, None] if pro else x
+    w = (torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5).requires_grad_(True)
+    dy = torch.randn(B, co, H, W, generator=g)
+    F.conv2d(a, w, padding=k // 2).backward(dy)
+    dw = torch.empty(co, ci, k, k, device=device)
+    ops.conv_wgrad(nhwc(dy).to(device), nhwc(x).to(device), B, H, W, k, ci, co, dw,
+                   pro=(sc.to(device), sh.to(device), mask.to(device)) if pro else None)
+    assert rel(dw.cpu(), w.grad) <= 1e-5
+
+
+def test_conv_padded_channels(ops, device):
+    """conv2 of the 7-channel model: 28 real channels padded to 32."""
+    B, H, W, ci, co = 2, 10, 12, 28, 28
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, ci, H, W, generator=g)
+    w = torch.randn(co, ci, 3, 3, generator=g) / 16
+    b = torch.randn(co, generator=g)
+    ref = F.conv2d(x, w, b, padding=1)
+    xp = F.pad(nhwc(x), (0, 4)).to(device)
+    wp = ops.pack_conv_weight(w.to(device), 32, 32, ops.PACK_FWD)
+    y = ops.conv_fwd(xp, B, H, W, wp, ops.pad_vec(b.to(device), 32), 32, 3).cpu()
+    assert (nchw(y[:, :28], B, H, W) - ref).abs().max() <= 1e-4
+    assert y[:, 28:].abs().max() == 0
+
+
+@pytest.mark.parametrize("M,C", [(7, 32), (1000, 64), (4096 * 8 + 3, 128), (65536, 1024)])
+def test_bn_train_stats(ops, device, M, C):
+    g = torch.Generator().manual_seed(M)
+    y = torch.randn(M, C, generator=g) * 3 + 5
+    bn = torch.nn.BatchNorm2d(C).to(device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.1, 0.1)
+    st = ops.bn_train(y.to(device), bn, C, 0.1, 1e-5)
+    mean = y.double().mean(0)
+    var_b = y.double().var(0, unbiased=False)
+    var_u = y.double().var(0, unbiased=True)
+    assert (st.mean.cpu().double() - mean).abs().max() <= 1e-5 * 5
+    assert (st.invstd.cpu().double() - 1 / (var_b + 1e-5).sqrt()).abs().max() <= 1e-5
+    assert (bn.running_mean.cpu().double() - 0.1 * mean).abs().max() <= 1e-5
+    assert (bn.running_var.cpu().double() - (0.9 + 0.1 * var_u)).abs().max() <= 1e-4
+    assert int(bn.num_batches_tracked.item()) == 1
+
+
+def test_bn_act_and_bwd(ops, device):
+    """bn_train -> bn_act -> bn_bwd against autograd of F.batch_norm+lrelu*mask."""
+    B, C, H, W = 2, 64, 6, 5
+    g = torch.Generator().manual_seed(5)
+    y = (torch.randn(B, C, H, W, generator=g) * 2 + 1).requires_grad_(True)
+    gamma = (torch.rand(C, generator=g) + 0.5).requires_grad_(True)
+    beta = torch.randn(C, generator=g).requires_grad_(True)
+    mask = (torch.rand(B, C, generator=g) > 0.3).float() / 0.7
+    z = F.leaky_relu(F.batch_norm(y, None, None, gamma, beta, training=True), 0.2) * mask[:, :, None, None]
+    gz = torch.randn(B, C, H, W, generator=g)
+    z.backward(gz)
+    bn = torch.nn.BatchNorm2d(C).to(device)
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    yd = nhwc(y.detach()).to(device)
+    st = ops.bn_train(yd, bn, C, 0.1, 1e-5)
+    zz = ops.bn_act(yd, st)
+    zref = F.leaky_relu(F.batch_norm(y.detach(), None, None, gamma.detach(), beta.detach(), training=True), 0.2)
+    assert (nchw(zz.cpu(), B, H, W) - zref).abs().max() <= 1e-5
+    dg = torch.empty(C, device=device)
+    db = torch.empty(C, device=device)
+    dbias = torch.empty(C, device=device)
+    dy = ops.bn_bwd(nhwc(gz).to(device), yd, st, H * W, mask.to(device), C, dg, db, dbias)
+    assert rel(nchw(dy.cpu(), B, H, W), y.grad) <= 1e-5
+    assert rel(dg.cpu(), gamma.grad) <= 1e-5
+    assert rel(db.cpu(), beta.grad) <= 1e-5
+    assert dbias.abs().max().item() <= 1e-5
+
+
+@pytest.mark.parametrize("Hi,Wi,Ho,Wo", [(4, 5, 8, 10), (8, 10, 4, 5), (2, 4, 4, 8), (4, 8, 5, 9),
+                                         (67, 120, 134, 240), (134, 240, 135, 240), (1, 1, 2, 2),
+                                         (5, 5, 5, 5), (64, 64, 32, 32)])
+def test_resize(ops, device, Hi, Wi, Ho, Wo):
+    B, C = 2, 8
+    g = torch.Generator().manual_seed(Hi * Wo)
+    x = torch.randn(B, C, Hi, Wi, generator=g, requires_grad=True)
+    ref = F.interpolate(x, size=(Ho, Wo), mode="bilinear", align_corners=True)
+    gy = torch.randn(B, C, Ho, Wo, generator=g)
+    ref.backward(gy)
+    y = ops.resize(nhwc(x.detach()).to(device), B, Hi, Wi, Ho, Wo)
+    assert (nchw(y.cpu(), B, Ho, Wo) - ref.detach()).abs().max() <= 1e-5
+    dx = ops.resize_bwd(nhwc(gy).to(device), B, Hi, Wi, Ho, Wo)
+    assert (nchw(dx.cpu(), B, Hi, Wi) - x.grad).abs().max() <= 1e-5 * max(1, x.grad.abs().max().item())
+
+
+def test_resize_identity_bitwise(ops, device):
+    x = torch.randn(3 * 7 * 9, 16, device=device)
+    y = ops.resize(x, 3, 7, 9, 7, 9)
+    assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("H,W", [(8, 8), (7, 9), (135, 240)])
+def test_avgpool(ops, device, H, W):
+    B, C = 2, 16
+    g = torch.Generator().manual_seed(H)
+    x = torch.randn(B, C, H, W, generator=g, requires_grad=True)
+    ref = F.avg_pool2d(x, 2)
+    gy = torch.randn_like(ref)
+    ref.backward(gy)
+    skip = torch.randn(B, C, H, W, generator=g)
+    y = ops.avgpool2(nhwc(x.detach()).to(device), B, H, W)
+    assert (nchw(y.cpu(), B, H // 2, W // 2) - ref.detach()).abs().max() <= 1e-6
+    dx = ops.avgpool2_bwd_add(nhwc(gy).to(device), B, H, W, nhwc(skip).to(device))
+    assert (nchw(dx.cpu(), B, H, W) - (x.grad + skip)).abs().max() <= 1e-6
+
+
+def test_input_prep_and_grad(ops, device):
+    B, C, H, W = 2, 7, 6, 10
+    x = torch.randn(B, C, H, W)
+    X = ops.input_prep(x.to(device), 32).cpu()
+    ref = nhwc(F.pixel_unshuffle(x, 2))
+    assert torch.equal(X[:, :28], ref) and X[:, 28:].abs().max() == 0
+    dx = ops.input_grad(X.to(device), B, C, H, W).cpu()
+    assert torch.equal(dx, x)
+
+
+def test_head(ops, device):
+    B, Rh, Rw = 2, 5, 6
+    g = torch.Generator().manual_seed(9)
+    z = torch.randn(B, 16, Rh, Rw, generator=g, requires_grad=True)
+    w = (torch.randn(4, 16, 1, 1, generator=g) * 0.3).requires_grad_(True)
+    b = torch.randn(4, generator=g).requires_grad_(True)
+    out = torch.sigmoid(F.pixel_shuffle(F.conv2d(z, w, b), 2))
+    go = torch.randn_like(out)
+    out.backward(go)
+    zp = F.pad(nhwc(z.detach()), (0, 16)).to(device)
+    o = ops.head_fwd(zp, B, Rh, Rw, w.detach().to(device), b.detach().to(device))
+    assert (o.cpu() - out.detach()).abs().max() <= 1e-6
+    dw = torch.empty(4, 16, 1, 1, device=device)
+    db = torch.empty(4, device=device)
+    dz = ops.head_bwd(go.to(device), o, zp, B, Rh, Rw, w.detach().to(device), dw, db).cpu()
+    assert rel(nchw(dz[:, :16], B, Rh, Rw), z.grad) <= 1e-5 and dz[:, 16:].abs().max() == 0
+    assert rel(dw.cpu(), w.grad) <= 1e-5 and rel(db.cpu(), b.grad) <= 1e-5
+
+
+def test_l1_loss(device):
+    from nsm_amd.losses import l1_loss
+    g = torch.Generator().manual_seed(1)
+    o = torch.rand(2, 1, 64, 64, generator=g)
+    t = (torch.randint(0, 256, (2, 1, 64, 64), generator=g) / 255.0)
+    t[0, 0, 0, :4] = o[0, 0, 0, :4]  # exact ties: sign(0) = 0
+    oo = o.clone().requires_grad_(True)
+    ref = 0.9 * F.l1_loss(oo, t)
+    ref.backward()
+    od = o.to(device).requires_grad_(True)
+    loss = l1_loss(od, t.to(device), 0.9)
+    loss.backward()
+    assert abs(loss.item() - ref.item()) <= 1e-6 * ref.item()
+    assert torch.equal(od.grad.cpu(), oo.grad)
+
+
+def test_adamw_clip(device):
+    from nsm_amd.optim import FlatAdamW
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(s)) for s in [(64, 16, 3, 3), (64,), (7,)]]
+    ref = [torch.nn.Parameter(p.detach().clone()) for p in ps]
+    dps = [torch.nn.Parameter(p.detach().clone().to(device)) for p in ps]
+    opt_r = torch.optim.AdamW(ref, lr=7e-4, weight_decay=1e-3)
+    opt = FlatAdamW(dps, lr=7e-4, weight_decay=1e-3, max_grad_norm=1.0)
+    for step in range(3):
+        grads = [torch.randn_like(p) * (step + 1) for p in ps]
+        for p, gg in zip(ref, grads):
+            p.grad = gg.clone()
+        torch.nn.utils.clip_grad_norm_(ref, 1.0)
+        opt_r.step()
+        for p, gg in zip(dps, grads):
+            p.grad = gg.to(device)
+        opt.step()
+    for a, b in zip(dps, ref):
+        assert (a.detach().cpu() - b.detach()).abs().max() <= 1e-6
