@@ -494,20 +494,22 @@ static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksiz
   return pl;
 }
 
-// dw[co][ci][tap] (real dims) = sum_s ws[s][co][tap*cin_p + ci]
+// dw[co][ci][tap] (real dims) = sum_s ws[s][co][tap*cin_p + ci]; one thread
+// per (co, ci) walks the taps so reads stay coalesced along ci and each thread
+// writes its taps contiguously.
 __global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, int cin_p,
                                     int taps, int cin, int cout, float* __restrict__ dw) {
   int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  int total = cout * taps * cin;
-  if (idx >= total) return;
+  if (idx >= cout * cin) return;
   int ci = idx % cin;
-  int t = idx / cin;
-  int tap = t % taps;
-  int co = t / taps;
-  const float* src = ws + (size_t)co * N + tap * cin_p + ci;
-  float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += src[(size_t)k * M * N];
-  dw[((size_t)co * cin + ci) * taps + tap] = s;
+  int co = idx / cin;
+  const float* src = ws + (size_t)co * N + ci;
+  float* dst = dw + ((size_t)co * cin + ci) * taps;
+  for (int tap = 0; tap < taps; ++tap) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += src[(size_t)k * M * N + tap * cin_p];
+    dst[tap] = s;
+  }
 }
 
 __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int taps,
@@ -653,7 +655,7 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
     rc = dispatch_wgrad<false, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
   if (rc) return rc;
   int taps = ksize * ksize;
-  int total = cout * taps * cin;
+  int total = cout * cin;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, s, ws, pl.splits,
                      M, N, cin_p, taps, cin, cout, dw);
   NSM_LAUNCH_CHECK("conv_wgrad reduce");

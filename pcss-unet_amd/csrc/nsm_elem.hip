@@ -32,7 +32,7 @@ static ColRed colred_plan(int M, int C) {
   r.rl = 256 / r.cl;
   r.gx = (C / 4) / r.cl;
   long long want = (M + 63) / 64;
-  long long cap = 2048 / r.gx;
+  long long cap = 1024 / r.gx;  // ~1024 blocks fill the 256 CUs; finalize stays short
   if (cap < 1) cap = 1;
   r.nchunk = (int)(want < cap ? want : cap);
   if (r.nchunk < 1) r.nchunk = 1;
@@ -79,27 +79,44 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const float* __restrict__
   }
 }
 
-__global__ void bn_finalize_train_kernel(const float* __restrict__ partial, int nchunk, int rpc,
-                                         int M, int C, int c_real, const float* __restrict__ gamma,
-                                         const float* __restrict__ beta, float* run_mean,
-                                         float* run_var, int64_t* num_batches, float momentum,
-                                         float eps, int n_updates, float* mean_o, float* invstd_o,
-                                         float* scale_o, float* shift_o) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && num_batches) *num_batches += n_updates;
-  if (c >= C) return;
-  double tot = 0.0;
-  for (int k = 0; k < nchunk; ++k) tot += partial[(size_t)k * 2 * C + c];
-  const double mean = tot / M;
+// Finalize kernels: one block per 32 channels; 8 chunk-lanes per channel
+// reduce the partial rows in a fixed order (double), then merge in LDS.
+constexpr int FIN_CL = 32, FIN_KL = 8;
+
+__device__ __forceinline__ double fin_reduce(double v, double* sh, int cc, int kc) {
+  __syncthreads();
+  sh[kc * FIN_CL + cc] = v;
+  __syncthreads();
+  double t = 0.0;
+#pragma unroll
+  for (int k = 0; k < FIN_KL; ++k) t += sh[k * FIN_CL + cc];
+  return t;
+}
+
+__global__ void __launch_bounds__(256) bn_finalize_train_kernel(
+    const float* __restrict__ partial, int nchunk, int rpc, int M, int C, int c_real,
+    const float* __restrict__ gamma, const float* __restrict__ beta, float* run_mean,
+    float* run_var, int64_t* num_batches, float momentum, float eps, int n_updates, float* mean_o,
+    float* invstd_o, float* scale_o, float* shift_o) {
+  __shared__ double sh[FIN_KL * FIN_CL];
+  const int cc = threadIdx.x % FIN_CL, kc = threadIdx.x / FIN_CL;
+  const int c = blockIdx.x * FIN_CL + cc;
+  if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) *num_batches += n_updates;
+  const bool ok = c < C;
+  double s = 0.0;
+  if (ok)
+    for (int k = kc; k < nchunk; k += FIN_KL) s += partial[(size_t)k * 2 * C + c];
+  const double mean = fin_reduce(s, sh, cc, kc) / M;
   double m2 = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    int r0 = k * rpc, r1 = min(M, r0 + rpc);
-    int nk = r1 - r0;
-    if (nk <= 0) continue;
-    double mk = partial[(size_t)k * 2 * C + c] / nk;
-    double d = mk - mean;
-    m2 += partial[(size_t)k * 2 * C + C + c] + nk * d * d;
-  }
+  if (ok)
+    for (int k = kc; k < nchunk; k += FIN_KL) {
+      int r0 = k * rpc, nk = min(M, r0 + rpc) - r0;
+      if (nk <= 0) continue;
+      double d = partial[(size_t)k * 2 * C + c] / nk - mean;
+      m2 += partial[(size_t)k * 2 * C + C + c] + nk * d * d;
+    }
+  m2 = fin_reduce(m2, sh, cc, kc);
+  if (!ok || kc != 0) return;
   const float var_b = (float)(m2 / M);
   const float var_u = M > 1 ? (float)(m2 / (M - 1)) : var_b;
   const float mf = (float)mean;
@@ -205,17 +222,23 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(const float* __restrict__ partial, int nchunk, int M, int C,
-                                       int c_real, const float* __restrict__ gamma,
-                                       const float* __restrict__ invstd, float* dgamma,
-                                       float* dbeta, float* dbias_prev, float* coef) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double S1 = 0.0, S2 = 0.0;
-  for (int k = 0; k < nchunk; ++k) {
-    S1 += partial[(size_t)k * 2 * C + c];
-    S2 += partial[(size_t)k * 2 * C + C + c];
-  }
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
+    const float* __restrict__ partial, int nchunk, int M, int C, int c_real,
+    const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma,
+    float* dbeta, float* dbias_prev, float* coef) {
+  __shared__ double sh[FIN_KL * FIN_CL];
+  const int cc = threadIdx.x % FIN_CL, kc = threadIdx.x / FIN_CL;
+  const int c = blockIdx.x * FIN_CL + cc;
+  const bool ok = c < C;
+  double s1 = 0.0, s2 = 0.0;
+  if (ok)
+    for (int k = kc; k < nchunk; k += FIN_KL) {
+      s1 += partial[(size_t)k * 2 * C + c];
+      s2 += partial[(size_t)k * 2 * C + C + c];
+    }
+  const double S1 = fin_reduce(s1, sh, cc, kc);
+  const double S2 = fin_reduce(s2, sh, cc, kc);
+  if (!ok || kc != 0) return;
   const float gm = gamma[c], is = invstd[c];
   const double mdz = S1 / M, mdzx = S2 / M;
   const float k1 = gm * is;
@@ -307,9 +330,10 @@ __global__ void avgpool2_bwd_add_kernel(const float* __restrict__ dy, int B, int
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void lin_idx(float scale, int dst, int in, int& i0, int& i1, float& l0,
                                         float& l1) {
-  // __fmul_rn: keep src rounded to fp32 as ATen does; letting the compiler
-  // contract scale*dst - i0 into one FMA shifts lambda by up to ~1e-5.
-  float src = __fmul_rn(scale, (float)dst);
+  // keep src rounded to fp32 as ATen does; letting the compiler contract
+  // scale*dst - i0 into one FMA shifts lambda by up to ~1e-5.
+#pragma clang fp contract(off)
+  float src = scale * (float)dst;
   i0 = min((int)src, in - 1);
   l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
   l0 = 1.f - l1;
@@ -565,17 +589,25 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(
   }
 }
 
-// out[j] = sum_b partial[b][j]  (j < width) -> dw10 [64] then db10 [4]
-__global__ void head_reduce_kernel(const float* __restrict__ partial, int nblk, float* dw10,
-                                   float* db10) {
-  int j = threadIdx.x;
-  if (j >= 68) return;
+// out[j] = sum_b partial[b][j]: one block per output column j (< 68)
+__global__ void __launch_bounds__(256) head_reduce_kernel(const float* __restrict__ partial,
+                                                          int nblk, float* dw10, float* db10) {
+  __shared__ double sh[256];
+  const int j = blockIdx.x;
   double s = 0.0;
-  for (int b = 0; b < nblk; ++b) s += partial[(size_t)b * 68 + j];
-  if (j < 64)
-    dw10[j] = (float)s;
-  else
-    db10[j - 64] = (float)s;
+  for (int b = threadIdx.x; b < nblk; b += 256) s += partial[(size_t)b * 68 + j];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (j < 64)
+      dw10[j] = (float)sh[0];
+    else
+      db10[j - 64] = (float)sh[0];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -758,7 +790,7 @@ extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int M, in
   NSM_CHECK_ARG(M > 1, "bn_finalize: Expected more than 1 value per channel when training");
   ColRed r = colred_plan(M, C);
   NSM_CHECK_ARG(nchunk == r.nchunk, "bn_finalize: nchunk mismatch");
-  hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(ceil_div(C, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(ceil_div(C, FIN_CL)), dim3(256), 0,
                      as_stream(stream), partial, nchunk, r.rpc, M, C, c_real, gamma, beta, run_mean,
                      run_var, num_batches, momentum, eps, n_updates, mean, invstd, scale, shift);
   NSM_LAUNCH_CHECK("bn_finalize_train");
@@ -807,7 +839,7 @@ extern "C" int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int 
                                    const float* gamma, const float* invstd, float* dgamma,
                                    float* dbeta, float* dbias_prev, float* coef, void* stream) {
   NSM_CHECK_ARG(partial && gamma && invstd && coef, "bn_bwd_finalize: bad args");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, FIN_CL)), dim3(256), 0,
                      as_stream(stream), partial, nchunk, M, C, c_real, gamma, invstd, dgamma, dbeta,
                      dbias_prev, coef);
   NSM_LAUNCH_CHECK("bn_bwd_finalize");
@@ -928,7 +960,7 @@ extern "C" int nsm_head_bwd(const float* gout, const float* out, const float* z,
   hipLaunchKernelGGL(head_bwd_kernel, dim3(nblk), dim3(256), 0, s, gout, out, z, ldz, B, Rh, Rw,
                      w10, dz, partial);
   NSM_LAUNCH_CHECK("head_bwd");
-  hipLaunchKernelGGL(head_reduce_kernel, dim3(1), dim3(128), 0, s, partial, nblk, dw10, db10);
+  hipLaunchKernelGGL(head_reduce_kernel, dim3(68), dim3(256), 0, s, partial, nblk, dw10, db10);
   NSM_LAUNCH_CHECK("head_reduce");
   return 0;
 }

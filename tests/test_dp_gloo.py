@@ -1,0 +1,94 @@
+"""CPU, world_size 2 over gloo: the data-parallel exchange of the hot path.
+
+Each rank takes its contiguous shard (nsm_amd.data.shard_range), computes the
+oracle gradients of its shard into ONE flat buffer (the layout the HIP
+backward produces), and calls nsm_amd.optim.allreduce_grads. The result must
+equal the sum of both shards' gradients computed in one process (DDP
+semantics: per-rank BN batch statistics, summed grads, mean folded into the
+optimizer's clip coefficient)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def shard_grads(x_np, y_np, lo, hi):
+    from oracle import unet_ref as O
+    from oracle.weights import make_state
+    sd = O.torch_state(make_state(7, 42), requires_grad=True)
+    out, _ = O.forward(sd, torch.from_numpy(x_np[lo:hi]), True, None, 0.0)
+    O.custom_loss(out, torch.from_numpy(y_np[lo:hi]), 0.9).backward()
+    keys = O.param_keys(7)
+    return [sd[k].grad.detach().clone() for k in keys]
+
+
+def _worker(rank, world, port, x_np, y_np, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pcss-unet_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from nsm_amd.data import shard_range
+    from nsm_amd.optim import allreduce_grads, flat_grad
+    lo, hi = shard_range(len(x_np), world, rank)
+    grads = shard_grads(x_np, y_np, lo, hi)
+    total = sum(g.numel() for g in grads)
+    flat = torch.empty(total)
+    params, off = [], 0
+    for g in grads:
+        p = torch.nn.Parameter(torch.zeros_like(g))
+        p.grad = flat[off:off + g.numel()].view_as(g)
+        p.grad.copy_(g)
+        params.append(p)
+        off += g.numel()
+    assert flat_grad(params) is not None
+    allreduce_grads(params)
+    if rank == 0:
+        q.put([p.grad.clone().numpy() for p in params])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_shard_range_partitions():
+    from nsm_amd.data import shard_range
+    for n in (1, 7, 8, 512, 1001):
+        for w in (1, 2, 4, 8):
+            spans = [shard_range(n, w, r) for r in range(w)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+@pytest.mark.timeout(600)
+def test_dp_allreduce_matches_sum_of_shards():
+    from oracle.weights import synthetic_batch
+    x_np, y_np = synthetic_batch(4, 7, 32, 32)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, x_np, y_np, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=500)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    sys.path[:0] = [ROOT]
+    ref = [a + b for a, b in zip(shard_grads(x_np, y_np, 0, 2), shard_grads(x_np, y_np, 2, 4))]
+    for g, r in zip(got, ref):
+        np.testing.assert_allclose(g, r.numpy(), rtol=1e-5, atol=1e-7)
