@@ -60,7 +60,9 @@ def cpu_baseline(in_ch, H, W, frames=1, reps=3):
     from oracle import unet_ref as O
     from oracle.weights import make_state, synthetic_batch
     cores = len(os.sched_getaffinity(0))
-    torch.set_num_threads(min(cores, 64))
+    # the box grants this job a CPU share (OMP_NUM_THREADS, 16 per GPU); use it
+    share = int(os.environ.get("OMP_NUM_THREADS", cores))
+    torch.set_num_threads(max(1, min(cores, share)))
     sd = O.torch_state(make_state(in_ch, 42), requires_grad=True)
     x_np, y_np = synthetic_batch(frames, in_ch, H, W)
     y = torch.from_numpy(y_np)

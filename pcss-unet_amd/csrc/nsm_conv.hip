@@ -481,7 +481,8 @@ static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksiz
   pl.BM = cout_p >= 128 ? 128 : (cout_p >= 64 ? 64 : 32);
   pl.BN = cin_p >= 128 ? 128 : (cin_p >= 64 ? 64 : 32);
   long long tiles = (long long)ceil_div(M, pl.BM) * ceil_div(N, pl.BN);
-  long long want = (2048 + tiles - 1) / tiles;
+  long long want = (1024 + tiles - 1) / tiles;  // >= 2 waves of 2 blocks/CU
+  if (want > 32) want = 32;                      // bound the partial-slab traffic
   long long maxs = (K + 255) / 256;  // at least 256 pixels (8 K-slabs) per split
   long long sp = want < maxs ? want : maxs;
   if (sp < 1) sp = 1;
@@ -494,22 +495,30 @@ static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksiz
   return pl;
 }
 
-// dw[co][ci][tap] (real dims) = sum_s ws[s][co][tap*cin_p + ci]; one thread
-// per (co, ci) walks the taps so reads stay coalesced along ci and each thread
-// writes its taps contiguously.
-__global__ void wgrad_reduce_kernel(const float* __restrict__ ws, int splits, int M, int N, int cin_p,
-                                    int taps, int cin, int cout, float* __restrict__ dw) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= cout * cin) return;
-  int ci = idx % cin;
-  int co = idx / cin;
-  const float* src = ws + (size_t)co * N + ci;
-  float* dst = dw + ((size_t)co * cin + ci) * taps;
-  for (int tap = 0; tap < taps; ++tap) {
+// dw[co][ci][tap] (real dims) = sum_s ws[s][co][tap*cin_p + ci].
+// Block = one output channel co x 64 input channels: split-K partials are read
+// coalesced along ci (GEMM layout), summed in a fixed order, transposed through
+// LDS, and written as one contiguous [64][taps] run of the reference layout.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ ws, int splits,
+                                                           int M, int N, int cin_p, int taps,
+                                                           int cin, int cout,
+                                                           float* __restrict__ dw) {
+  __shared__ float tile[64 * 9];
+  const int co = blockIdx.y, ci0 = blockIdx.x * 64;
+  const int nci = min(64, cin - ci0);
+  const size_t MN = (size_t)M * N;
+  for (int i = threadIdx.x; i < 64 * taps; i += 256) {
+    int tap = i / 64, cl = i % 64;
     float s = 0.f;
-    for (int k = 0; k < splits; ++k) s += src[(size_t)k * M * N + tap * cin_p];
-    dst[tap] = s;
+    if (cl < nci) {
+      const float* src = ws + (size_t)co * N + tap * cin_p + ci0 + cl;
+      for (int k = 0; k < splits; ++k) s += src[k * MN];
+    }
+    tile[cl * taps + tap] = s;
   }
+  __syncthreads();
+  float* dst = dw + ((size_t)co * cin + ci0) * taps;
+  for (int j = threadIdx.x; j < nci * taps; j += 256) dst[j] = tile[j];
 }
 
 __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int taps,
@@ -655,8 +664,7 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
     rc = dispatch_wgrad<false, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
   if (rc) return rc;
   int taps = ksize * ksize;
-  int total = cout * cin;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(total, 256)), dim3(256), 0, s, ws, pl.splits,
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(cin, 64), cout), dim3(256), 0, s, ws, pl.splits,
                      M, N, cin_p, taps, cin, cout, dw);
   NSM_LAUNCH_CHECK("conv_wgrad reduce");
   return 0;
