@@ -59,6 +59,17 @@ int nsm_conv_fwd(const float* x, int ldx, int B, int H, int W, int cin_p, const 
                  const float* bias, int cout_p, int ksize, float* y, int ldy, const float* pro_scale,
                  const float* pro_shift, const float* pro_mask, float slope, void* stream);
 
+/* Same, plus fused BatchNorm batch statistics of y (bias included): if
+ * stats != NULL it receives per-M-block partials [ceil(M/R)][2][cout_p]
+ * {sum, M2 about the block mean}, R = nsm_conv_stat_rows(); feed them to
+ * nsm_bn_finalize_train with rows_per_chunk = R (replaces the separate
+ * statistics pass of nn.BatchNorm2d in train mode, Unetmodel.py:22,27). */
+int nsm_conv_stat_rows(int B, int H, int W, int cout_p);
+int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, int cin_p, const float* wpk,
+                       const float* bias, int cout_p, int ksize, float* y, int ldy,
+                       const float* pro_scale, const float* pro_shift, const float* pro_mask,
+                       float slope, float* stats, void* stream);
+
 /* nsm_conv_wgrad: dw[co][ci][kh][kw] (real cout x cin, reference layout) =
  *   sum_p dy[p][co] * pro(x[p+off(tap)][ci]); deterministic split-K over
  *   pixels through `ws` (nsm_conv_wgrad_ws() floats). Replaces the weight
@@ -72,13 +83,15 @@ int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx, int B, in
 
 /* ---- BatchNorm2d(eps, momentum) train/eval (Unetmodel.py:22,27) ----------- */
 int nsm_reduce_chunks(int M, int C); /* partial-buffer rows for the two below */
+int nsm_reduce_rows(int M, int C);   /* rows per chunk of that plan */
 /* per-channel chunk partials {sum, M2 about chunk mean}: partial[nchunk][2][C] */
 int nsm_bn_stats(const float* y, int ld, int M, int C, float* partial, int nchunk, void* stream);
 /* merge partials; batch mean/biased var normalise; unbiased var feeds running
  * stats, applied n_updates times (2 for conv5: checkpoint recompute,
  * Unetmodel.py:114-116); num_batches_tracked += n_updates.
  * Emits scale=gamma*invstd, shift=beta-mean*scale, mean, invstd. */
-int nsm_bn_finalize_train(const float* partial, int nchunk, int M, int C, int c_real,
+int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_per_chunk, int M, int C,
+                          int c_real,
                           const float* gamma, const float* beta, float* run_mean, float* run_var,
                           int64_t* num_batches, float momentum, float eps, int n_updates,
                           float* mean, float* invstd, float* scale, float* shift, void* stream);

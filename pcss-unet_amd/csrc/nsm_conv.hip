@@ -264,29 +264,110 @@ __device__ __forceinline__ void read_frag(const float* S, int rb, int lane, int 
 // Epilogues. acc[tm][tn] register i holds C[row][col] with
 //   col = lane & 31, row = (i & 3) + 8 * (i >> 2) + 4 * (lane >> 5).
 // ---------------------------------------------------------------------------
+struct EpiCtx {
+  int m0, n0;  // block origin
+  int mb, nb;  // this wave's tile origin
+  int wm, wn, lane;
+  float* lds;  // the GEMM's LDS array (free after the main loop)
+};
+
 struct EpiStoreP {
   float* y;
   int ldy;
   const float* bias;
+  float* stats;  // optional BN partials [gridDim.x][2][N]: {sum, M2 about block mean}
 };
 struct EpiStore {
   using P = EpiStoreP;
-  template <int TM, int TN>
-  __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], int mb, int nb, int lane, int M,
-                               int N, int) {
-    const int col = lane & 31, h = lane >> 5;
+  template <int TM, int TN, int WM, int WN>
+  __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
+                               int) {
+    const int col = cx.lane & 31, h = cx.lane >> 5;
+    float bv[TN];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
-      int n = nb + tn * 32 + col;
+      int n = cx.nb + tn * 32 + col;
+      bv[tn] = (e.bias && n < N) ? e.bias[n] : 0.f;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[tm][tn][i] += bv[tn];
+    }
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      int n = cx.nb + tn * 32 + col;
       if (n >= N) continue;
-      float bv = e.bias ? e.bias[n] : 0.f;
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-          int m = mb + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (m < M) e.y[(size_t)m * e.ldy + n] = acc[tm][tn][i] + bv;
+          int m = cx.mb + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (m < M) e.y[(size_t)m * e.ldy + n] = acc[tm][tn][i];
         }
+      }
+    }
+    if (!e.stats) return;
+    // ---- fused BatchNorm batch statistics of this block's rows (two-pass) ----
+    constexpr int BN = WN * TN * 32;
+    float* red = cx.lds;  // [WM][BN]
+    const int cnt = min(M - cx.m0, WM * TM * 32);
+    float s[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      float t = 0.f;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          int m = cx.mb + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          t += (m < M) ? acc[tm][tn][i] : 0.f;
+        }
+      t += __shfl_xor(t, 32, 64);
+      s[tn] = t;
+    }
+    if (h == 0)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) red[cx.wm * BN + cx.wn * TN * 32 + tn * 32 + col] = s[tn];
+    __syncthreads();
+    float mean[TN], tot[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) t += red[w * BN + cx.wn * TN * 32 + tn * 32 + col];
+      tot[tn] = t;
+      mean[tn] = t / (float)cnt;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      float t = 0.f;
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          int m = cx.mb + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
+          float d = acc[tm][tn][i] - mean[tn];
+          t += (m < M) ? d * d : 0.f;
+        }
+      t += __shfl_xor(t, 32, 64);
+      s[tn] = t;
+    }
+    if (h == 0)
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) red[cx.wm * BN + cx.wn * TN * 32 + tn * 32 + col] = s[tn];
+    __syncthreads();
+    if (cx.wm == 0 && h == 0) {
+      float* pr = e.stats + (size_t)blockIdx.x * 2 * N;
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        int n = cx.nb + tn * 32 + col;
+        if (n >= N) continue;
+        float q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) q += red[w * BN + cx.wn * TN * 32 + tn * 32 + col];
+        pr[n] = tot[tn];
+        pr[N + n] = q;
       }
     }
   }
@@ -297,10 +378,11 @@ struct EpiSlabP {
 };
 struct EpiSlab {
   using P = EpiSlabP;
-  template <int TM, int TN>
-  __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], int mb, int nb, int lane, int M,
-                               int N, int split) {
-    const int col = lane & 31, h = lane >> 5;
+  template <int TM, int TN, int WM, int WN>
+  __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
+                               int split) {
+    const int col = cx.lane & 31, h = cx.lane >> 5;
+    const int mb = cx.mb, nb = cx.nb;
     float* out = e.ws + (size_t)split * M * N;
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
@@ -323,8 +405,11 @@ struct EpiSlab {
 // MFMA tiles; grid (ceil(M/BM), ceil(N/BN), splits); split z covers
 // K range [z*kchunk, min(K,(z+1)*kchunk)).
 // ---------------------------------------------------------------------------
+// LDS (2 stages, ~74 KB at 128x128) caps residency at 2 blocks per CU, i.e.
+// <= 2 waves per SIMD for 256-thread blocks: tell the compiler so it spends
+// registers on keeping LDS reads in flight instead of maximising occupancy.
 template <int BM, int BN, int WM, int WN, class AL, class BL, class EP, class AP, class BP>
-__global__ void __launch_bounds__(WM * WN * 64)
+__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(1, 2)))
     gemm_f32_kernel(AP ap, BP bp, typename EP::P ep, int M, int N, int K, int kchunk) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -373,21 +458,36 @@ __global__ void __launch_bounds__(WM * WN * 64)
       a.load(ap, ar);
       b.load(bp, br);
     }
+    // fragments of group j+1 are read while group j's MFMAs issue (register
+    // double buffer; all indices compile-time after unrolling)
+    float fa[2][TM][4], fb[2][TN][4];
+#pragma unroll
+    for (int tm = 0; tm < TM; ++tm) read_frag<AL::KM, BM>(As, arb + tm * 32, lane, 0, fa[0][tm]);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) read_frag<BL::KM, BN>(Bs, brb + tn * 32, lane, 0, fb[0][tn]);
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float fa[TM][4], fb[TN][4];
+      const int cur = j & 1;
+      if (j < 3) {
 #pragma unroll
-      for (int tm = 0; tm < TM; ++tm) read_frag<AL::KM, BM>(As, arb + tm * 32, lane, j, fa[tm]);
+        for (int tm = 0; tm < TM; ++tm)
+          read_frag<AL::KM, BM>(As, arb + tm * 32, lane, j + 1, fa[cur ^ 1][tm]);
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn) read_frag<BL::KM, BN>(Bs, brb + tn * 32, lane, j, fb[tn]);
+        for (int tn = 0; tn < TN; ++tn)
+          read_frag<BL::KM, BN>(Bs, brb + tn * 32, lane, j + 1, fb[cur ^ 1][tn]);
+      }
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
         for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
           for (int tn = 0; tn < TN; ++tn)
-            acc[tm][tn] =
-                __builtin_amdgcn_mfma_f32_32x32x2f32(fa[tm][q], fb[tn][q], acc[tm][tn], 0, 0, 0);
+            acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[cur][tm][q], fb[cur][tn][q],
+                                                               acc[tm][tn], 0, 0, 0);
+      // pin the order: group j+1's LDS reads, then group j's MFMAs
+      if (j < 3) __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 4 * TM * TN, 0);
     }
     if (more) {
       float* An = lds + ((it + 1) & 1) * STAGE;
@@ -396,7 +496,8 @@ __global__ void __launch_bounds__(WM * WN * 64)
     }
     __syncthreads();
   }
-  EP::template apply<TM, TN>(ep, acc, m0 + arb, n0 + brb, lane, M, N, split);
+  EpiCtx cx{m0, n0, m0 + arb, n0 + brb, wm, wn, lane, lds};
+  EP::template apply<TM, TN, WM, WN>(ep, acc, cx, M, N, split);
 }
 
 // ---------------------------------------------------------------------------
@@ -413,6 +514,14 @@ static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const EpiStoreP
                      dim3(NT), 0, s, ap, bp, ep, M, N, K, K);
   NSM_LAUNCH_CHECK("conv_fwd");
   return 0;
+}
+
+// BM chosen by dispatch_conv_fwd (rows per BN-stat partial)
+static int conv_fwd_bm(long long M, int N) {
+  long long mb128 = ceil_div(M, 128);
+  if (N >= 128) return mb128 * ceil_div(N, 128) >= 512 ? 128 : 64;
+  if (N >= 64) return mb128 * ceil_div(N, 64) >= 512 ? 128 : 64;
+  return mb128 >= 512 ? 128 : 64;
 }
 
 template <bool PRO>
@@ -481,10 +590,15 @@ static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksiz
   pl.BM = cout_p >= 128 ? 128 : (cout_p >= 64 ? 64 : 32);
   pl.BN = cin_p >= 128 ? 128 : (cin_p >= 64 ? 64 : 32);
   long long tiles = (long long)ceil_div(M, pl.BM) * ceil_div(N, pl.BN);
-  long long want = (1024 + tiles - 1) / tiles;  // >= 2 waves of 2 blocks/CU
-  if (want > 32) want = 32;                      // bound the partial-slab traffic
-  long long maxs = (K + 255) / 256;  // at least 256 pixels (8 K-slabs) per split
+  // ~4096 blocks (8 waves of 2 blocks/CU) keeps the tail under ~6 %; each
+  // split keeps >= 8 K-slabs, and the fp32 partial slabs stay <= 512 MB.
+  long long want = (4096 + tiles - 1) / tiles;
+  long long maxs = (K + 255) / 256;
+  long long slab_cap = (128ll << 20) / ((long long)M * N);
+  if (slab_cap < 1) slab_cap = 1;
   long long sp = want < maxs ? want : maxs;
+  if (sp > slab_cap) sp = slab_cap;
+  if (sp > 512) sp = 512;
   if (sp < 1) sp = 1;
   long long kc = (K + sp - 1) / sp;
   kc = (kc + BK - 1) / BK * BK;
@@ -492,6 +606,7 @@ static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksiz
   pl.splits = (int)sp;
   pl.kchunk = (int)kc;
   pl.ws_floats = (size_t)sp * M * N;
+  if (sp > 16) pl.ws_floats += (size_t)((sp + 15) / 16) * M * N;  // stage-1 sums
   return pl;
 }
 
@@ -519,6 +634,26 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   __syncthreads();
   float* dst = dw + ((size_t)co * cin + ci0) * taps;
   for (int j = threadIdx.x; j < nci * taps; j += 256) dst[j] = tile[j];
+}
+
+// First reduction stage for many splits: dst[g][i] = sum of src[s][i] over the
+// splits s in group g (16 per group), float4 per thread, fixed order.
+__global__ void __launch_bounds__(256) splitsum_kernel(const float* __restrict__ src, int splits,
+                                                       long long L4, int per,
+                                                       float* __restrict__ dst) {
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= L4) return;
+  const int g = blockIdx.y;
+  const int s0 = g * per, s1 = min(splits, s0 + per);
+  const f32x4* p = (const f32x4*)src + i;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+  int s = s0;
+  for (; s + 1 < s1; s += 2) {
+    a += p[(size_t)s * L4];
+    b += p[(size_t)(s + 1) * L4];
+  }
+  if (s < s1) a += p[(size_t)s * L4];
+  ((f32x4*)dst)[(size_t)g * L4 + i] = a + b;
 }
 
 __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int taps,
@@ -576,6 +711,19 @@ extern "C" int nsm_conv_fwd(const float* x, int ldx, int B, int H, int W, int ci
                             const float* wpk, const float* bias, int cout_p, int ksize, float* y,
                             int ldy, const float* pro_scale, const float* pro_shift,
                             const float* pro_mask, float slope, void* stream) {
+  return nsm_conv_fwd_stats(x, ldx, B, H, W, cin_p, wpk, bias, cout_p, ksize, y, ldy, pro_scale,
+                            pro_shift, pro_mask, slope, nullptr, stream);
+}
+
+extern "C" int nsm_conv_stat_rows(int B, int H, int W, int cout_p) {
+  long long M = (long long)B * H * W;
+  return conv_fwd_bm(M, cout_p);
+}
+
+extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, int cin_p,
+                                  const float* wpk, const float* bias, int cout_p, int ksize,
+                                  float* y, int ldy, const float* pro_scale, const float* pro_shift,
+                                  const float* pro_mask, float slope, float* stats, void* stream) {
   NSM_CHECK_ARG(x && wpk && y, "conv_fwd: null pointer");
   NSM_CHECK_ARG(B > 0 && H > 0 && W > 0, "conv_fwd: bad shape");
   NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0, "conv_fwd: channels must be multiples of 32");
@@ -602,7 +750,7 @@ extern "C" int nsm_conv_fwd(const float* x, int ldx, int B, int H, int W, int ci
   ap.slope = slope;
   int K = ksize * ksize * cin_p;
   RowsKP bp{wpk, K, cout_p};
-  EpiStoreP ep{y, ldy, bias};
+  EpiStoreP ep{y, ldy, bias, stats};
   hipStream_t s = as_stream(stream);
   if (pro_scale) return dispatch_conv_fwd<true>(ap, bp, ep, (int)Ml, cout_p, K, s);
   return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s);
@@ -664,8 +812,22 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
     rc = dispatch_wgrad<false, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
   if (rc) return rc;
   int taps = ksize * ksize;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(cin, 64), cout), dim3(256), 0, s, ws, pl.splits,
-                     M, N, cin_p, taps, cin, cout, dw);
+  const float* red_src = ws;
+  int red_splits = pl.splits;
+  if (pl.splits > 16) {
+    // two-stage reduction: groups of 16 splits summed in parallel into the
+    // tail of the workspace (planned by plan_wgrad), then the transposing pass
+    const int per = 16, groups = ceil_div(pl.splits, per);
+    long long L4 = (long long)M * N / 4;
+    float* stage = ws + (size_t)pl.splits * M * N;
+    hipLaunchKernelGGL(splitsum_kernel, dim3(ceil_div(L4, 256), groups), dim3(256), 0, s, ws,
+                       pl.splits, L4, per, stage);
+    NSM_LAUNCH_CHECK("conv_wgrad splitsum");
+    red_src = stage;
+    red_splits = groups;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(cin, 64), cout), dim3(256), 0, s, red_src,
+                     red_splits, M, N, cin_p, taps, cin, cout, dw);
   NSM_LAUNCH_CHECK("conv_wgrad reduce");
   return 0;
 }

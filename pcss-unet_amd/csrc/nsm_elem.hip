@@ -79,18 +79,13 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const float* __restrict__
   }
 }
 
-// Finalize kernels: one block per 32 channels; 8 chunk-lanes per channel
-// reduce the partial rows in a fixed order (double), then merge in LDS.
-constexpr int FIN_CL = 32, FIN_KL = 8;
-
-__device__ __forceinline__ double fin_reduce(double v, double* sh, int cc, int kc) {
-  __syncthreads();
-  sh[kc * FIN_CL + cc] = v;
-  __syncthreads();
-  double t = 0.0;
+// Finalize kernels: one wave per channel; lanes stride over the partial rows
+// (4 independent accumulators keep several loads in flight), fixed-order
+// double reduction with cross-lane butterflies.
+__device__ __forceinline__ double wave_sum_d(double v) {
 #pragma unroll
-  for (int k = 0; k < FIN_KL; ++k) t += sh[k * FIN_CL + cc];
-  return t;
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
 __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
@@ -98,25 +93,39 @@ __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
     const float* __restrict__ gamma, const float* __restrict__ beta, float* run_mean,
     float* run_var, int64_t* num_batches, float momentum, float eps, int n_updates, float* mean_o,
     float* invstd_o, float* scale_o, float* shift_o) {
-  __shared__ double sh[FIN_KL * FIN_CL];
-  const int cc = threadIdx.x % FIN_CL, kc = threadIdx.x / FIN_CL;
-  const int c = blockIdx.x * FIN_CL + cc;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) *num_batches += n_updates;
-  const bool ok = c < C;
-  double s = 0.0;
-  if (ok)
-    for (int k = kc; k < nchunk; k += FIN_KL) s += partial[(size_t)k * 2 * C + c];
-  const double mean = fin_reduce(s, sh, cc, kc) / M;
-  double m2 = 0.0;
-  if (ok)
-    for (int k = kc; k < nchunk; k += FIN_KL) {
-      int r0 = k * rpc, nk = min(M, r0 + rpc) - r0;
-      if (nk <= 0) continue;
-      double d = partial[(size_t)k * 2 * C + c] / nk - mean;
-      m2 += partial[(size_t)k * 2 * C + C + c] + nk * d * d;
+  if (c >= C) return;
+  const size_t st = (size_t)2 * C;
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+  int k = lane;
+  for (; k + 192 < nchunk; k += 256) {
+    s0 += partial[k * st + c];
+    s1 += partial[(k + 64) * st + c];
+    s2 += partial[(k + 128) * st + c];
+    s3 += partial[(k + 192) * st + c];
+  }
+  for (; k < nchunk; k += 64) s0 += partial[k * st + c];
+  const double mean = wave_sum_d((s0 + s1) + (s2 + s3)) / M;
+  double q0 = 0.0, q1 = 0.0;
+  for (k = lane; k < nchunk; k += 128) {
+    int n0 = min(M, k * rpc + rpc) - k * rpc;
+    if (n0 > 0) {
+      double d = partial[k * st + c] / n0 - mean;
+      q0 += partial[k * st + C + c] + n0 * d * d;
     }
-  m2 = fin_reduce(m2, sh, cc, kc);
-  if (!ok || kc != 0) return;
+    int k1 = k + 64;
+    if (k1 < nchunk) {
+      int n1 = min(M, k1 * rpc + rpc) - k1 * rpc;
+      if (n1 > 0) {
+        double d = partial[k1 * st + c] / n1 - mean;
+        q1 += partial[k1 * st + C + c] + n1 * d * d;
+      }
+    }
+  }
+  const double m2 = wave_sum_d(q0 + q1);
+  if (lane != 0) return;
   const float var_b = (float)(m2 / M);
   const float var_u = M > 1 ? (float)(m2 / (M - 1)) : var_b;
   const float mf = (float)mean;
@@ -226,19 +235,24 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
     const float* __restrict__ partial, int nchunk, int M, int C, int c_real,
     const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma,
     float* dbeta, float* dbias_prev, float* coef) {
-  __shared__ double sh[FIN_KL * FIN_CL];
-  const int cc = threadIdx.x % FIN_CL, kc = threadIdx.x / FIN_CL;
-  const int c = blockIdx.x * FIN_CL + cc;
-  const bool ok = c < C;
-  double s1 = 0.0, s2 = 0.0;
-  if (ok)
-    for (int k = kc; k < nchunk; k += FIN_KL) {
-      s1 += partial[(size_t)k * 2 * C + c];
-      s2 += partial[(size_t)k * 2 * C + C + c];
-    }
-  const double S1 = fin_reduce(s1, sh, cc, kc);
-  const double S2 = fin_reduce(s2, sh, cc, kc);
-  if (!ok || kc != 0) return;
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= C) return;
+  const size_t st = (size_t)2 * C;
+  double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
+  int k = lane;
+  for (; k + 64 < nchunk; k += 128) {
+    a0 += partial[k * st + c];
+    b0 += partial[k * st + C + c];
+    a1 += partial[(k + 64) * st + c];
+    b1 += partial[(k + 64) * st + C + c];
+  }
+  for (; k < nchunk; k += 64) {
+    a0 += partial[k * st + c];
+    b0 += partial[k * st + C + c];
+  }
+  const double S1 = wave_sum_d(a0 + a1), S2 = wave_sum_d(b0 + b1);
+  if (lane != 0) return;
   const float gm = gamma[c], is = invstd[c];
   const double mdz = S1 / M, mdzx = S2 / M;
   const float k1 = gm * is;
@@ -781,17 +795,23 @@ extern "C" int nsm_bn_stats(const float* y, int ld, int M, int C, float* partial
   return 0;
 }
 
-extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int M, int C, int c_real,
-                                     const float* gamma, const float* beta, float* run_mean,
-                                     float* run_var, int64_t* num_batches, float momentum,
-                                     float eps, int n_updates, float* mean, float* invstd,
-                                     float* scale, float* shift, void* stream) {
+extern "C" int nsm_reduce_rows(int M, int C) {
+  if (M <= 0 || C <= 0 || C % 4) return 0;
+  return colred_plan(M, C).rpc;
+}
+
+extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_per_chunk, int M,
+                                     int C, int c_real, const float* gamma, const float* beta,
+                                     float* run_mean, float* run_var, int64_t* num_batches,
+                                     float momentum, float eps, int n_updates, float* mean,
+                                     float* invstd, float* scale, float* shift, void* stream) {
   NSM_CHECK_ARG(partial && gamma && beta && mean && invstd && scale && shift, "bn_finalize: null");
   NSM_CHECK_ARG(M > 1, "bn_finalize: Expected more than 1 value per channel when training");
-  ColRed r = colred_plan(M, C);
-  NSM_CHECK_ARG(nchunk == r.nchunk, "bn_finalize: nchunk mismatch");
-  hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(ceil_div(C, FIN_CL)), dim3(256), 0,
-                     as_stream(stream), partial, nchunk, r.rpc, M, C, c_real, gamma, beta, run_mean,
+  NSM_CHECK_ARG(nchunk >= 1 && rows_per_chunk >= 1 && (long long)nchunk * rows_per_chunk >= M,
+                "bn_finalize: chunks do not cover M");
+  hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(ceil_div(C, 4)), dim3(256), 0,
+                     as_stream(stream), partial, nchunk, rows_per_chunk, M, C, c_real, gamma, beta,
+                     run_mean,
                      run_var, num_batches, momentum, eps, n_updates, mean, invstd, scale, shift);
   NSM_LAUNCH_CHECK("bn_finalize_train");
   return 0;
@@ -839,7 +859,7 @@ extern "C" int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int 
                                    const float* gamma, const float* invstd, float* dgamma,
                                    float* dbeta, float* dbias_prev, float* coef, void* stream) {
   NSM_CHECK_ARG(partial && gamma && invstd && coef, "bn_bwd_finalize: bad args");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, FIN_CL)), dim3(256), 0,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 4)), dim3(256), 0,
                      as_stream(stream), partial, nchunk, M, C, c_real, gamma, invstd, dgamma, dbeta,
                      dbias_prev, coef);
   NSM_LAUNCH_CHECK("bn_bwd_finalize");

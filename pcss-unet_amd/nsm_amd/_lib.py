@@ -25,11 +25,14 @@ _SIGS = {
     "nsm_pack_conv_weight": (I, [P, I, I, I, I, I, I, P, P]),
     "nsm_pad_vec": (I, [P, I, I, P, P]),
     "nsm_conv_fwd": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P]),
+    "nsm_conv_stat_rows": (I, [I, I, I, I]),
+    "nsm_conv_fwd_stats": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
     "nsm_conv_wgrad_ws": (Z, [I, I, I, I, I, I]),
     "nsm_conv_wgrad": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
     "nsm_reduce_chunks": (I, [I, I]),
+    "nsm_reduce_rows": (I, [I, I]),
     "nsm_bn_stats": (I, [P, I, I, I, P, I, P]),
-    "nsm_bn_finalize_train": (I, [P, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P]),
+    "nsm_bn_finalize_train": (I, [P, I, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P]),
     "nsm_bn_finalize_eval": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
     "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, P]),
     "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, P]),

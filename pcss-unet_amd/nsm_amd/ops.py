@@ -54,20 +54,41 @@ def _probe(tag):
     return b
 
 
+class Partials:
+    """Per-channel BN partials {sum, M2} over row chunks: [nchunk][2][C]."""
+    __slots__ = ("buf", "nchunk", "rpc")
+
+    def __init__(self, buf, nchunk, rpc):
+        self.buf, self.nchunk, self.rpc = buf, nchunk, rpc
+
+
 def conv_fwd(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None):
     """x: [B*H*W, cin_p]; returns y [B*H*W, cout_p]. pro=(scale, shift, mask|None)."""
+    return conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro, out, tag, stats=False)[0]
+
+
+def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None, stats=True):
+    """conv_fwd returning (y, Partials|None): with stats=True the GEMM epilogue
+    also emits the BN batch-statistics partials of y."""
+    from ._lib import lib
     M, cin_p = x.shape
     y = out if out is not None else empty(M, cout_p, device=x.device)
     sc = sh = mk = None
     slope = 0.2
     if pro is not None:
         sc, sh, mk = pro
+    part = None
+    if stats:
+        rpc = lib.nsm_conv_stat_rows(B, H, W, cout_p)
+        nchunk = -(-M // rpc)
+        part = Partials(empty(nchunk * 2 * cout_p, device=x.device), nchunk, rpc)
     ev = _probe(tag)
-    call("nsm_conv_fwd", ptr(x), x.stride(0), B, H, W, cin_p, ptr(wpk), ptr(bias), cout_p, ksize,
-         ptr(y), y.stride(0), ptr(sc), ptr(sh), ptr(mk), slope, stream())
+    call("nsm_conv_fwd_stats", ptr(x), x.stride(0), B, H, W, cin_p, ptr(wpk), ptr(bias), cout_p,
+         ksize, ptr(y), y.stride(0), ptr(sc), ptr(sh), ptr(mk), slope,
+         ptr(part.buf) if part is not None else None, stream())
     if ev is not None:
         ev.record()
-    return y
+    return y, part
 
 
 def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None):
@@ -98,46 +119,57 @@ def reduce_chunks(M, C):
 
 class BNState:
     """Per-BN tensors the backward needs (all [C_padded])."""
-    __slots__ = ("scale", "shift", "mean", "invstd", "partial", "nchunk", "gamma")
+    __slots__ = ("scale", "shift", "mean", "invstd", "part", "nchunk", "gamma")
 
     def __init__(self, C, device):
         self.scale = empty(C, device=device)
         self.shift = empty(C, device=device)
         self.mean = empty(C, device=device)
         self.invstd = empty(C, device=device)
-        self.partial = None
+        self.part = None
         self.nchunk = 0
         self.gamma = None
 
 
-def bn_train(y, bn_mod, c_real, momentum, eps, n_updates=1):
-    """Batch statistics of y [M, C] + running-stat update (in place on the
-    module's buffers) -> BNState with scale/shift for the fused apply."""
+def bn_partials(y):
+    """Standalone batch-statistics pass over y [M, C] (when not fused)."""
+    from ._lib import lib
     M, C = y.shape
-    st = BNState(C, y.device)
-    st.nchunk = reduce_chunks(M, C)
-    st.partial = empty(st.nchunk * 2 * C, device=y.device)
-    call("nsm_bn_stats", ptr(y), y.stride(0), M, C, ptr(st.partial), st.nchunk, stream())
-    st.gamma = pad_vec(bn_mod.weight.detach(), C)
+    nchunk, rpc = reduce_chunks(M, C), lib.nsm_reduce_rows(M, C)
+    part = Partials(empty(nchunk * 2 * C, device=y.device), nchunk, rpc)
+    call("nsm_bn_stats", ptr(y), y.stride(0), M, C, ptr(part.buf), nchunk, stream())
+    return part
+
+
+def _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, gamma):
     beta = pad_vec(bn_mod.bias.detach(), C)
-    rm = bn_mod.running_mean if bn_mod.track_running_stats else None
-    rv = bn_mod.running_var if bn_mod.track_running_stats else None
-    nbt = bn_mod.num_batches_tracked if bn_mod.track_running_stats else None
-    call("nsm_bn_finalize_train", ptr(st.partial), st.nchunk, M, C, c_real, ptr(st.gamma), ptr(beta),
-         ptr(rm), ptr(rv), ptr(nbt), momentum, eps, n_updates, ptr(st.mean), ptr(st.invstd),
-         ptr(st.scale), ptr(st.shift), stream())
+    track = bn_mod.track_running_stats
+    call("nsm_bn_finalize_train", ptr(part.buf), part.nchunk, part.rpc, M, C, c_real, ptr(gamma),
+         ptr(beta), ptr(bn_mod.running_mean if track else None),
+         ptr(bn_mod.running_var if track else None),
+         ptr(bn_mod.num_batches_tracked if track else None), momentum, eps, n_updates,
+         ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift), stream())
+
+
+def bn_train(y, bn_mod, c_real, momentum, eps, n_updates=1, part=None):
+    """Train-mode BN: batch statistics of y [M, C] (given as fused GEMM
+    partials, or computed here) + running-stat update in place on the module's
+    buffers -> BNState with scale/shift for the fused apply."""
+    M, C = y.shape
+    if part is None:
+        part = bn_partials(y)
+    st = BNState(C, y.device)
+    st.part, st.nchunk = part, part.nchunk
+    st.gamma = pad_vec(bn_mod.weight.detach(), C)
+    _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, st.gamma)
     return st
 
 
 def bn_running_update(st, M, C, bn_mod, c_real, momentum, eps, n_updates=1):
     """Re-apply the running-stat update from saved partials (the conv5
     checkpoint recompute in the reference's backward)."""
-    scratch = BNState(C, st.partial.device)
-    beta = pad_vec(bn_mod.bias.detach(), C)
-    call("nsm_bn_finalize_train", ptr(st.partial), st.nchunk, M, C, c_real, ptr(st.gamma), ptr(beta),
-         ptr(bn_mod.running_mean), ptr(bn_mod.running_var), ptr(bn_mod.num_batches_tracked),
-         momentum, eps, n_updates, ptr(scratch.mean), ptr(scratch.invstd), ptr(scratch.scale),
-         ptr(scratch.shift), stream())
+    scratch = BNState(C, st.part.buf.device)
+    _finalize(st.part, M, C, bn_mod, c_real, momentum, eps, n_updates, scratch, st.gamma)
 
 
 def bn_eval(bn_mod, C, c_real, eps, device):
@@ -162,12 +194,13 @@ def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2):
     """Backward through lrelu(.)*mask after a train-mode BN: returns dy
     (grad wrt the BN input) and writes dgamma/dbeta/dbias_prev (real chans)."""
     M, C = y.shape
-    partial = empty(st.nchunk * 2 * C, device=y.device)
+    nchunk = reduce_chunks(M, C)
+    partial = empty(nchunk * 2 * C, device=y.device)
     call("nsm_bn_bwd_reduce", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
-         ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(st.invstd), ptr(partial), st.nchunk,
+         ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(st.invstd), ptr(partial), nchunk,
          stream())
     coef = empty(3 * C, device=y.device)
-    call("nsm_bn_bwd_finalize", ptr(partial), st.nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
+    call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
          ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
     dy = empty(M, C, device=y.device)
     call("nsm_bn_bwd_apply", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),

@@ -131,18 +131,18 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     assert X.shape[1] == cip, (X.shape, cip)
     w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD)
     b1 = ops.pad_vec(c0.bias.detach(), cip)
-    Y1 = ops.conv_fwd(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd")
+    Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd", stats=training)
     eps1, eps2 = bn1m.eps, bn2m.eps
     if training:
-        bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1)
+        bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1)
     else:
         bn1 = ops.bn_eval(bn1m, cip, ci, eps1, X.device)
     w2 = ops.pack_conv_weight(c4.weight.detach(), cop, cip, ops.PACK_FWD)
     b2 = ops.pad_vec(c4.bias.detach(), cop)
-    Y2 = ops.conv_fwd(Y1, B, H, W, w2, b2, cop, 1, pro=(bn1.scale, bn1.shift, mask),
-                      tag=name + ".conv.4.fwd")
+    Y2, part2 = ops.conv_fwd_bn(Y1, B, H, W, w2, b2, cop, 1, pro=(bn1.scale, bn1.shift, mask),
+                             tag=name + ".conv.4.fwd", stats=training)
     if training:
-        bn2 = ops.bn_train(Y2, bn2m, co, bn2m.momentum, eps2)
+        bn2 = ops.bn_train(Y2, bn2m, co, bn2m.momentum, eps2, part=part2)
     else:
         bn2 = ops.bn_eval(bn2m, cop, co, eps2, X.device)
     s = _BlockSaved()
