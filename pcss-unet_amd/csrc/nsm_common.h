@@ -53,7 +53,9 @@ inline FastDiv make_fastdiv(uint32_t d) {
 }
 
 __device__ __forceinline__ uint32_t fdiv(uint32_t n, const FastDiv& f) {
-  return f.mul == 0 ? n : (__umulhi(n, f.mul) >> f.shr);
+  // d == 1 has mul == 0: umulhi gives 0 and the second term returns n
+  // (arithmetic select: no branch around the division).
+  return (__umulhi(n, f.mul) >> f.shr) + (f.mul == 0 ? n : 0u);
 }
 
 __device__ __forceinline__ float lrelu(float v, float slope) {

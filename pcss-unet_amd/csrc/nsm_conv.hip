@@ -27,6 +27,21 @@ namespace nsm {
 constexpr int BK = 32;
 constexpr int LDK = BK + 4;
 
+// Branch-free operand loads: buffer_load_dwordx4 through a per-block resource
+// descriptor whose base sits just below the block's lowest address; an
+// invalid lane gets an offset past num_records and the hardware returns 0
+// (zero padding / tails without exec-mask branches).
+constexpr uint32_t OOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const float* base, long long floats) {
+  long long bytes = floats * 4;
+  if (bytes > 0x7FFFFFFFll) bytes = 0x7FFFFFFFll;
+  if (bytes < 0) bytes = 0;
+  return __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ f32x4 bload4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
 // ---------------------------------------------------------------------------
 // Operand loaders. R = rows of the operand tile (BM or BN), NT = threads.
 // ---------------------------------------------------------------------------
@@ -48,13 +63,16 @@ struct ConvActLoader {  // MK image
   static constexpr int RSTEP = NT / (BK / 4);
   static constexpr int LDS_FLOATS = R * LDK;
   static_assert(NPT >= 1 && NPT * RSTEP == R, "loader shape");
-  int pix[NPT];
+  __amdgpu_buffer_rsrc_t rsrc;
+  int rel[NPT];  // pixel index relative to the descriptor base
   int py[NPT], px[NPT], pb[NPT];
   int kc, row0, tap, c0;
 
   __device__ void init(const ConvActP& p, int m0, int kbeg, int tid) {
     kc = (tid & 7) * 4;
     row0 = tid >> 3;
+    const int base_pix = max(0, m0 - p.W - 1);
+    rsrc = make_rsrc(p.x + (size_t)base_pix * p.ld, (long long)(p.M - base_pix) * p.ld);
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       int q = m0 + row0 + i * RSTEP;
@@ -64,7 +82,7 @@ struct ConvActLoader {  // MK image
       int xx = q - t * p.W;
       int b = (int)fdiv((uint32_t)t, p.fdH);
       int yy = t - b * p.H;
-      pix[i] = q;
+      rel[i] = q - base_pix;
       px[i] = xx;
       py[i] = v ? yy : -0x40000000;  // invalid rows never pass the bounds test
       pb[i] = b;
@@ -79,6 +97,7 @@ struct ConvActLoader {  // MK image
       dx = tap - (tap / 3) * 3 - 1;
     }
     const int c = c0 + kc;
+    const int shift = dy * p.W + dx;
     f32x4 sc, sh;
     if constexpr (PRO) {
       sc = *(const f32x4*)(p.scale + c);
@@ -87,21 +106,18 @@ struct ConvActLoader {  // MK image
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       int yy = py[i] + dy, xx = px[i] + dx;
-      bool ok = (unsigned)yy < (unsigned)p.H && (unsigned)xx < (unsigned)p.W;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (ok) {
-        const float* a = p.x + (size_t)(pix[i] + dy * p.W + dx) * p.ld + c;
-        v = *(const f32x4*)a;
-        if constexpr (PRO) {
-          v.x = lrelu(v.x * sc.x + sh.x, p.slope);
-          v.y = lrelu(v.y * sc.y + sh.y, p.slope);
-          v.z = lrelu(v.z * sc.z + sh.z, p.slope);
-          v.w = lrelu(v.w * sc.w + sh.w, p.slope);
-          if (p.mask) {
-            f32x4 mk = *(const f32x4*)(p.mask + (size_t)pb[i] * p.mask_ld + c);
-            v *= mk;
-          }
-        }
+      bool ok = ((unsigned)yy < (unsigned)p.H) & ((unsigned)xx < (unsigned)p.W);
+      uint32_t off = ok ? (uint32_t)((rel[i] + shift) * p.ld + c) * 4u : OOB;
+      f32x4 v = bload4(rsrc, off);
+      if constexpr (PRO) {
+        f32x4 a;
+        a.x = lrelu(v.x * sc.x + sh.x, p.slope);
+        a.y = lrelu(v.y * sc.y + sh.y, p.slope);
+        a.z = lrelu(v.z * sc.z + sh.z, p.slope);
+        a.w = lrelu(v.w * sc.w + sh.w, p.slope);
+        if (p.mask) a *= *(const f32x4*)(p.mask + (size_t)pb[i] * p.mask_ld + c);
+        // rows past M only feed masked output rows, but keep them 0 anyway
+        v = ok ? a : f32x4{0.f, 0.f, 0.f, 0.f};
       }
       r[i] = v;
     }
@@ -131,6 +147,7 @@ struct RowsKLoader {  // MK / NK image
   static constexpr int RSTEP = NT / (BK / 4);
   static constexpr int LDS_FLOATS = R * LDK;
   static_assert(NPT >= 1 && NPT * RSTEP == R, "loader shape");
+  __amdgpu_buffer_rsrc_t rsrc;
   int kc, row0, k0, n0;
 
   __device__ void init(const RowsKP& p, int n0_, int kbeg, int tid) {
@@ -138,14 +155,14 @@ struct RowsKLoader {  // MK / NK image
     row0 = tid >> 3;
     k0 = kbeg;
     n0 = n0_;
+    rsrc = make_rsrc(p.w + (size_t)n0 * p.ldw, (long long)(p.nrows - n0) * p.ldw);
   }
   __device__ void load(const RowsKP& p, f32x4* r) const {
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
-      int n = n0 + row0 + i * RSTEP;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (n < p.nrows) v = *(const f32x4*)(p.w + (size_t)n * p.ldw + k0 + kc);
-      r[i] = v;
+      int row = row0 + i * RSTEP;
+      uint32_t off = (n0 + row < p.nrows) ? (uint32_t)(row * p.ldw + k0 + kc) * 4u : OOB;
+      r[i] = bload4(rsrc, off);
     }
   }
   __device__ void advance(const RowsKP&) { k0 += BK; }
@@ -176,7 +193,8 @@ struct PixRowsLoader {  // KM / KN image
   static constexpr int NPT = BK / KSTEP;
   static constexpr int LDS_FLOATS = BK * (R + 4);
   static_assert(NPT >= 1 && NPT * KSTEP == BK && KSTEP * C4 == NT, "loader shape");
-  int col, c4o, krow0, k0, kend, dy, dx;
+  __amdgpu_buffer_rsrc_t rsrc;
+  int col, c4o, krow0, k0, kend, dy, dx, base_pix;
   bool colok;
   f32x4 sc, sh;
 
@@ -198,6 +216,8 @@ struct PixRowsLoader {  // KM / KN image
     }
     k0 = kbeg;
     kend = kend_;
+    base_pix = max(0, kbeg - p.W - 1);
+    rsrc = make_rsrc(p.x + (size_t)base_pix * p.ld, (long long)(p.M - base_pix) * p.ld);
     if constexpr (PRO) {
       sc = colok ? *(const f32x4*)(p.scale + col) : f32x4{0.f, 0.f, 0.f, 0.f};
       sh = colok ? *(const f32x4*)(p.shift + col) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -206,31 +226,31 @@ struct PixRowsLoader {  // KM / KN image
   __device__ void load(const PixRowsP& p, f32x4* r) const {
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
-      int q = k0 + krow0 + i * KSTEP;
-      bool ok = colok && q < kend;
+      const int q = k0 + krow0 + i * KSTEP;  // < 2^30 always: no guard needed for fdiv
+      bool ok = colok & (q < kend);
       int b = 0;
       int src = q;
-      if (SHIFT || PRO) {
-        int qq = ok ? q : 0;
-        int t = (int)fdiv((uint32_t)qq, p.fdW);
-        int xx = qq - t * p.W;
+      if constexpr (SHIFT || PRO) {
+        const int t = (int)fdiv((uint32_t)q, p.fdW);
+        const int xx = q - t * p.W;
         b = (int)fdiv((uint32_t)t, p.fdH);
-        int yy = t - b * p.H;
-        if (SHIFT) {
-          ok = ok && (unsigned)(yy + dy) < (unsigned)p.H && (unsigned)(xx + dx) < (unsigned)p.W;
+        const int yy = t - b * p.H;
+        if constexpr (SHIFT) {
+          ok = ok & ((unsigned)(yy + dy) < (unsigned)p.H) & ((unsigned)(xx + dx) < (unsigned)p.W);
           src = q + dy * p.W + dx;
         }
+        if constexpr (PRO) b = ok ? b : 0;
       }
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (ok) {
-        v = *(const f32x4*)(p.x + (size_t)src * p.ld + col);
-        if constexpr (PRO) {
-          v.x = lrelu(v.x * sc.x + sh.x, p.slope);
-          v.y = lrelu(v.y * sc.y + sh.y, p.slope);
-          v.z = lrelu(v.z * sc.z + sh.z, p.slope);
-          v.w = lrelu(v.w * sc.w + sh.w, p.slope);
-          if (p.mask) v *= *(const f32x4*)(p.mask + (size_t)b * p.mask_ld + col);
-        }
+      uint32_t off = ok ? (uint32_t)((src - base_pix) * p.ld + col) * 4u : OOB;
+      f32x4 v = bload4(rsrc, off);
+      if constexpr (PRO) {
+        f32x4 a;
+        a.x = lrelu(v.x * sc.x + sh.x, p.slope);
+        a.y = lrelu(v.y * sc.y + sh.y, p.slope);
+        a.z = lrelu(v.z * sc.z + sh.z, p.slope);
+        a.w = lrelu(v.w * sc.w + sh.w, p.slope);
+        if (p.mask) a *= *(const f32x4*)(p.mask + (size_t)b * p.mask_ld + col);
+        v = ok ? a : f32x4{0.f, 0.f, 0.f, 0.f};  // pixels past the split must add 0
       }
       r[i] = v;
     }
