@@ -52,7 +52,7 @@ struct ConvActP {  // im2col of NHWC activations; rows = pixels, K = (tap, chann
   const float* scale;  // prologue (1x1 fwd only): lrelu(v*scale+shift)*mask
   const float* shift;
   const float* mask;
-  int mask_ld;
+  int mask_ld, mask_on;
   float slope;
 };
 
@@ -107,7 +107,9 @@ struct ConvActLoader {  // MK image
     for (int i = 0; i < NPT; ++i) {
       int yy = py[i] + dy, xx = px[i] + dx;
       bool ok = ((unsigned)yy < (unsigned)p.H) & ((unsigned)xx < (unsigned)p.W);
-      uint32_t off = ok ? (uint32_t)((rel[i] + shift) * p.ld + c) * 4u : OOB;
+      // OR-ing the OOB bit (not a select of two addresses) keeps this
+      // straight-line: no exec-masked region splitting the K-loop block
+      uint32_t off = ((uint32_t)((rel[i] + shift) * p.ld + c) * 4u) | (ok ? 0u : OOB);
       f32x4 v = bload4(rsrc, off);
       if constexpr (PRO) {
         f32x4 a;
@@ -115,7 +117,9 @@ struct ConvActLoader {  // MK image
         a.y = lrelu(v.y * sc.y + sh.y, p.slope);
         a.z = lrelu(v.z * sc.z + sh.z, p.slope);
         a.w = lrelu(v.w * sc.w + sh.w, p.slope);
-        if (p.mask) a *= *(const f32x4*)(p.mask + (size_t)pb[i] * p.mask_ld + c);
+        // mask always readable (host points it at `scale` with ld 0 when absent)
+        const f32x4 mk = *(const f32x4*)(p.mask + (size_t)pb[i] * p.mask_ld + c);
+        a *= p.mask_on ? mk : f32x4{1.f, 1.f, 1.f, 1.f};
         // rows past M only feed masked output rows, but keep them 0 anyway
         v = ok ? a : f32x4{0.f, 0.f, 0.f, 0.f};
       }
@@ -161,7 +165,7 @@ struct RowsKLoader {  // MK / NK image
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       int row = row0 + i * RSTEP;
-      uint32_t off = (n0 + row < p.nrows) ? (uint32_t)(row * p.ldw + k0 + kc) * 4u : OOB;
+      uint32_t off = ((uint32_t)(row * p.ldw + k0 + kc) * 4u) | (n0 + row < p.nrows ? 0u : OOB);
       r[i] = bload4(rsrc, off);
     }
   }
@@ -181,7 +185,7 @@ struct PixRowsP {  // rows = pixels (the GEMM K of wgrad), columns contiguous ch
   const float* scale;  // prologue (1x1 wgrad B operand: recomputed BN+LReLU+dropout)
   const float* shift;
   const float* mask;
-  int mask_ld;
+  int mask_ld, mask_on;
   float slope;
 };
 
@@ -241,7 +245,7 @@ struct PixRowsLoader {  // KM / KN image
         }
         if constexpr (PRO) b = ok ? b : 0;
       }
-      uint32_t off = ok ? (uint32_t)((src - base_pix) * p.ld + col) * 4u : OOB;
+      uint32_t off = ((uint32_t)((src - base_pix) * p.ld + col) * 4u) | (ok ? 0u : OOB);
       f32x4 v = bload4(rsrc, off);
       if constexpr (PRO) {
         f32x4 a;
@@ -249,7 +253,8 @@ struct PixRowsLoader {  // KM / KN image
         a.y = lrelu(v.y * sc.y + sh.y, p.slope);
         a.z = lrelu(v.z * sc.z + sh.z, p.slope);
         a.w = lrelu(v.w * sc.w + sh.w, p.slope);
-        if (p.mask) a *= *(const f32x4*)(p.mask + (size_t)b * p.mask_ld + col);
+        const f32x4 mk = *(const f32x4*)(p.mask + (size_t)b * p.mask_ld + col);
+        a *= p.mask_on ? mk : f32x4{1.f, 1.f, 1.f, 1.f};
         v = ok ? a : f32x4{0.f, 0.f, 0.f, 0.f};  // pixels past the split must add 0
       }
       r[i] = v;
@@ -468,24 +473,23 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
   __syncthreads();
 
   const int arb = wm * TM * 32, brb = wn * TN * 32;
+  // One basic block per K-slab: the next slab's loads are issued
+  // unconditionally (on the last slab they hit the zero-fill / stay inside the
+  // descriptor range and land in the idle LDS stage), so the scheduler can
+  // interleave them, the LDS fragment reads and the MFMAs freely; the
+  // sched_group_barrier sequence below pins that interleave.
   for (int it = 0; it < nk; ++it) {
     const float* As = lds + (it & 1) * STAGE;
     const float* Bs = As + A_SZ;
-    const bool more = it + 1 < nk;
-    if (more) {
-      a.advance(ap);
-      b.advance(bp);
-      a.load(ap, ar);
-      b.load(bp, br);
-    }
-    // fragments of group j+1 are read while group j's MFMAs issue (register
-    // double buffer; all indices compile-time after unrolling)
+    a.advance(ap);
+    b.advance(bp);
     float fa[2][TM][4], fb[2][TN][4];
 #pragma unroll
     for (int tm = 0; tm < TM; ++tm) read_frag<AL::KM, BM>(As, arb + tm * 32, lane, 0, fa[0][tm]);
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) read_frag<BL::KM, BN>(Bs, brb + tn * 32, lane, 0, fb[0][tn]);
-    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+    a.load(ap, ar);
+    b.load(bp, br);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int cur = j & 1;
@@ -505,15 +509,28 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
           for (int tn = 0; tn < TN; ++tn)
             acc[tm][tn] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[cur][tm][q], fb[cur][tn][q],
                                                                acc[tm][tn], 0, 0, 0);
-      // pin the order: group j+1's LDS reads, then group j's MFMAs
-      if (j < 3) __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
-      __builtin_amdgcn_sched_group_barrier(0x008, 4 * TM * TN, 0);
     }
-    if (more) {
-      float* An = lds + ((it + 1) & 1) * STAGE;
-      a.store(An, ar);
-      b.store(An + A_SZ, br);
+    float* An = lds + ((it + 1) & 1) * STAGE;
+    a.store(An, ar);
+    b.store(An + A_SZ, br);
+    // ---- pinned interleave (LLVM SchedGroupMask: VALU 0x2, MFMA 0x8,
+    //      VMEM_READ 0x20, DS_READ 0x100, DS_WRITE 0x200) ----
+    constexpr int NMF = 4 * TM * TN;               // MFMAs per fragment group
+    constexpr int NLD = AL::NPT + BL::NPT;         // global loads per slab
+    __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);  // group-0 fragments
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int m = 0; m < NMF; ++m) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (j == 0 && m < NLD) {
+          __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+          __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+        }
+        if (j < 3 && m < 8) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      }
     }
+    __builtin_amdgcn_sched_group_barrier(0x200, 16, 0);
     __syncthreads();
   }
   EpiCtx cx{m0, n0, m0 + arb, n0 + brb, wm, wn, lane, lds};
@@ -765,8 +782,9 @@ extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, 
   ap.fdH = make_fastdiv(H);
   ap.scale = pro_scale;
   ap.shift = pro_shift;
-  ap.mask = pro_mask;
-  ap.mask_ld = cin_p;
+  ap.mask = pro_mask ? pro_mask : pro_scale;
+  ap.mask_ld = pro_mask ? cin_p : 0;
+  ap.mask_on = pro_mask != nullptr;
   ap.slope = slope;
   int K = ksize * ksize * cin_p;
   RowsKP bp{wpk, K, cout_p};
@@ -818,8 +836,9 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
   bp.ksize = ksize;
   bp.scale = pro_scale;
   bp.shift = pro_shift;
-  bp.mask = pro_mask;
-  bp.mask_ld = cin_p;
+  bp.mask = pro_mask ? pro_mask : pro_scale;
+  bp.mask_ld = pro_mask ? cin_p : 0;
+  bp.mask_on = pro_mask != nullptr;
   bp.slope = slope;
   EpiSlabP ep{ws};
   hipStream_t s = as_stream(stream);
