@@ -54,6 +54,42 @@ def unet_fwd_flops(in_ch, H, W):
     return f
 
 
+STAGES = ["conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv8", "conv9", "head"]
+
+
+def stage_work(in_ch, H, W, B, bytes_per=4):
+    """Algorithmic FLOPs and HBM bytes per stage for one train step (SURVEY.md
+    §8(d) definitions: conv FLOPs 2*H*W*Cin*Cout*k^2; bytes = (Cin+Cout)*H*W*s
+    + weights*s per conv; backward = 2x forward for both)."""
+    R = (H // 2, W // 2)
+    ch = {2: (4 * in_ch, 64), 3: (64, 128), 4: (128, 512), 5: (512, 1024),
+          6: (1024, 512), 7: (512, 128), 8: (128, 64), 9: (64, 16)}
+    res = {2: R, 3: (R[0] // 2, R[1] // 2), 4: (R[0] // 4, R[1] // 4), 5: (R[0] // 8, R[1] // 8),
+           6: (R[0] // 4, R[1] // 4), 7: (R[0] // 2, R[1] // 2), 8: R, 9: R}
+    out = {}
+    for k, (ci, co) in ch.items():
+        h, w = res[k]
+        px = B * h * w
+        f = 2.0 * px * (ci * ci * 9 + ci * co)
+        by = ((ci + ci) * px + 9 * ci * ci + (ci + co) * px + ci * co) * bytes_per
+        out[f"conv{k}"] = (f, by)
+    px = B * R[0] * R[1]
+    out["head"] = (2.0 * px * 16 * 4, (16 * px + 4 * px) * bytes_per)
+    return out
+
+
+def load_traffic():
+    """HBM bytes per launch of the dominant kernel from the committed rocprofv3
+    PMC summary (FETCH_SIZE x2 per the gfx950 calibration + WRITE_SIZE)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_conv6_fwd.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        t = json.load(f)
+    return t.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+
+
 def cpu_baseline(in_ch, H, W, frames=1, reps=3):
     """Oracle restatement (same ATen ops as the reference) fp32 fwd+bwd on the
     host cores: frames/s on a bounded sample (`frames` frames x `reps`)."""
@@ -138,6 +174,9 @@ def main():
 
     probe_tag = "conv6.conv.0.fwd"
     nops.PROBES[probe_tag] = []
+    for st in STAGES:
+        nops.PROBES[st + ".fwd"] = []
+        nops.PROBES[st + ".bwd"] = []
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -155,6 +194,23 @@ def main():
         elapsed = float(t.item())
     evs = nops.PROBES.pop(probe_tag)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else float("nan")
+    stage_rows = []
+    work = stage_work(C, H, W, B)
+    for st in STAGES:
+        fw = nops.PROBES.pop(st + ".fwd")
+        bw = nops.PROBES.pop(st + ".bwd")
+        if not fw or not bw:
+            continue
+        t_ms = (np.mean([a.elapsed_time(b) for a, b in fw]) + np.mean([a.elapsed_time(b) for a, b in bw]))
+        fl, by = work[st]
+        tf = 3 * fl / (t_ms * 1e-3) / 1e12
+        gbs = 3 * by / (t_ms * 1e-3) / 1e9
+        ai = fl / by
+        stage_rows.append({"stage": st, "ms": round(float(t_ms), 3), "tflops": round(tf, 2),
+                           "mfma_frac": round(tf / FP32_PEAK_TFLOPS, 3), "gbs": round(gbs, 1),
+                           "hbm_frac": round(gbs / HBM_PEAK_GBS, 3), "flop_per_byte": round(ai, 1),
+                           "bound": "mfma" if ai > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9) else "hbm"})
+    traffic, traffic_src = load_traffic()
 
     frames = world * B * args.steps
     value = frames / elapsed
@@ -185,7 +241,10 @@ def main():
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                      "avg_launch_ms": round(kern_ms, 4), "launches": len(evs),
-                     "algorithmic_flops_per_launch": k_flops, "traffic": None},
+                     "algorithmic_flops_per_launch": k_flops,
+                     "algorithmic_bytes_per_launch": (2 * B * (Rh // 4) ** 2 * 1024 + 9 * 1024 * 1024) * 4,
+                     "traffic": traffic, "traffic_source": traffic_src},
+        "stages": stage_rows,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(C, H, W)

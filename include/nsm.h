@@ -70,6 +70,20 @@ int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, int cin_p, 
                        const float* pro_scale, const float* pro_shift, const float* pro_mask,
                        float slope, float* stats, void* stream);
 
+/* Winograd F(2x2,3x3) 3x3 convolution (same padding 1) for deep layers:
+ * nsm_wino_weight transforms w[co][ci][3][3] into U[16][n_p][k_p] (flip=0:
+ * forward, n=co, k=ci; flip=1: input-gradient, n=ci, k=co, filter rotated
+ * 180 deg); nsm_conv3x3_wino then computes y = conv(x, W) + bias through
+ * 16 batched MFMA GEMMs, using nsm_wino_ws() floats of workspace.
+ * Replaces the same F.conv2d 3x3 / ConvolutionBackward dgrad as nsm_conv_fwd
+ * (Unetmodel.py:21) with 2.25x fewer multiplies. */
+size_t nsm_wino_ws(int B, int H, int W, int cin_p, int cout_p);
+int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k_p, int flip, float* U,
+                    void* stream);
+int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p, const float* U,
+                     const float* bias, int cout_p, float* y, int ldy, float* ws, size_t ws_floats,
+                     void* stream);
+
 /* nsm_conv_wgrad: dw[co][ci][kh][kw] (real cout x cin, reference layout) =
  *   sum_p dy[p][co] * pro(x[p+off(tap)][ci]); deterministic split-K over
  *   pixels through `ws` (nsm_conv_wgrad_ws() floats). Replaces the weight
@@ -129,6 +143,13 @@ int nsm_resize_fwd(const float* x, int B, int Hi, int Wi, int C, float* y, int H
                    void* stream);
 int nsm_resize_bwd(const float* dy, int B, int Hi, int Wi, int C, float* dx, int Ho, int Wo,
                    void* stream);
+
+/* up x2 then resize to (th,tw) in one pass (Unetmodel.py:140-141: up9 then
+ * _upsample_and_match back to the skip size); no 4x intermediate. */
+int nsm_up2_resize_fwd(const float* x, int B, int h, int w, int C, float* y, int th, int tw,
+                       void* stream);
+int nsm_up2_resize_bwd(const float* dy, int B, int h, int w, int C, float* dx, int th, int tw,
+                       void* stream);
 
 /* ---- model boundary ---------------------------------------------------------
  * pixel_unshuffle(2) + NCHW->NHWC + channel pad (Unetmodel.py:65-67,101) */

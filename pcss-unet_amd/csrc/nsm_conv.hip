@@ -142,6 +142,7 @@ struct ConvActLoader {  // MK image
 struct RowsKP {  // dense rows with contiguous K (packed weights); rows >= nrows are zero
   const float* w;
   int ldw, nrows;
+  long long bstride;  // floats between batch entries (Winograd: one GEMM per xi = blockIdx.z)
 };
 
 template <int R, int NT>
@@ -159,7 +160,8 @@ struct RowsKLoader {  // MK / NK image
     row0 = tid >> 3;
     k0 = kbeg;
     n0 = n0_;
-    rsrc = make_rsrc(p.w + (size_t)n0 * p.ldw, (long long)(p.nrows - n0) * p.ldw);
+    const float* base = p.w + (size_t)blockIdx.z * p.bstride;
+    rsrc = make_rsrc(base + (size_t)n0 * p.ldw, (long long)(p.nrows - n0) * p.ldw);
   }
   __device__ void load(const RowsKP& p, f32x4* r) const {
 #pragma unroll
@@ -301,6 +303,7 @@ struct EpiStoreP {
   int ldy;
   const float* bias;
   float* stats;  // optional BN partials [gridDim.x][2][N]: {sum, M2 about block mean}
+  long long bstride;  // batched GEMM (Winograd): output offset per blockIdx.z
 };
 struct EpiStore {
   using P = EpiStoreP;
@@ -308,6 +311,7 @@ struct EpiStore {
   __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
                                int) {
     const int col = cx.lane & 31, h = cx.lane >> 5;
+    float* yb = e.y + (size_t)blockIdx.z * e.bstride;
     float bv[TN];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
@@ -327,7 +331,7 @@ struct EpiStore {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           int m = cx.mb + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (m < M) e.y[(size_t)m * e.ldy + n] = acc[tm][tn][i];
+          if (m < M) yb[(size_t)m * e.ldy + n] = acc[tm][tn][i];
         }
       }
     }
@@ -435,7 +439,7 @@ struct EpiSlab {
 // registers on keeping LDS reads in flight instead of maximising occupancy.
 template <int BM, int BN, int WM, int WN, class AL, class BL, class EP, class AP, class BP>
 __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(1, 2)))
-    gemm_f32_kernel(AP ap, BP bp, typename EP::P ep, int M, int N, int K, int kchunk) {
+    gemm_f32_kernel(AP ap, BP bp, typename EP::P ep, int M, int N, int K, int kchunk, int batched) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   constexpr int A_SZ = AL::LDS_FLOATS, B_SZ = BL::LDS_FLOATS, STAGE = A_SZ + B_SZ;
@@ -443,7 +447,7 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, split = blockIdx.z;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, split = batched ? 0 : blockIdx.z;
   const int kbeg = split * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int nk = (kend - kbeg + BK - 1) / BK;
@@ -548,7 +552,7 @@ static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const EpiStoreP
   using BL = RowsKLoader<BN, NT>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 1);
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiStore, ConvActP, RowsKP>), grid,
-                     dim3(NT), 0, s, ap, bp, ep, M, N, K, K);
+                     dim3(NT), 0, s, ap, bp, ep, M, N, K, K, 0);
   NSM_LAUNCH_CHECK("conv_fwd");
   return 0;
 }
@@ -590,7 +594,7 @@ static int launch_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& 
   using BL = PixRowsLoader<BN, NT, SHIFT, PRO>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), splits);
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlab, PixRowsP, PixRowsP>), grid,
-                     dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk);
+                     dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, 0);
   NSM_LAUNCH_CHECK("conv_wgrad");
   return 0;
 }
@@ -719,6 +723,153 @@ __global__ void pad_vec_kernel(const float* __restrict__ v, int n, int n_p, floa
   if (i < n_p) out[i] = i < n ? v[i] : 0.f;
 }
 
+// ===========================================================================
+// Winograd F(2x2,3x3) for the deep 3x3 convolutions (fwd and dgrad).
+//   V[xi][t][c]  = (B^T d B)   input tile d = 4x4 window at (2ty-1, 2tx-1)
+//   U[xi][n][k]  = (G g G^T)   g = 3x3 filter of (out n, in k)
+//   M[xi][t][n]  = sum_k V[xi][t][k] U[xi][n][k]     (16 batched MFMA GEMMs)
+//   Y(2x2 tile)  = A^T M A  (+ bias)
+// 16 multiplies per 4 outputs instead of 36: 2.25x fewer MFMA flops, same fp32
+// arithmetic (the transforms are adds and exact halvings).
+// ===========================================================================
+__global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int cin, int n_p,
+                                   int k_p, int flip, float* __restrict__ U) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n_p * k_p) return;
+  const int k = idx % k_p, n = idx / k_p;
+  // fwd: n = co, k = ci, g = w[co][ci];  dgrad: n = ci, k = co, g = rot180(w[co][ci])
+  const int co = flip ? k : n, ci = flip ? n : k;
+  float g[3][3];
+  const bool ok = co < cout && ci < cin;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const int sa = flip ? 2 - a : a, sb = flip ? 2 - b : b;
+      g[a][b] = ok ? w[((size_t)co * cin + ci) * 9 + sa * 3 + sb] : 0.f;
+    }
+  float t[4][3];  // G g
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    t[0][b] = g[0][b];
+    t[1][b] = 0.5f * (g[0][b] + g[1][b] + g[2][b]);
+    t[2][b] = 0.5f * (g[0][b] - g[1][b] + g[2][b]);
+    t[3][b] = g[2][b];
+  }
+  const size_t plane = (size_t)n_p * k_p;
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const float u[4] = {t[a][0], 0.5f * (t[a][0] + t[a][1] + t[a][2]),
+                        0.5f * (t[a][0] - t[a][1] + t[a][2]), t[a][2]};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) U[(a * 4 + b) * plane + (size_t)n * k_p + k] = u[b];
+  }
+}
+
+__global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict__ x, int ld, int H,
+                                                         int W, int C, int TH, int TW, long long T,
+                                                         float* __restrict__ V) {
+  const int C4 = C / 4;
+  const long long total = T * C4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const long long t = i / C4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    f32x4 d[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int yy = 2 * ty - 1 + a;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int xx = 2 * tx - 1 + e;
+        d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                      ? *(const f32x4*)(x + ((size_t)(b * H + yy) * W + xx) * ld + c)
+                      : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    f32x4 s[4][4];  // B^T d
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      s[0][e] = d[0][e] - d[2][e];
+      s[1][e] = d[1][e] + d[2][e];
+      s[2][e] = d[2][e] - d[1][e];
+      s[3][e] = d[1][e] - d[3][e];
+    }
+    const size_t plane = (size_t)T * C;
+    float* out = V + (size_t)t * C + c;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      *(f32x4*)(out + (a * 4 + 0) * plane) = s[a][0] - s[a][2];
+      *(f32x4*)(out + (a * 4 + 1) * plane) = s[a][1] + s[a][2];
+      *(f32x4*)(out + (a * 4 + 2) * plane) = s[a][2] - s[a][1];
+      *(f32x4*)(out + (a * 4 + 3) * plane) = s[a][1] - s[a][3];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
+                                                          int W, int TH, int TW, long long T,
+                                                          const float* __restrict__ bias,
+                                                          float* __restrict__ y, int ldy) {
+  const int N4 = N / 4;
+  const long long total = T * N4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % N4) * 4;
+    const long long t = i / N4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    const size_t plane = (size_t)T * N;
+    const float* in = Mb + (size_t)t * N + c;
+    f32x4 f[2][4];  // A^T M
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f32x4 m0 = *(const f32x4*)(in + (0 * 4 + e) * plane);
+      const f32x4 m1 = *(const f32x4*)(in + (1 * 4 + e) * plane);
+      const f32x4 m2 = *(const f32x4*)(in + (2 * 4 + e) * plane);
+      const f32x4 m3 = *(const f32x4*)(in + (3 * 4 + e) * plane);
+      f[0][e] = m0 + m1 + m2;
+      f[1][e] = m1 - m2 - m3;
+    }
+    const f32x4 bv = bias ? *(const f32x4*)(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+      const int yy = 2 * ty + a;
+      if (yy >= H) continue;
+      const f32x4 o0 = f[a][0] + f[a][1] + f[a][2] + bv;
+      const f32x4 o1 = f[a][1] - f[a][2] - f[a][3] + bv;
+      float* row = y + ((size_t)(b * H + yy) * W + 2 * tx) * ldy + c;
+      *(f32x4*)row = o0;
+      if (2 * tx + 1 < W) *(f32x4*)(row + ldy) = o1;
+    }
+  }
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_wino_gemm(const RowsKP& ap, const RowsKP& bp, const EpiStoreP& ep, int M, int N,
+                            int K, hipStream_t s) {
+  constexpr int NT = WM * WN * 64;
+  using AL = RowsKLoader<BM, NT>;
+  using BL = RowsKLoader<BN, NT>;
+  dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 16);
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiStore, RowsKP, RowsKP>), grid,
+                     dim3(NT), 0, s, ap, bp, ep, M, N, K, K, 1);
+  NSM_LAUNCH_CHECK("wino_gemm");
+  return 0;
+}
+
+static int grid_1d(long long work) {
+  long long g = (work + 255) / 256;
+  if (g > 16384) g = 16384;
+  return (int)(g < 1 ? 1 : g);
+}
+
 }  // namespace nsm
 
 using namespace nsm;
@@ -787,8 +938,8 @@ extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, 
   ap.mask_on = pro_mask != nullptr;
   ap.slope = slope;
   int K = ksize * ksize * cin_p;
-  RowsKP bp{wpk, K, cout_p};
-  EpiStoreP ep{y, ldy, bias, stats};
+  RowsKP bp{wpk, K, cout_p, 0};
+  EpiStoreP ep{y, ldy, bias, stats, 0};
   hipStream_t s = as_stream(stream);
   if (pro_scale) return dispatch_conv_fwd<true>(ap, bp, ep, (int)Ml, cout_p, K, s);
   return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s);
@@ -868,5 +1019,58 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(cin, 64), cout), dim3(256), 0, s, red_src,
                      red_splits, M, N, cin_p, taps, cin, cout, dw);
   NSM_LAUNCH_CHECK("conv_wgrad reduce");
+  return 0;
+}
+
+extern "C" size_t nsm_wino_ws(int B, int H, int W, int cin_p, int cout_p) {
+  const long long T = (long long)B * ((H + 1) / 2) * ((W + 1) / 2);
+  return (size_t)16 * T * (cin_p + cout_p);
+}
+
+extern "C" int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k_p, int flip,
+                               float* U, void* stream) {
+  NSM_CHECK_ARG(w && U && n_p % 32 == 0 && k_p % 32 == 0, "wino_weight: bad args");
+  NSM_CHECK_ARG(flip ? (n_p >= cin && k_p >= cout) : (n_p >= cout && k_p >= cin),
+                "wino_weight: padded dims too small");
+  hipLaunchKernelGGL(wino_weight_kernel, dim3(ceil_div(n_p * k_p, 256)), dim3(256), 0,
+                     as_stream(stream), w, cout, cin, n_p, k_p, flip, U);
+  NSM_LAUNCH_CHECK("wino_weight");
+  return 0;
+}
+
+extern "C" int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p,
+                                const float* U, const float* bias, int cout_p, float* y, int ldy,
+                                float* ws, size_t ws_floats, void* stream) {
+  NSM_CHECK_ARG(x && U && y && ws, "conv3x3_wino: null pointer");
+  NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0 && ldx % 4 == 0 && ldy % 4 == 0,
+                "conv3x3_wino: channels must be x32");
+  const int TH = (H + 1) / 2, TW = (W + 1) / 2;
+  const long long T = (long long)B * TH * TW;
+  NSM_CHECK_ARG(T < (1ll << 30), "conv3x3_wino: too many tiles");
+  if (ws_floats < nsm_wino_ws(B, H, W, cin_p, cout_p))
+    return fail(NSM_E_WS, "conv3x3_wino: workspace too small");
+  hipStream_t s = as_stream(stream);
+  float* V = ws;
+  float* Mb = ws + (size_t)16 * T * cin_p;
+  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_1d(T * cin_p / 4)), dim3(256), 0, s, x, ldx, H, W,
+                     cin_p, TH, TW, T, V);
+  NSM_LAUNCH_CHECK("wino_input");
+  RowsKP ap{V, cin_p, (int)T, T * cin_p};
+  RowsKP bp{U, cin_p, cout_p, (long long)cout_p * cin_p};
+  EpiStoreP ep{Mb, cout_p, nullptr, nullptr, T * cout_p};
+  const int M = (int)T, N = cout_p, K = cin_p;
+  int rc;
+  long long mb128 = ceil_div(M, 128);
+  if (N >= 128)
+    rc = (mb128 * ceil_div(N, 128) * 16 >= 1024) ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, s)
+                                                  : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, s);
+  else if (N >= 64)
+    rc = launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, s);
+  else
+    rc = launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, s);
+  if (rc) return rc;
+  hipLaunchKernelGGL(wino_output_kernel, dim3(grid_1d(T * cout_p / 4)), dim3(256), 0, s, Mb, cout_p,
+                     H, W, TH, TW, T, bias, y, ldy);
+  NSM_LAUNCH_CHECK("wino_output");
   return 0;
 }

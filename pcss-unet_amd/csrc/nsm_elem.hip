@@ -452,6 +452,106 @@ __global__ void resize_bwd_kernel(const float* __restrict__ dy, int B, int Hi, i
 }
 
 // ---------------------------------------------------------------------------
+// Composite: nn.Upsample(x2) to (2h,2w) followed by _upsample_and_match to
+// (th,tw) (Unetmodel.py:140-141, the up9 "blur"), without materialising the
+// 4x intermediate. Forward evaluates the up-sampled values exactly as the
+// two-step path rounds them (fp32 per intermediate sample); backward uses the
+// separable combined weights W[o->i] = sum_m w2(o->m) w1(m->i).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ f32x4 up_sample4(const float* __restrict__ x, size_t rb, int h, int w,
+                                            int C, int c4, float s1h, float s1w, int my, int mx) {
+  int y0, y1, x0, x1;
+  float a0, a1, b0, b1;
+  lin_idx(s1h, my, h, y0, y1, a0, a1);
+  lin_idx(s1w, mx, w, x0, x1, b0, b1);
+  const f32x4 v00 = *(const f32x4*)(x + ((rb + y0) * w + x0) * C + c4 * 4);
+  const f32x4 v01 = *(const f32x4*)(x + ((rb + y0) * w + x1) * C + c4 * 4);
+  const f32x4 v10 = *(const f32x4*)(x + ((rb + y1) * w + x0) * C + c4 * 4);
+  const f32x4 v11 = *(const f32x4*)(x + ((rb + y1) * w + x1) * C + c4 * 4);
+  return a0 * (b0 * v00 + b1 * v01) + a1 * (b0 * v10 + b1 * v11);
+}
+
+__global__ void up2_resize_fwd_kernel(const float* __restrict__ x, int B, int h, int w, int C,
+                                      float* __restrict__ y, int th, int tw, float s1h, float s1w,
+                                      float s2h, float s2w) {
+  const int C4 = C / 4, h2 = 2 * h, w2 = 2 * w;
+  long long total = (long long)B * th * tw * C4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C4);
+    long long t = i / C4;
+    int ox = (int)(t % tw);
+    t /= tw;
+    int oy = (int)(t % th);
+    int b = (int)(t / th);
+    int m0, m1, n0, n1;
+    float l0, l1, k0, k1;
+    lin_idx(s2h, oy, h2, m0, m1, l0, l1);
+    lin_idx(s2w, ox, w2, n0, n1, k0, k1);
+    const size_t rb = (size_t)b * h;
+    f32x4 u00 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m0, n0);
+    f32x4 u01 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m0, n1);
+    f32x4 u10 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m1, n0);
+    f32x4 u11 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m1, n1);
+    *(f32x4*)(y + (size_t)i * 4) = l0 * (k0 * u00 + k1 * u01) + l1 * (k0 * u10 + k1 * u11);
+  }
+}
+
+// combined 1-D weight of final output index o on input index i
+__device__ __forceinline__ float comb_w(float s2, int o, int n2, float s1, int n1, int i) {
+  int m0, m1;
+  float l0, l1;
+  lin_idx(s2, o, n2, m0, m1, l0, l1);
+  float wgt = 0.f;
+  if (l0 != 0.f) wgt += l0 * lin_w(s1, m0, n1, i);
+  if (l1 != 0.f) wgt += l1 * lin_w(s1, m1, n1, i);
+  return wgt;
+}
+
+__global__ void up2_resize_bwd_kernel(const float* __restrict__ dy, int B, int h, int w, int C,
+                                      float* __restrict__ dx, int th, int tw, float s1h, float s1w,
+                                      float s2h, float s2w) {
+  const int C4 = C / 4, h2 = 2 * h, w2 = 2 * w;
+  long long total = (long long)B * h * w * C4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C4);
+    long long t = i / C4;
+    int ix = (int)(t % w);
+    t /= w;
+    int iy = (int)(t % h);
+    int b = (int)(t / h);
+    // intermediate rows touching iy, then final rows touching those
+    int mlo, mhi, olo, ohi, olo2, ohi2;
+    cand_range(s1h, iy, h2, mlo, mhi);
+    cand_range(s2h, mlo, th, olo, ohi2);
+    cand_range(s2h, mhi, th, olo2, ohi);
+    olo = min(olo, olo2);
+    ohi = max(ohi, ohi2);
+    int nlo, nhi, plo, phi, plo2, phi2;
+    cand_range(s1w, ix, w2, nlo, nhi);
+    cand_range(s2w, nlo, tw, plo, phi2);
+    cand_range(s2w, nhi, tw, plo2, phi);
+    plo = min(plo, plo2);
+    phi = max(phi, phi2);
+    float wx[24];
+    int nx = 0;
+    for (int ox = plo; ox <= phi && nx < 24; ++ox) wx[nx++] = comb_w(s2w, ox, w2, s1w, w, ix);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int oy = olo; oy <= ohi; ++oy) {
+      float wy = comb_w(s2h, oy, h2, s1h, h, iy);
+      if (wy == 0.f) continue;
+      const float* row = dy + ((size_t)b * th + oy) * tw * C + c * 4;
+      for (int k = 0; k < nx; ++k) {
+        if (wx[k] == 0.f) continue;
+        acc += (wy * wx[k]) * *(const f32x4*)(row + (size_t)(plo + k) * C);
+      }
+    }
+    *(f32x4*)(dx + (size_t)i * 4) = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Model boundary: pixel_unshuffle(2) + NCHW->NHWC (+ zero channel pad), and its
 // inverse for the input gradient.
 // ---------------------------------------------------------------------------
@@ -478,18 +578,23 @@ __global__ void input_prep_kernel(const float* __restrict__ x, int B, int C, int
 
 __global__ void input_grad_kernel(const float* __restrict__ dX, int B, int C, int H, int W, int cp,
                                   float* __restrict__ dx) {
+  // thread per (b, c, ry, rx): one float4 of dX (channels 4c..4c+3 of pixel
+  // (ry,rx)) -> the 2x2 block of plane c; rx fastest so stores coalesce.
   const int Rh = H / 2, Rw = W / 2;
-  long long total = (long long)B * C * H * W;
+  long long total = (long long)B * C * Rh * Rw;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int xx = (int)(i % W);
-    long long t = i / W;
-    int yy = (int)(t % H);
-    t /= H;
+    int rx = (int)(i % Rw);
+    long long t = i / Rw;
+    int ry = (int)(t % Rh);
+    t /= Rh;
     int c = (int)(t % C);
     int b = (int)(t / C);
-    int ch = 4 * c + 2 * (yy & 1) + (xx & 1);
-    dx[i] = dX[(((size_t)b * Rh + (yy >> 1)) * Rw + (xx >> 1)) * cp + ch];
+    f32x4 v = *(const f32x4*)(dX + (((size_t)b * Rh + ry) * Rw + rx) * cp + 4 * c);
+    float* o = dx + (((size_t)b * C + c) * H + 2 * ry) * W + 2 * rx;
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    *(f32x2*)o = f32x2{v.x, v.y};
+    *(f32x2*)(o + W) = f32x2{v.z, v.w};
   }
 }
 
@@ -936,6 +1041,32 @@ extern "C" int nsm_resize_bwd(const float* dy, int B, int Hi, int Wi, int C, flo
   return 0;
 }
 
+extern "C" int nsm_up2_resize_fwd(const float* x, int B, int h, int w, int C, float* y, int th,
+                                  int tw, void* stream) {
+  NSM_CHECK_ARG(x && y && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 4 == 0,
+                "up2_resize_fwd: bad args");
+  long long work = (long long)B * th * tw * (C / 4);
+  hipLaunchKernelGGL(up2_resize_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                     x, B, h, w, C, y, th, tw, ac_scale(h, 2 * h), ac_scale(w, 2 * w),
+                     ac_scale(2 * h, th), ac_scale(2 * w, tw));
+  NSM_LAUNCH_CHECK("up2_resize_fwd");
+  return 0;
+}
+
+extern "C" int nsm_up2_resize_bwd(const float* dy, int B, int h, int w, int C, float* dx, int th,
+                                  int tw, void* stream) {
+  NSM_CHECK_ARG(dy && dx && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 4 == 0,
+                "up2_resize_bwd: bad args");
+  // the combined-weight gather assumes a downsizing second step of at most ~2x
+  NSM_CHECK_ARG(th * 3 >= 2 * h && tw * 3 >= 2 * w, "up2_resize_bwd: target too small");
+  long long work = (long long)B * h * w * (C / 4);
+  hipLaunchKernelGGL(up2_resize_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
+                     dy, B, h, w, C, dx, th, tw, ac_scale(h, 2 * h), ac_scale(w, 2 * w),
+                     ac_scale(2 * h, th), ac_scale(2 * w, tw));
+  NSM_LAUNCH_CHECK("up2_resize_bwd");
+  return 0;
+}
+
 extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, float* out, int cp,
                               void* stream) {
   NSM_CHECK_ARG(x && out && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C, "input_prep: bad args");
@@ -948,8 +1079,9 @@ extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, float*
 
 extern "C" int nsm_input_grad(const float* dX, int B, int C, int H, int W, int cp, float* dx,
                               void* stream) {
-  NSM_CHECK_ARG(dX && dx && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C, "input_grad: bad args");
-  long long work = (long long)B * C * H * W;
+  NSM_CHECK_ARG(dX && dx && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C && cp % 4 == 0,
+                "input_grad: bad args");
+  long long work = (long long)B * C * (H / 2) * (W / 2);
   hipLaunchKernelGGL(input_grad_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), dX,
                      B, C, H, W, cp, dx);
   NSM_LAUNCH_CHECK("input_grad");

@@ -27,6 +27,9 @@ _SIGS = {
     "nsm_conv_fwd": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P]),
     "nsm_conv_stat_rows": (I, [I, I, I, I]),
     "nsm_conv_fwd_stats": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
+    "nsm_wino_ws": (Z, [I, I, I, I, I]),
+    "nsm_wino_weight": (I, [P, I, I, I, I, I, P, P]),
+    "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, P, I, P, Z, P]),
     "nsm_conv_wgrad_ws": (Z, [I, I, I, I, I, I]),
     "nsm_conv_wgrad": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
     "nsm_reduce_chunks": (I, [I, I]),
@@ -42,6 +45,8 @@ _SIGS = {
     "nsm_avgpool2_bwd_add": (I, [P, I, I, I, I, P, P, P]),
     "nsm_resize_fwd": (I, [P, I, I, I, I, P, I, I, P]),
     "nsm_resize_bwd": (I, [P, I, I, I, I, P, I, I, P]),
+    "nsm_up2_resize_fwd": (I, [P, I, I, I, I, P, I, I, P]),
+    "nsm_up2_resize_bwd": (I, [P, I, I, I, I, P, I, I, P]),
     "nsm_input_prep": (I, [P, I, I, I, I, P, I, P]),
     "nsm_input_grad": (I, [P, I, I, I, I, I, P, P]),
     "nsm_head_fwd": (I, [P, I, I, I, I, P, P, P, P]),

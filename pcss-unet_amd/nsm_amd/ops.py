@@ -62,6 +62,26 @@ class Partials:
         self.buf, self.nchunk, self.rpc = buf, nchunk, rpc
 
 
+class stage:
+    """Context manager: if `tag` is registered in PROBES, bracket everything
+    launched inside with HIP events on the current stream (bench.py uses it
+    for the per-stage roofline table)."""
+    __slots__ = ("tag", "end")
+
+    def __init__(self, tag):
+        self.tag = tag
+        self.end = None
+
+    def __enter__(self):
+        self.end = _probe(self.tag)
+        return self
+
+    def __exit__(self, *exc):
+        if self.end is not None:
+            self.end.record()
+        return False
+
+
 def conv_fwd(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None):
     """x: [B*H*W, cin_p]; returns y [B*H*W, cout_p]. pro=(scale, shift, mask|None)."""
     return conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro, out, tag, stats=False)[0]
@@ -89,6 +109,30 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
     if ev is not None:
         ev.record()
     return y, part
+
+
+def wino_weight(w, n_p, k_p, flip):
+    """Winograd-domain filters U[16][n_p][k_p] of a 3x3 conv weight
+    (flip=False: forward; flip=True: input-gradient of that conv)."""
+    cout, cin = w.shape[0], w.shape[1]
+    U = empty(16 * n_p * k_p, device=w.device)
+    call("nsm_wino_weight", ptr(w), cout, cin, n_p, k_p, int(flip), ptr(U), stream())
+    return U
+
+
+def conv3x3_wino(x, B, H, W, U, bias, cout_p, tag=None):
+    """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(2x2,3x3)."""
+    from ._lib import lib
+    M, cin_p = x.shape
+    n = int(lib.nsm_wino_ws(B, H, W, cin_p, cout_p))
+    ws = empty(n, device=x.device)
+    y = empty(M, cout_p, device=x.device)
+    ev = _probe(tag)
+    call("nsm_conv3x3_wino", ptr(x), x.stride(0), B, H, W, cin_p, ptr(U), ptr(bias), cout_p, ptr(y),
+         y.stride(0), ptr(ws), n, stream())
+    if ev is not None:
+        ev.record()
+    return y
 
 
 def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None):
@@ -234,6 +278,21 @@ def resize_bwd(dy, B, Hi, Wi, Ho, Wo):
     C = dy.shape[-1]
     dx = empty(B * Hi * Wi, C, device=dy.device)
     call("nsm_resize_bwd", ptr(dy), B, Hi, Wi, C, ptr(dx), Ho, Wo, stream())
+    return dx
+
+
+def up2_resize(x, B, h, w, th, tw):
+    """bilinear x2 (align_corners) then resize to (th, tw), one pass."""
+    C = x.shape[-1]
+    y = empty(B * th * tw, C, device=x.device)
+    call("nsm_up2_resize_fwd", ptr(x), B, h, w, C, ptr(y), th, tw, stream())
+    return y
+
+
+def up2_resize_bwd(dy, B, h, w, th, tw):
+    C = dy.shape[-1]
+    dx = empty(B * h * w, C, device=dy.device)
+    call("nsm_up2_resize_bwd", ptr(dy), B, h, w, C, ptr(dx), th, tw, stream())
     return dx
 
 

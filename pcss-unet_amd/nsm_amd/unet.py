@@ -24,7 +24,13 @@ import torch.nn as nn
 from . import ops
 from ._lib import require_gpu
 
+import os
+
 SLOPE = 0.2
+# 3x3 convolutions with at least this many (padded) input channels use the
+# Winograd F(2x2,3x3) path for forward and input-gradient (MFMA-bound layers);
+# NSM_WINOGRAD=0 disables it (direct implicit GEMM everywhere).
+WINOGRAD_MIN_CHANNELS = 256 if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30
 ENCODER = (2, 3, 4, 5)
 DECODER = (6, 7, 8, 9)
 SKIP_OF = {6: 4, 7: 3, 8: 2}          # merge_k = conv_k(...) + c_skip  (Unetmodel.py:125,131,137)
@@ -129,9 +135,15 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     ci, co = c0.in_channels, c4.out_channels
     cip, cop = ops.pad32(ci), ops.pad32(co)
     assert X.shape[1] == cip, (X.shape, cip)
-    w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD)
     b1 = ops.pad_vec(c0.bias.detach(), cip)
-    Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd", stats=training)
+    if cip >= WINOGRAD_MIN_CHANNELS:
+        U1 = ops.wino_weight(c0.weight.detach(), cip, cip, flip=False)
+        Y1 = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tag=name + ".conv.0.fwd")
+        part1 = ops.bn_partials(Y1) if training else None
+    else:
+        w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD)
+        Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd",
+                                    stats=training)
     eps1, eps2 = bn1m.eps, bn2m.eps
     if training:
         bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1)
@@ -167,6 +179,9 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
     ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
     if not need_dx:
         return None
+    if s.cip >= WINOGRAD_MIN_CHANNELS:
+        U1d = ops.wino_weight(c0.weight.detach(), s.cip, s.cip, flip=True)
+        return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tag=name + ".conv.0.dgrad")
     w1d = ops.pack_conv_weight(c0.weight.detach(), s.cip, s.cip, ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
 
@@ -194,29 +209,33 @@ class _UnetFn(torch.autograd.Function):
         saved, c, shapes = {}, {}, {}
         inp, h, w = X, Rh, Rw
         for k in ENCODER:
-            s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}")
-            saved[k], shapes[k] = s, (h, w)
-            c[k] = ops.bn_act(s.Y2, s.bn2, SLOPE)
-            if k < 5:
-                inp = ops.avgpool2(c[k], B, h, w)
-                h, w = h // 2, w // 2
+            with ops.stage(f"conv{k}.fwd"):
+                s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}")
+                saved[k], shapes[k] = s, (h, w)
+                c[k] = ops.bn_act(s.Y2, s.bn2, SLOPE)
+                if k < 5:
+                    inp = ops.avgpool2(c[k], B, h, w)
+                    h, w = h // 2, w // 2
         skip_shape = {6: shapes[4], 7: shapes[3], 8: shapes[2], 9: (Rh, Rw)}
         cur, (h, w) = c[5], shapes[5]
         ups = {}
         for k in DECODER:
-            h2, w2 = 2 * h, 2 * w
-            up = ops.resize(cur, B, h, w, h2, w2)
-            th, tw = skip_shape[k]
-            if (th, tw) != (h2, w2):
-                up = ops.resize(up, B, h2, w2, th, tw)
-            ups[k] = (h, w, h2, w2, th, tw)
-            s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}")
-            saved[k] = s
-            res = c[SKIP_OF[k]] if k in SKIP_OF else None
-            cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
-            h, w = th, tw
+            with ops.stage(f"conv{k}.fwd"):
+                h2, w2 = 2 * h, 2 * w
+                th, tw = skip_shape[k]
+                if (th, tw) != (h2, w2):   # up x2 then _upsample_and_match, fused
+                    up = ops.up2_resize(cur, B, h, w, th, tw)
+                else:                      # match is the identity (bitwise, as in ATen)
+                    up = ops.resize(cur, B, h, w, h2, w2)
+                ups[k] = (h, w, h2, w2, th, tw)
+                s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}")
+                saved[k] = s
+                res = c[SKIP_OF[k]] if k in SKIP_OF else None
+                cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
+                h, w = th, tw
         z9 = cur
-        out = ops.head_fwd(z9, B, Rh, Rw, mod.conv10.weight.detach(), mod.conv10.bias.detach())
+        with ops.stage("head.fwd"):
+            out = ops.head_fwd(z9, B, Rh, Rw, mod.conv10.weight.detach(), mod.conv10.bias.detach())
 
         ctx.mod = mod
         ctx.saved_blocks = saved
@@ -248,17 +267,20 @@ class _UnetFn(torch.autograd.Function):
             off += p.numel()
 
         gout = gout.contiguous().to(torch.float32)
-        G = ops.head_bwd(gout, out, ctx.z9, B, Rh, Rw, mod.conv10.weight.detach(),
-                         grads[mod.conv10.weight], grads[mod.conv10.bias])
+        with ops.stage("head.bwd"):
+            G = ops.head_bwd(gout, out, ctx.z9, B, Rh, Rw, mod.conv10.weight.detach(),
+                             grads[mod.conv10.weight], grads[mod.conv10.bias])
         sb = ctx.saved_blocks
         skip_grad = {}
         for k in (9, 8, 7, 6):
             s = sb[k]
-            dX = _block_bwd(mod.block(k), s, G, grads, True, f"conv{k}")
-            h, w, h2, w2, th, tw = ctx.ups[k]
-            if (th, tw) != (h2, w2):
-                dX = ops.resize_bwd(dX, B, h2, w2, th, tw)
-            dprev = ops.resize_bwd(dX, B, h, w, h2, w2)
+            with ops.stage(f"conv{k}.bwd"):
+                dX = _block_bwd(mod.block(k), s, G, grads, True, f"conv{k}")
+                h, w, h2, w2, th, tw = ctx.ups[k]
+                if (th, tw) != (h2, w2):
+                    dprev = ops.up2_resize_bwd(dX, B, h, w, th, tw)
+                else:
+                    dprev = ops.resize_bwd(dX, B, h, w, h2, w2)
             # the previous merge / c5 receives dprev; merge_{k-1} = conv + c_skip
             if k - 1 in SKIP_OF:
                 skip_grad[SKIP_OF[k - 1]] = dprev
@@ -267,6 +289,8 @@ class _UnetFn(torch.autograd.Function):
         need_x = ctx.needs_input_grad[0]
         for k in (5, 4, 3, 2):
             s = sb[k]
+            st = ops.stage(f"conv{k}.bwd")
+            st.__enter__()
             dX = _block_bwd(mod.block(k), s, G, grads, need_dx=(k > 2 or need_x), name=f"conv{k}")
             if k == 5 and training and mod.emulate_checkpoint_bn:
                 # checkpoint recompute of conv5 (Unetmodel.py:114-116): 2nd BN update
@@ -281,6 +305,7 @@ class _UnetFn(torch.autograd.Function):
                 G = ops.avgpool2_bwd_add(dX, B, ph, pw, skip_grad.get(k - 1))
             else:
                 G = dX
+            st.__exit__(None, None, None)
         dx = None
         if need_x:
             dx = ops.input_grad(G, B, C, H, W)

@@ -91,6 +91,25 @@ def test_conv_wgrad(ops, device, B, H, W, ci, co, k, pro):
     assert rel(dw.cpu(), w.grad) <= 1e-5
 
 
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 9, 11, 32, 64), (1, 16, 16, 256, 128), (2, 7, 5, 64, 32),
+                                        (2, 32, 32, 512, 256), (1, 67, 120, 64, 64)])
+def test_conv3x3_winograd(ops, device, B, H, W, ci, co):
+    """Winograd F(2x2,3x3) forward and input-gradient vs F.conv2d / autograd."""
+    g = torch.Generator().manual_seed(ci + co + H)
+    x = torch.randn(B, ci, H, W, generator=g, requires_grad=True)
+    w = torch.randn(co, ci, 3, 3, generator=g) / (ci * 9) ** 0.5
+    b = torch.randn(co, generator=g)
+    ref = F.conv2d(x, w, b, padding=1)
+    dy = torch.randn_like(ref)
+    ref.backward(dy)
+    U = ops.wino_weight(w.to(device), co, ci, flip=False)
+    y = ops.conv3x3_wino(nhwc(x.detach()).to(device), B, H, W, U, b.to(device), co)
+    assert (nchw(y.cpu(), B, H, W) - ref.detach()).abs().max().item() <= 5e-5 * max(1.0, ref.abs().max().item())
+    Ud = ops.wino_weight(w.to(device), ci, co, flip=True)
+    dx = ops.conv3x3_wino(nhwc(dy).to(device), B, H, W, Ud, None, ci)
+    assert rel(nchw(dx.cpu(), B, H, W), x.grad) <= 2e-5
+
+
 def test_conv_padded_channels(ops, device):
     """conv2 of the 7-channel model: 28 real channels padded to 32."""
     B, H, W, ci, co = 2, 10, 12, 28, 28
@@ -169,6 +188,23 @@ def test_resize(ops, device, Hi, Wi, Ho, Wo):
     assert (nchw(y.cpu(), B, Ho, Wo) - ref.detach()).abs().max() <= 1e-5
     dx = ops.resize_bwd(nhwc(gy).to(device), B, Hi, Wi, Ho, Wo)
     assert (nchw(dx.cpu(), B, Hi, Wi) - x.grad).abs().max() <= 1e-5 * max(1, x.grad.abs().max().item())
+
+
+@pytest.mark.parametrize("h,w,th,tw", [(8, 10, 8, 10), (32, 32, 32, 32), (2, 4, 5, 9), (67, 120, 135, 240),
+                                       (5, 7, 5, 7)])
+def test_up2_resize_composite(ops, device, h, w, th, tw):
+    """fused up x2 + _upsample_and_match == the two-step reference path."""
+    B, C = 2, 8
+    g = torch.Generator().manual_seed(h * 31 + tw)
+    x = torch.randn(B, C, h, w, generator=g, requires_grad=True)
+    ref = F.interpolate(F.interpolate(x, size=(2 * h, 2 * w), mode="bilinear", align_corners=True),
+                        size=(th, tw), mode="bilinear", align_corners=True)
+    gy = torch.randn(B, C, th, tw, generator=g)
+    ref.backward(gy)
+    y = ops.up2_resize(nhwc(x.detach()).to(device), B, h, w, th, tw)
+    assert (nchw(y.cpu(), B, th, tw) - ref.detach()).abs().max() <= 1e-5
+    dx = ops.up2_resize_bwd(nhwc(gy).to(device), B, h, w, th, tw)
+    assert (nchw(dx.cpu(), B, h, w) - x.grad).abs().max() <= 2e-5 * max(1, x.grad.abs().max().item())
 
 
 def test_resize_identity_bitwise(ops, device):
