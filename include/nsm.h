@@ -84,6 +84,14 @@ int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p, co
                      const float* bias, int cout_p, float* y, int ldy, float* ws, size_t ws_floats,
                      void* stream);
 
+/* Winograd weight gradient of the same 3x3 conv: dw[co][ci][3][3] (reference
+ * layout, real dims) from dy [pixels][cout_p] and the forward's transformed
+ * input V (the first 16*T*cin_p floats of that call's workspace). */
+size_t nsm_wino_wgrad_ws(int B, int H, int W, int cin_p, int cout_p);
+int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int H, int W,
+                           int cin_p, int cout_p, int cin, int cout, float* dw, float* ws,
+                           size_t ws_floats, void* stream);
+
 /* nsm_conv_wgrad: dw[co][ci][kh][kw] (real cout x cin, reference layout) =
  *   sum_p dy[p][co] * pro(x[p+off(tap)][ci]); deterministic split-K over
  *   pixels through `ws` (nsm_conv_wgrad_ws() floats). Replaces the weight

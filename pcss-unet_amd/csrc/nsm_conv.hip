@@ -68,7 +68,7 @@ struct ConvActLoader {  // MK image
   int py[NPT], px[NPT], pb[NPT];
   int kc, row0, tap, c0;
 
-  __device__ void init(const ConvActP& p, int m0, int kbeg, int tid) {
+  __device__ void init(const ConvActP& p, int m0, int kbeg, int tid, int) {
     kc = (tid & 7) * 4;
     row0 = tid >> 3;
     const int base_pix = max(0, m0 - p.W - 1);
@@ -155,12 +155,12 @@ struct RowsKLoader {  // MK / NK image
   __amdgpu_buffer_rsrc_t rsrc;
   int kc, row0, k0, n0;
 
-  __device__ void init(const RowsKP& p, int n0_, int kbeg, int tid) {
+  __device__ void init(const RowsKP& p, int n0_, int kbeg, int tid, int batch) {
     kc = (tid & 7) * 4;
     row0 = tid >> 3;
     k0 = kbeg;
     n0 = n0_;
-    const float* base = p.w + (size_t)blockIdx.z * p.bstride;
+    const float* base = p.w + (size_t)batch * p.bstride;
     rsrc = make_rsrc(base + (size_t)n0 * p.ldw, (long long)(p.nrows - n0) * p.ldw);
   }
   __device__ void load(const RowsKP& p, f32x4* r) const {
@@ -189,6 +189,7 @@ struct PixRowsP {  // rows = pixels (the GEMM K of wgrad), columns contiguous ch
   const float* mask;
   int mask_ld, mask_on;
   float slope;
+  long long bstride;  // batched GEMM: floats between batch entries
 };
 
 template <int R, int NT, bool SHIFT, bool PRO>
@@ -204,7 +205,7 @@ struct PixRowsLoader {  // KM / KN image
   bool colok;
   f32x4 sc, sh;
 
-  __device__ void init(const PixRowsP& p, int off, int kbeg, int kend_, int tid) {
+  __device__ void init(const PixRowsP& p, int off, int kbeg, int kend_, int tid, int batch) {
     int c4 = tid % C4;
     c4o = c4 * 4;
     krow0 = tid / C4;
@@ -223,7 +224,8 @@ struct PixRowsLoader {  // KM / KN image
     k0 = kbeg;
     kend = kend_;
     base_pix = max(0, kbeg - p.W - 1);
-    rsrc = make_rsrc(p.x + (size_t)base_pix * p.ld, (long long)(p.M - base_pix) * p.ld);
+    rsrc = make_rsrc(p.x + (size_t)batch * p.bstride + (size_t)base_pix * p.ld,
+                     (long long)(p.M - base_pix) * p.ld);
     if constexpr (PRO) {
       sc = colok ? *(const f32x4*)(p.scale + col) : f32x4{0.f, 0.f, 0.f, 0.f};
       sh = colok ? *(const f32x4*)(p.shift + col) : f32x4{0.f, 0.f, 0.f, 0.f};
@@ -311,7 +313,7 @@ struct EpiStore {
   __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
                                int) {
     const int col = cx.lane & 31, h = cx.lane >> 5;
-    float* yb = e.y + (size_t)blockIdx.z * e.bstride;
+    float* yb = e.y + (size_t)blockIdx.z * e.bstride;  // store paths run with zsplit == 1
     float bv[TN];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
@@ -412,7 +414,7 @@ struct EpiSlab {
                                int split) {
     const int col = cx.lane & 31, h = cx.lane >> 5;
     const int mb = cx.mb, nb = cx.nb;
-    float* out = e.ws + (size_t)split * M * N;
+    float* out = e.ws + (size_t)blockIdx.z * M * N;  // slab per (batch, split)
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       int n = nb + tn * 32 + col;
@@ -439,7 +441,7 @@ struct EpiSlab {
 // registers on keeping LDS reads in flight instead of maximising occupancy.
 template <int BM, int BN, int WM, int WN, class AL, class BL, class EP, class AP, class BP>
 __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(1, 2)))
-    gemm_f32_kernel(AP ap, BP bp, typename EP::P ep, int M, int N, int K, int kchunk, int batched) {
+    gemm_f32_kernel(AP ap, BP bp, typename EP::P ep, int M, int N, int K, int kchunk, int zsplit) {
   constexpr int NT = WM * WN * 64;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   constexpr int A_SZ = AL::LDS_FLOATS, B_SZ = BL::LDS_FLOATS, STAGE = A_SZ + B_SZ;
@@ -447,17 +449,19 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid / WN, wn = wid % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN, split = batched ? 0 : blockIdx.z;
+  // blockIdx.z = batch * zsplit + split (batch: Winograd xi; split: split-K slice)
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int split = blockIdx.z % zsplit, batch = blockIdx.z / zsplit;
   const int kbeg = split * kchunk;
   const int kend = min(K, kbeg + kchunk);
   const int nk = (kend - kbeg + BK - 1) / BK;
 
   AL a;
   BL b;
-  if constexpr (AL::KM) a.init(ap, m0, kbeg, kend, tid);
-  else a.init(ap, m0, kbeg, tid);
-  if constexpr (BL::KM) b.init(bp, n0, kbeg, kend, tid);
-  else b.init(bp, n0, kbeg, tid);
+  if constexpr (AL::KM) a.init(ap, m0, kbeg, kend, tid, batch);
+  else a.init(ap, m0, kbeg, tid, batch);
+  if constexpr (BL::KM) b.init(bp, n0, kbeg, kend, tid, batch);
+  else b.init(bp, n0, kbeg, tid, batch);
 
   f32x16 acc[TM][TN];
 #pragma unroll
@@ -552,7 +556,7 @@ static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const EpiStoreP
   using BL = RowsKLoader<BN, NT>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 1);
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiStore, ConvActP, RowsKP>), grid,
-                     dim3(NT), 0, s, ap, bp, ep, M, N, K, K, 0);
+                     dim3(NT), 0, s, ap, bp, ep, M, N, K, K, 1);
   NSM_LAUNCH_CHECK("conv_fwd");
   return 0;
 }
@@ -594,7 +598,7 @@ static int launch_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& 
   using BL = PixRowsLoader<BN, NT, SHIFT, PRO>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), splits);
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlab, PixRowsP, PixRowsP>), grid,
-                     dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, 0);
+                     dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, splits);
   NSM_LAUNCH_CHECK("conv_wgrad");
   return 0;
 }
@@ -851,6 +855,81 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
   }
 }
 
+// dM[xi][t][n] = (A dY_t A^T): transpose of the output transform, 2x2 -> 4x4
+__global__ void __launch_bounds__(256) wino_dout_kernel(const float* __restrict__ dy, int ld, int H,
+                                                        int W, int N, int TH, int TW, long long T,
+                                                        float* __restrict__ dM) {
+  const int N4 = N / 4;
+  const long long total = T * N4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % N4) * 4;
+    const long long t = i / N4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    f32x4 g[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int yy = 2 * ty + a, xx = 2 * tx + e;
+        g[a][e] = (yy < H && xx < W) ? *(const f32x4*)(dy + ((size_t)(b * H + yy) * W + xx) * ld + c)
+                                     : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    f32x4 s[4][2];  // A dY
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      s[0][e] = g[0][e];
+      s[1][e] = g[0][e] + g[1][e];
+      s[2][e] = g[0][e] - g[1][e];
+      s[3][e] = -g[1][e];
+    }
+    const size_t plane = (size_t)T * N;
+    float* out = dM + (size_t)t * N + c;
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      *(f32x4*)(out + (a * 4 + 0) * plane) = s[a][0];
+      *(f32x4*)(out + (a * 4 + 1) * plane) = s[a][0] + s[a][1];
+      *(f32x4*)(out + (a * 4 + 2) * plane) = s[a][0] - s[a][1];
+      *(f32x4*)(out + (a * 4 + 3) * plane) = -s[a][1];
+    }
+  }
+}
+
+// dw[co][ci][3][3] = G^T (sum_s dU[xi][s][co][ci]) G, one thread per (co, ci)
+__global__ void __launch_bounds__(256) wino_wgrad_out_kernel(const float* __restrict__ slab,
+                                                             int splits, int M, int N, int cin,
+                                                             int cout, float* __restrict__ dw) {
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= cout * cin) return;
+  const int ci = idx % cin, co = idx / cin;
+  const size_t MN = (size_t)M * N;
+  const float* src = slab + (size_t)co * N + ci;
+  float u[4][4];
+#pragma unroll
+  for (int x = 0; x < 16; ++x) {
+    float s = 0.f;
+    for (int k = 0; k < splits; ++k) s += src[((size_t)x * splits + k) * MN];
+    u[x / 4][x % 4] = s;
+  }
+  float t[3][4];  // G^T dU
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    t[0][j] = u[0][j] + 0.5f * (u[1][j] + u[2][j]);
+    t[1][j] = 0.5f * (u[1][j] - u[2][j]);
+    t[2][j] = 0.5f * (u[1][j] + u[2][j]) + u[3][j];
+  }
+  float* o = dw + ((size_t)co * cin + ci) * 9;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {
+    o[r * 3 + 0] = t[r][0] + 0.5f * (t[r][1] + t[r][2]);
+    o[r * 3 + 1] = 0.5f * (t[r][1] - t[r][2]);
+    o[r * 3 + 2] = 0.5f * (t[r][1] + t[r][2]) + t[r][3];
+  }
+}
+
 template <int BM, int BN, int WM, int WN>
 static int launch_wino_gemm(const RowsKP& ap, const RowsKP& bp, const EpiStoreP& ep, int M, int N,
                             int K, hipStream_t s) {
@@ -1072,5 +1151,109 @@ extern "C" int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, in
   hipLaunchKernelGGL(wino_output_kernel, dim3(grid_1d(T * cout_p / 4)), dim3(256), 0, s, Mb, cout_p,
                      H, W, TH, TW, T, bias, y, ldy);
   NSM_LAUNCH_CHECK("wino_output");
+  return 0;
+}
+
+// ---- Winograd weight gradient -------------------------------------------------
+struct WinoWgradPlan {
+  int BM, BN, splits, kchunk;
+  size_t slab_floats, dm_floats;
+};
+
+static WinoWgradPlan plan_wino_wgrad(long long T, int cin_p, int cout_p) {
+  WinoWgradPlan p;
+  p.BM = cout_p >= 128 ? 128 : (cout_p >= 64 ? 64 : 32);
+  p.BN = cin_p >= 128 ? 128 : (cin_p >= 64 ? 64 : 32);
+  long long tiles = (long long)ceil_div(cout_p, p.BM) * ceil_div(cin_p, p.BN) * 16;
+  long long want = (4096 + tiles - 1) / tiles;
+  long long maxs = (T + 255) / 256;
+  long long sp = want < maxs ? want : maxs;
+  if (sp > 64) sp = 64;
+  if (sp < 1) sp = 1;
+  long long kc = (T + sp - 1) / sp;
+  kc = (kc + BK - 1) / BK * BK;
+  sp = (T + kc - 1) / kc;
+  p.splits = (int)sp;
+  p.kchunk = (int)kc;
+  p.slab_floats = (size_t)16 * sp * cout_p * cin_p;
+  p.dm_floats = (size_t)16 * T * cout_p;
+  return p;
+}
+
+extern "C" size_t nsm_wino_wgrad_ws(int B, int H, int W, int cin_p, int cout_p) {
+  const long long T = (long long)B * ((H + 1) / 2) * ((W + 1) / 2);
+  WinoWgradPlan p = plan_wino_wgrad(T, cin_p, cout_p);
+  return p.slab_floats + p.dm_floats;
+}
+
+template <int BM, int BN, int WM, int WN>
+static int launch_wino_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& ep, int M,
+                             int N, int K, int kchunk, int splits, hipStream_t s) {
+  constexpr int NT = WM * WN * 64;
+  using AL = PixRowsLoader<BM, NT, false, false>;
+  using BL = PixRowsLoader<BN, NT, false, false>;
+  dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 16 * splits);
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlab, PixRowsP, PixRowsP>), grid,
+                     dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, splits);
+  NSM_LAUNCH_CHECK("wino_wgrad_gemm");
+  return 0;
+}
+
+extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int H,
+                                      int W, int cin_p, int cout_p, int cin, int cout, float* dw,
+                                      float* ws, size_t ws_floats, void* stream) {
+  NSM_CHECK_ARG(dy && V && dw && ws, "conv3x3_wgrad_wino: null pointer");
+  NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0 && lddy % 4 == 0 && cin <= cin_p &&
+                    cout <= cout_p, "conv3x3_wgrad_wino: bad channels");
+  const int TH = (H + 1) / 2, TW = (W + 1) / 2;
+  const long long T = (long long)B * TH * TW;
+  NSM_CHECK_ARG(T < (1ll << 30), "conv3x3_wgrad_wino: too many tiles");
+  WinoWgradPlan pl = plan_wino_wgrad(T, cin_p, cout_p);
+  if (ws_floats < pl.slab_floats + pl.dm_floats)
+    return fail(NSM_E_WS, "conv3x3_wgrad_wino: workspace too small");
+  hipStream_t s = as_stream(stream);
+  float* slab = ws;
+  float* dM = ws + pl.slab_floats;
+  hipLaunchKernelGGL(wino_dout_kernel, dim3(grid_1d(T * cout_p / 4)), dim3(256), 0, s, dy, lddy, H,
+                     W, cout_p, TH, TW, T, dM);
+  NSM_LAUNCH_CHECK("wino_dout");
+  PixRowsP ap{};
+  ap.x = dM;
+  ap.ld = cout_p;
+  ap.ncols = cout_p;
+  ap.cin = 0;
+  ap.H = 1;
+  ap.W = 1;
+  ap.M = (int)T;
+  ap.ksize = 1;
+  ap.fdW = make_fastdiv(1);
+  ap.fdH = make_fastdiv(1);
+  ap.bstride = T * cout_p;
+  PixRowsP bp = ap;
+  bp.x = V;
+  bp.ld = cin_p;
+  bp.ncols = cin_p;
+  bp.bstride = T * cin_p;
+  EpiSlabP ep{slab};
+  const int M = cout_p, N = cin_p, K = (int)T;
+  int rc;
+#define NSM_WW(bm, bn, wm, wn) \
+  if (pl.BM == bm && pl.BN == bn) \
+    rc = launch_wino_wgrad<bm, bn, wm, wn>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, s); \
+  else
+  NSM_WW(128, 128, 2, 2)
+  NSM_WW(128, 64, 2, 2)
+  NSM_WW(64, 128, 2, 2)
+  NSM_WW(64, 64, 2, 2)
+  NSM_WW(128, 32, 4, 1)
+  NSM_WW(32, 128, 1, 4)
+  NSM_WW(64, 32, 2, 1)
+  NSM_WW(32, 64, 1, 2)
+  rc = launch_wino_wgrad<32, 32, 1, 1>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, s);
+#undef NSM_WW
+  if (rc) return rc;
+  hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(ceil_div(cout * cin, 256)), dim3(256), 0, s, slab,
+                     pl.splits, M, N, cin, cout, dw);
+  NSM_LAUNCH_CHECK("wino_wgrad_out");
   return 0;
 }

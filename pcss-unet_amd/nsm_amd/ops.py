@@ -120,8 +120,10 @@ def wino_weight(w, n_p, k_p, flip):
     return U
 
 
-def conv3x3_wino(x, B, H, W, U, bias, cout_p, tag=None):
-    """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(2x2,3x3)."""
+def conv3x3_wino(x, B, H, W, U, bias, cout_p, tag=None, keep_v=False):
+    """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(2x2,3x3).
+    keep_v=True also returns the workspace, whose head holds the transformed
+    input V reused by the Winograd weight gradient."""
     from ._lib import lib
     M, cin_p = x.shape
     n = int(lib.nsm_wino_ws(B, H, W, cin_p, cout_p))
@@ -132,7 +134,20 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tag=None):
          y.stride(0), ptr(ws), n, stream())
     if ev is not None:
         ev.record()
-    return y
+    return (y, ws) if keep_v else y
+
+
+def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tag=None):
+    """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino)."""
+    from ._lib import lib
+    cout_p = dy.shape[1]
+    n = int(lib.nsm_wino_wgrad_ws(B, H, W, cin_p, cout_p))
+    ws = empty(n, device=dy.device)
+    ev = _probe(tag)
+    call("nsm_conv3x3_wgrad_wino", ptr(dy), dy.stride(0), ptr(V), B, H, W, cin_p, cout_p, cin, cout,
+         ptr(dw), ptr(ws), n, stream())
+    if ev is not None:
+        ev.record()
 
 
 def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None):

@@ -127,7 +127,7 @@ def _masks_for(mod, B, device, training):
 
 
 class _BlockSaved:
-    __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop")
+    __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop", "V")
 
 
 def _block_fwd(blk, X, B, H, W, training, mask, name=""):
@@ -136,9 +136,10 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     cip, cop = ops.pad32(ci), ops.pad32(co)
     assert X.shape[1] == cip, (X.shape, cip)
     b1 = ops.pad_vec(c0.bias.detach(), cip)
+    V = None
     if cip >= WINOGRAD_MIN_CHANNELS:
         U1 = ops.wino_weight(c0.weight.detach(), cip, cip, flip=False)
-        Y1 = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tag=name + ".conv.0.fwd")
+        Y1, V = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tag=name + ".conv.0.fwd", keep_v=True)
         part1 = ops.bn_partials(Y1) if training else None
     else:
         w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD)
@@ -160,6 +161,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     s = _BlockSaved()
     s.X, s.Y1, s.Y2, s.bn1, s.bn2, s.mask = X, Y1, Y2, bn1, bn2, mask
     s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
+    s.V = V if training else None  # Winograd-domain input, reused by the weight gradient
     return s
 
 
@@ -176,7 +178,12 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
     ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
                    pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
     dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias], g[c0.bias])
-    ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
+    if s.V is not None:
+        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight],
+                               tag=name + ".conv.0.wgrad")
+        s.V = None
+    else:
+        ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
     if not need_dx:
         return None
     if s.cip >= WINOGRAD_MIN_CHANNELS:

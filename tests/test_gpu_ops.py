@@ -110,6 +110,22 @@ def test_conv3x3_winograd(ops, device, B, H, W, ci, co):
     assert rel(nchw(dx.cpu(), B, H, W), x.grad) <= 2e-5
 
 
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 9, 11, 32, 64), (1, 16, 16, 256, 128), (2, 7, 5, 64, 32),
+                                        (2, 32, 32, 512, 256), (4, 64, 64, 64, 64)])
+def test_conv3x3_wgrad_winograd(ops, device, B, H, W, ci, co):
+    """Winograd weight gradient (reusing the forward's V) vs autograd."""
+    g = torch.Generator().manual_seed(ci * 3 + co + W)
+    x = torch.randn(B, ci, H, W, generator=g)
+    w = (torch.randn(co, ci, 3, 3, generator=g) / (ci * 9) ** 0.5).requires_grad_(True)
+    dy = torch.randn(B, co, H, W, generator=g)
+    F.conv2d(x, w, padding=1).backward(dy)
+    U = ops.wino_weight(w.detach().to(device), co, ci, flip=False)
+    _, V = ops.conv3x3_wino(nhwc(x).to(device), B, H, W, U, None, co, keep_v=True)
+    dw = torch.empty(co, ci, 3, 3, device=device)
+    ops.conv3x3_wgrad_wino(nhwc(dy).to(device), V, B, H, W, ci, ci, co, dw)
+    assert rel(dw.cpu(), w.grad) <= 2e-5
+
+
 def test_conv_padded_channels(ops, device):
     """conv2 of the 7-channel model: 28 real channels padded to 32."""
     B, H, W, ci, co = 2, 10, 12, 28, 28
