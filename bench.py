@@ -13,9 +13,10 @@ resident in HBM and requiring grad like the reference's batches
 (setdata.py:325-326). Weak scaling: per-GPU batch fixed as N grows.
 
 Rank 0 prints ONE JSON line with the metric, a roofline object for the
-dominant kernel (conv6.conv.0 forward: 3x3, 1024->1024 at 64x64, the largest
-MFMA launch) timed with HIP events on its launch stream during the timed
-steps, and a CPU baseline (the oracle restatement on the host cores).
+dominant kernel (the Winograd F(2x2,3x3) batched MFMA GEMM of conv6.conv.0
+forward: 16 x [T=B*32*32, 1024] x [1024, 1024], the largest launch of the
+step) timed with HIP events on its launch stream during the timed steps, a
+per-stage table, and a CPU baseline (the oracle restatement on the host cores).
 """
 import argparse
 import json
@@ -57,10 +58,15 @@ def unet_fwd_flops(in_ch, H, W):
 STAGES = ["conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv8", "conv9", "head"]
 
 
-def stage_work(in_ch, H, W, B, bytes_per=4):
-    """Algorithmic FLOPs and HBM bytes per stage for one train step (SURVEY.md
-    §8(d) definitions: conv FLOPs 2*H*W*Cin*Cout*k^2; bytes = (Cin+Cout)*H*W*s
-    + weights*s per conv; backward = 2x forward for both)."""
+def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=256):
+    """Per stage and train step: (algorithmic FLOPs, executed MFMA FLOPs, HBM bytes).
+
+    Algorithmic = SURVEY.md §8(d): conv FLOPs 2*H*W*Cin*Cout*k^2, backward =
+    2x forward; bytes = (Cin+Cout)*H*W*s + weights*s per conv, x3. Executed
+    counts what the MFMA units really do: 3x3 convs with Cin >= wino_min run
+    Winograd F(2x2,3x3) (16 GEMMs of T = B*ceil(h/2)*ceil(w/2) rows for fwd,
+    dgrad and wgrad: 32*T*Cin*Cout instead of 18*B*h*w*Cin*Cout), and conv5's
+    forward runs twice (checkpoint recompute, Unetmodel.py:118)."""
     R = (H // 2, W // 2)
     ch = {2: (4 * in_ch, 64), 3: (64, 128), 4: (128, 512), 5: (512, 1024),
           6: (1024, 512), 7: (512, 128), 8: (128, 64), 9: (64, 16)}
@@ -71,10 +77,15 @@ def stage_work(in_ch, H, W, B, bytes_per=4):
         h, w = res[k]
         px = B * h * w
         f = 2.0 * px * (ci * ci * 9 + ci * co)
+        T = B * ((h + 1) // 2) * ((w + 1) // 2)
+        f3 = 32.0 * T * ci * ci if ci >= wino_min else 18.0 * px * ci * ci
+        f1 = 2.0 * px * ci * co
+        ex = (4 if k == 5 else 3) * (f3 + f1)
         by = ((ci + ci) * px + 9 * ci * ci + (ci + co) * px + ci * co) * bytes_per
-        out[f"conv{k}"] = (f, by)
+        out[f"conv{k}"] = (3 * f, ex, 3 * by)
     px = B * R[0] * R[1]
-    out["head"] = (2.0 * px * 16 * 4, (16 * px + 4 * px) * bytes_per)
+    fh = 2.0 * px * 16 * 4
+    out["head"] = (3 * fh, 3 * fh, 3 * (16 * px + 4 * px) * bytes_per)
     return out
 
 
@@ -82,7 +93,7 @@ def load_traffic():
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     PMC summary (FETCH_SIZE x2 per the gfx950 calibration + WRITE_SIZE)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_conv6_fwd.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_wino_gemm_conv6.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -90,7 +101,7 @@ def load_traffic():
     return t.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(in_ch, H, W, frames=1, reps=3):
+def cpu_baseline(in_ch, H, W, frames=4, reps=5):
     """Oracle restatement (same ATen ops as the reference) fp32 fwd+bwd on the
     host cores: frames/s on a bounded sample (`frames` frames x `reps`)."""
     from oracle import unet_ref as O
@@ -202,12 +213,14 @@ def main():
         if not fw or not bw:
             continue
         t_ms = (np.mean([a.elapsed_time(b) for a, b in fw]) + np.mean([a.elapsed_time(b) for a, b in bw]))
-        fl, by = work[st]
-        tf = 3 * fl / (t_ms * 1e-3) / 1e12
-        gbs = 3 * by / (t_ms * 1e-3) / 1e9
-        ai = fl / by
+        fl, ex, by = work[st]
+        tf = fl / (t_ms * 1e-3) / 1e12
+        mf = ex / (t_ms * 1e-3) / 1e12
+        gbs = by / (t_ms * 1e-3) / 1e9
+        ai = ex / by
         stage_rows.append({"stage": st, "ms": round(float(t_ms), 3), "tflops": round(tf, 2),
-                           "mfma_frac": round(tf / FP32_PEAK_TFLOPS, 3), "gbs": round(gbs, 1),
+                           "mfma_tflops": round(mf, 2),
+                           "mfma_frac": round(mf / FP32_PEAK_TFLOPS, 3), "gbs": round(gbs, 1),
                            "hbm_frac": round(gbs / HBM_PEAK_GBS, 3), "flop_per_byte": round(ai, 1),
                            "bound": "mfma" if ai > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9) else "hbm"})
     traffic, traffic_src = load_traffic()
@@ -215,7 +228,9 @@ def main():
     frames = world * B * args.steps
     value = frames / elapsed
     Rh = H // 2
-    k_flops = conv_flops(B, Rh // 4, Rh // 4, 1024, 1024, 3)
+    T6 = B * (Rh // 8) ** 2                      # conv6 runs at (H/8, W/8): 2x2 tiles
+    k_flops = 16 * 2.0 * T6 * 1024 * 1024
+    k_bytes = 16 * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
     achieved = k_flops / (kern_ms * 1e-3) / 1e12
     step_flops = 3 * unet_fwd_flops(C, H, W) * B
     res = {
@@ -236,13 +251,13 @@ def main():
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"dp{world}"},
         "model_tflops_per_s": round(step_flops * args.steps / elapsed / 1e12 / world, 2),
-        "roofline": {"kernel": f"{probe_tag} (nsm gemm_f32 implicit-GEMM 3x3, "
-                               f"M={B * (Rh // 4) ** 2} N=1024 K=9216)",
+        "roofline": {"kernel": f"{probe_tag} Winograd F(2x2,3x3) batched MFMA GEMM "
+                               f"(nsm_wino_gemm: 16 x M={T6} N=1024 K=1024)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                      "avg_launch_ms": round(kern_ms, 4), "launches": len(evs),
                      "algorithmic_flops_per_launch": k_flops,
-                     "algorithmic_bytes_per_launch": (2 * B * (Rh // 4) ** 2 * 1024 + 9 * 1024 * 1024) * 4,
+                     "algorithmic_bytes_per_launch": k_bytes,
                      "traffic": traffic, "traffic_source": traffic_src},
         "stages": stage_rows,
     }

