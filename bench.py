@@ -13,8 +13,8 @@ resident in HBM and requiring grad like the reference's batches
 (setdata.py:325-326). Weak scaling: per-GPU batch fixed as N grows.
 
 Rank 0 prints ONE JSON line with the metric, a roofline object for the
-dominant kernel (the Winograd F(2x2,3x3) batched MFMA GEMM of conv6.conv.0
-forward: 16 x [T=B*32*32, 1024] x [1024, 1024], the largest launch of the
+dominant kernel (the Winograd F(4x4,3x3) batched MFMA GEMM of conv6.conv.0
+forward: 36 x [T=B*16*16, 1024] x [1024, 1024], the largest launch of the
 step) timed with HIP events on its launch stream during the timed steps, a
 per-stage table, and a CPU baseline (the oracle restatement on the host cores).
 """
@@ -58,14 +58,15 @@ def unet_fwd_flops(in_ch, H, W):
 STAGES = ["conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv8", "conv9", "head"]
 
 
-def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=256):
+def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=256, tile=4):
     """Per stage and train step: (algorithmic FLOPs, executed MFMA FLOPs, HBM bytes).
 
     Algorithmic = SURVEY.md §8(d): conv FLOPs 2*H*W*Cin*Cout*k^2, backward =
     2x forward; bytes = (Cin+Cout)*H*W*s + weights*s per conv, x3. Executed
     counts what the MFMA units really do: 3x3 convs with Cin >= wino_min run
-    Winograd F(2x2,3x3) (16 GEMMs of T = B*ceil(h/2)*ceil(w/2) rows for fwd,
-    dgrad and wgrad: 32*T*Cin*Cout instead of 18*B*h*w*Cin*Cout), and conv5's
+    Winograd F(m x m,3x3), m = tile ((m+2)^2 GEMMs of T = B*ceil(h/m)*ceil(w/m)
+    rows for fwd, dgrad and wgrad: 2*(m+2)^2*T*Cin*Cout instead of
+    18*B*h*w*Cin*Cout), and conv5's
     forward runs twice (checkpoint recompute, Unetmodel.py:118)."""
     R = (H // 2, W // 2)
     ch = {2: (4 * in_ch, 64), 3: (64, 128), 4: (128, 512), 5: (512, 1024),
@@ -77,8 +78,8 @@ def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=256):
         h, w = res[k]
         px = B * h * w
         f = 2.0 * px * (ci * ci * 9 + ci * co)
-        T = B * ((h + 1) // 2) * ((w + 1) // 2)
-        f3 = 32.0 * T * ci * ci if ci >= wino_min else 18.0 * px * ci * ci
+        T = B * ((h + tile - 1) // tile) * ((w + tile - 1) // tile)
+        f3 = 2.0 * (tile + 2) ** 2 * T * ci * ci if ci >= wino_min else 18.0 * px * ci * ci
         f1 = 2.0 * px * ci * co
         ex = (4 if k == 5 else 3) * (f3 + f1)
         by = ((ci + ci) * px + 9 * ci * ci + (ci + co) * px + ci * co) * bytes_per
@@ -206,7 +207,8 @@ def main():
     evs = nops.PROBES.pop(probe_tag)
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else float("nan")
     stage_rows = []
-    work = stage_work(C, H, W, B)
+    from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
+    work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE)
     for st in STAGES:
         fw = nops.PROBES.pop(st + ".fwd")
         bw = nops.PROBES.pop(st + ".bwd")
@@ -228,9 +230,10 @@ def main():
     frames = world * B * args.steps
     value = frames / elapsed
     Rh = H // 2
-    T6 = B * (Rh // 8) ** 2                      # conv6 runs at (H/8, W/8): 2x2 tiles
-    k_flops = 16 * 2.0 * T6 * 1024 * 1024
-    k_bytes = 16 * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
+    m, nb = WINO_TILE, (WINO_TILE + 2) ** 2
+    T6 = B * ((Rh // 4 + m - 1) // m) ** 2       # conv6 runs at (H/8, W/8) in m x m tiles
+    k_flops = nb * 2.0 * T6 * 1024 * 1024
+    k_bytes = nb * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
     achieved = k_flops / (kern_ms * 1e-3) / 1e12
     step_flops = 3 * unet_fwd_flops(C, H, W) * B
     res = {
@@ -251,8 +254,8 @@ def main():
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"dp{world}"},
         "model_tflops_per_s": round(step_flops * args.steps / elapsed / 1e12 / world, 2),
-        "roofline": {"kernel": f"{probe_tag} Winograd F(2x2,3x3) batched MFMA GEMM "
-                               f"(nsm_wino_gemm: 16 x M={T6} N=1024 K=1024)",
+        "roofline": {"kernel": f"{probe_tag} Winograd F({m}x{m},3x3) batched MFMA GEMM "
+                               f"(nsm_wino_gemm: {nb} x M={T6} N=1024 K=1024)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
                      "avg_launch_ms": round(kern_ms, 4), "launches": len(evs),

@@ -70,34 +70,36 @@ int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, int cin_p, 
                        const float* pro_scale, const float* pro_shift, const float* pro_mask,
                        float slope, float* stats, void* stream);
 
-/* Winograd F(2x2,3x3) 3x3 convolution (same padding 1) for deep layers:
- * nsm_wino_weight transforms w[co][ci][3][3] into U[16][n_p][k_p] (flip=0:
- * forward, n=co, k=ci; flip=1: input-gradient, n=ci, k=co, filter rotated
- * 180 deg); nsm_conv3x3_wino then computes y = conv(x, W) + bias through
- * 16 batched MFMA GEMMs, using nsm_wino_ws() floats of workspace.
+/* Winograd F(m x m, 3x3) 3x3 convolution (same padding 1) for deep layers,
+ * tile m in {2, 4}, alpha = m + 2, T = B*ceil(H/m)*ceil(W/m) tiles:
+ * nsm_wino_weight transforms w[co][ci][3][3] into U[alpha^2][n_p][k_p]
+ * (flip=0: forward, n=co, k=ci; flip=1: input-gradient, n=ci, k=co, filter
+ * rotated 180 deg); nsm_conv3x3_wino then computes y = conv(x, W) + bias
+ * through alpha^2 batched MFMA GEMMs, using nsm_wino_ws() floats of workspace.
  * Replaces the same F.conv2d 3x3 / ConvolutionBackward dgrad as nsm_conv_fwd
- * (Unetmodel.py:21) with 2.25x fewer multiplies. */
-size_t nsm_wino_ws(int B, int H, int W, int cin_p, int cout_p);
-int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k_p, int flip, float* U,
-                    void* stream);
+ * (Unetmodel.py:21) with 2.25x (m=2) or 4x (m=4) fewer multiplies. */
+size_t nsm_wino_ws(int B, int H, int W, int cin_p, int cout_p, int tile);
+int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k_p, int flip, int tile,
+                    float* U, void* stream);
 int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p, const float* U,
-                     const float* bias, int cout_p, float* y, int ldy, float* ws, size_t ws_floats,
-                     void* stream);
-/* the three stages of nsm_conv3x3_wino: V[16][T][cin_p] = B^T d B;
- * Mb[16][T][cout_p] = V . U^T (16 batched MFMA GEMMs); y = A^T Mb A + bias */
-int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, float* V, void* stream);
+                     const float* bias, int cout_p, int tile, float* y, int ldy, float* ws,
+                     size_t ws_floats, void* stream);
+/* the three stages of nsm_conv3x3_wino: V[alpha^2][T][cin_p] = B^T d B;
+ * Mb[alpha^2][T][cout_p] = V . U^T (batched MFMA GEMMs); y = A^T Mb A + bias */
+int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile, float* V,
+                   void* stream);
 int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
-                  float* Mb, void* stream);
-int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, const float* bias, float* y,
-                    int ldy, void* stream);
+                  int tile, float* Mb, void* stream);
+int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, int tile, const float* bias,
+                    float* y, int ldy, void* stream);
 
 /* Winograd weight gradient of the same 3x3 conv: dw[co][ci][3][3] (reference
  * layout, real dims) from dy [pixels][cout_p] and the forward's transformed
- * input V (the first 16*T*cin_p floats of that call's workspace). */
-size_t nsm_wino_wgrad_ws(int B, int H, int W, int cin_p, int cout_p);
+ * input V[alpha^2][T][cin_p] (nsm_wino_input output, same tile). */
+size_t nsm_wino_wgrad_ws(int B, int H, int W, int cin_p, int cout_p, int tile);
 int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int H, int W,
-                           int cin_p, int cout_p, int cin, int cout, float* dw, float* ws,
-                           size_t ws_floats, void* stream);
+                           int cin_p, int cout_p, int cin, int cout, int tile, float* dw,
+                           float* ws, size_t ws_floats, void* stream);
 
 /* nsm_conv_wgrad: dw[co][ci][kh][kw] (real cout x cin, reference layout) =
  *   sum_p dy[p][co] * pro(x[p+off(tap)][ci]); deterministic split-K over

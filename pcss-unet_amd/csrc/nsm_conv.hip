@@ -728,16 +728,110 @@ __global__ void pad_vec_kernel(const float* __restrict__ v, int n, int n_p, floa
 }
 
 // ===========================================================================
-// Winograd F(2x2,3x3) for the deep 3x3 convolutions (fwd and dgrad).
-//   V[xi][t][c]  = (B^T d B)   input tile d = 4x4 window at (2ty-1, 2tx-1)
-//   U[xi][n][k]  = (G g G^T)   g = 3x3 filter of (out n, in k)
-//   M[xi][t][n]  = sum_k V[xi][t][k] U[xi][n][k]     (16 batched MFMA GEMMs)
-//   Y(2x2 tile)  = A^T M A  (+ bias)
-// 16 multiplies per 4 outputs instead of 36: 2.25x fewer MFMA flops, same fp32
-// arithmetic (the transforms are adds and exact halvings).
+// Winograd F(m x m, 3x3), m in {2, 4}, for the deep 3x3 convolutions
+// (forward, dgrad and wgrad). alpha = m + 2, tiles t = (b, ty, tx) of m x m outputs:
+//   V[xi][t][c]  = (B^T d B)     input tile d = alpha x alpha window at (m ty-1, m tx-1)
+//   U[xi][n][k]  = (G g G^T)     g = 3x3 filter of (out n, in k)
+//   M[xi][t][n]  = sum_k V[xi][t][k] U[xi][n][k]   (alpha^2 batched MFMA GEMMs)
+//   Y(m x m)     = A^T M A  (+ bias)
+// F(2x2): 16 GEMMs per 4 outputs (2.25x fewer MFMA flops than direct);
+// F(4x4): 36 per 16 (4x fewer). Matrices: exact Cook-Toom tables generated by
+// tools/wino_coeffs.py (F(4x4) uses points 0, 1, -1, 1/2, -2 for lower fp32 error).
 // ===========================================================================
-__global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int cin, int n_p,
-                                   int k_p, int flip, float* __restrict__ U) {
+template <int MT> struct WinoMats;
+template <> struct WinoMats<2> {
+  static constexpr int A = 4;
+  __device__ static constexpr float at(int i, int j) {
+    constexpr float t[2][4] = {{1.f, 1.f, 1.f, 0.f}, {0.f, 1.f, -1.f, 1.f}};
+    return t[i][j];
+  }
+  __device__ static constexpr float g(int i, int j) {
+    constexpr float t[4][3] = {{-1.f, 0.f, 0.f}, {0.5f, 0.5f, 0.5f}, {0.5f, -0.5f, 0.5f},
+                               {0.f, 0.f, 1.f}};
+    return t[i][j];
+  }
+  __device__ static constexpr float bt(int i, int j) {
+    constexpr float t[4][4] = {{-1.f, 0.f, 1.f, 0.f}, {0.f, 1.f, 1.f, 0.f},
+                               {0.f, -1.f, 1.f, 0.f}, {0.f, -1.f, 0.f, 1.f}};
+    return t[i][j];
+  }
+};
+template <> struct WinoMats<4> {
+  static constexpr int A = 6;
+  __device__ static constexpr float at(int i, int j) {
+    constexpr float t[4][6] = {{1.f, 1.f, 1.f, 1.f, 1.f, 0.f},
+                               {0.f, 1.f, -1.f, 0.5f, -2.f, 0.f},
+                               {0.f, 1.f, 1.f, 0.25f, 4.f, 0.f},
+                               {0.f, 1.f, -1.f, 0.125f, -8.f, 1.f}};
+    return t[i][j];
+  }
+  __device__ static constexpr float g(int i, int j) {
+    constexpr float t[6][3] = {{1.f, 0.f, 0.f},
+                               {1.f / 3, 1.f / 3, 1.f / 3},
+                               {-1.f / 3, 1.f / 3, -1.f / 3},
+                               {-16.f / 15, -8.f / 15, -4.f / 15},
+                               {1.f / 15, -2.f / 15, 4.f / 15},
+                               {0.f, 0.f, 1.f}};
+    return t[i][j];
+  }
+  __device__ static constexpr float bt(int i, int j) {
+    constexpr float t[6][6] = {{1.f, -1.5f, -2.f, 1.5f, 1.f, 0.f},
+                               {0.f, -1.f, 0.5f, 2.5f, 1.f, 0.f},
+                               {0.f, 1.f, -2.5f, 0.5f, 1.f, 0.f},
+                               {0.f, -2.f, -1.f, 2.f, 1.f, 0.f},
+                               {0.f, 0.5f, -1.f, -0.5f, 1.f, 0.f},
+                               {0.f, 1.f, -1.5f, -2.f, 1.5f, 1.f}};
+    return t[i][j];
+  }
+};
+// coefficient views: c(i, j) of B^T, A^T, G and the transposes used by the gradients
+template <int MT> struct CBt { __device__ static constexpr float c(int i, int j) { return WinoMats<MT>::bt(i, j); } };
+template <int MT> struct CAt { __device__ static constexpr float c(int i, int j) { return WinoMats<MT>::at(i, j); } };
+template <int MT> struct CA  { __device__ static constexpr float c(int i, int j) { return WinoMats<MT>::at(j, i); } };
+template <int MT> struct CG  { __device__ static constexpr float c(int i, int j) { return WinoMats<MT>::g(i, j); } };
+template <int MT> struct CGt { __device__ static constexpr float c(int i, int j) { return WinoMats<MT>::g(j, i); } };
+
+// y[i] = sum_j C(i, j) x[j] over the nonzero compile-time coefficients (after
+// unrolling every coefficient is a constant: zeros vanish, +-1 become moves/negations)
+template <class C, int NO, int NI, typename T>
+__device__ __forceinline__ void wmat(const T (&x)[NI], T (&y)[NO]) {
+#pragma unroll
+  for (int i = 0; i < NO; ++i) {
+    T acc{};
+    bool first = true;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const float c = C::c(i, j);
+      if (c == 0.f) continue;
+      const T term = c == 1.f ? x[j] : (c == -1.f ? -x[j] : c * x[j]);
+      acc = first ? term : acc + term;
+      first = false;
+    }
+    y[i] = acc;
+  }
+}
+
+// Y = C X C^T for a square tile X[NI][NI] -> Y[NO][NO]
+template <class C, int NO, int NI, typename T>
+__device__ __forceinline__ void wmat2(const T (&x)[NI][NI], T (&y)[NO][NO]) {
+  T s[NO][NI];
+#pragma unroll
+  for (int e = 0; e < NI; ++e) {
+    T col[NI], r[NO];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) col[j] = x[j][e];
+    wmat<C>(col, r);
+#pragma unroll
+    for (int i = 0; i < NO; ++i) s[i][e] = r[i];
+  }
+#pragma unroll
+  for (int i = 0; i < NO; ++i) wmat<C>(s[i], y[i]);
+}
+
+template <int MT>
+__global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int cin, int n_p, int k_p,
+                                   int flip, float* __restrict__ U) {
+  constexpr int A = MT + 2;
   int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= n_p * k_p) return;
   const int k = idx % k_p, n = idx / k_p;
@@ -752,27 +846,20 @@ __global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int ci
       const int sa = flip ? 2 - a : a, sb = flip ? 2 - b : b;
       g[a][b] = ok ? w[((size_t)co * cin + ci) * 9 + sa * 3 + sb] : 0.f;
     }
-  float t[4][3];  // G g
-#pragma unroll
-  for (int b = 0; b < 3; ++b) {
-    t[0][b] = g[0][b];
-    t[1][b] = 0.5f * (g[0][b] + g[1][b] + g[2][b]);
-    t[2][b] = 0.5f * (g[0][b] - g[1][b] + g[2][b]);
-    t[3][b] = g[2][b];
-  }
+  float u[A][A];
+  wmat2<CG<MT>>(g, u);
   const size_t plane = (size_t)n_p * k_p;
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    const float u[4] = {t[a][0], 0.5f * (t[a][0] + t[a][1] + t[a][2]),
-                        0.5f * (t[a][0] - t[a][1] + t[a][2]), t[a][2]};
+  for (int a = 0; a < A; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) U[(a * 4 + b) * plane + (size_t)n * k_p + k] = u[b];
-  }
+    for (int b = 0; b < A; ++b) U[(a * A + b) * plane + (size_t)n * k_p + k] = u[a][b];
 }
 
+template <int MT>
 __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict__ x, int ld, int H,
                                                          int W, int C, int TH, int TW, long long T,
                                                          float* __restrict__ V) {
+  constexpr int A = MT + 2;
   const int C4 = C / 4;
   const long long total = T * C4;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -783,42 +870,35 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
     const long long r = t / TW;
     const int ty = (int)(r % TH);
     const long long b = r / TH;
-    f32x4 d[4][4];
+    f32x4 d[A][A];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int yy = 2 * ty - 1 + a;
+    for (int a = 0; a < A; ++a) {
+      const int yy = MT * ty - 1 + a;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int xx = 2 * tx - 1 + e;
+      for (int e = 0; e < A; ++e) {
+        const int xx = MT * tx - 1 + e;
         d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
                       ? *(const f32x4*)(x + ((size_t)(b * H + yy) * W + xx) * ld + c)
                       : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    f32x4 s[4][4];  // B^T d
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      s[0][e] = d[0][e] - d[2][e];
-      s[1][e] = d[1][e] + d[2][e];
-      s[2][e] = d[2][e] - d[1][e];
-      s[3][e] = d[1][e] - d[3][e];
-    }
+    f32x4 v[A][A];
+    wmat2<CBt<MT>>(d, v);
     const size_t plane = (size_t)T * C;
     float* out = V + (size_t)t * C + c;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      *(f32x4*)(out + (a * 4 + 0) * plane) = s[a][0] - s[a][2];
-      *(f32x4*)(out + (a * 4 + 1) * plane) = s[a][1] + s[a][2];
-      *(f32x4*)(out + (a * 4 + 2) * plane) = s[a][2] - s[a][1];
-      *(f32x4*)(out + (a * 4 + 3) * plane) = s[a][1] - s[a][3];
-    }
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) *(f32x4*)(out + (a * A + e) * plane) = v[a][e];
   }
 }
 
+template <int MT>
 __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
                                                           int W, int TH, int TW, long long T,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ y, int ldy) {
+  constexpr int A = MT + 2;
   const int N4 = N / 4;
   const long long total = T * N4;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -831,34 +911,31 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
     const long long b = r / TH;
     const size_t plane = (size_t)T * N;
     const float* in = Mb + (size_t)t * N + c;
-    f32x4 f[2][4];  // A^T M
+    f32x4 m[A][A], o[MT][MT];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const f32x4 m0 = *(const f32x4*)(in + (0 * 4 + e) * plane);
-      const f32x4 m1 = *(const f32x4*)(in + (1 * 4 + e) * plane);
-      const f32x4 m2 = *(const f32x4*)(in + (2 * 4 + e) * plane);
-      const f32x4 m3 = *(const f32x4*)(in + (3 * 4 + e) * plane);
-      f[0][e] = m0 + m1 + m2;
-      f[1][e] = m1 - m2 - m3;
-    }
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) m[a][e] = *(const f32x4*)(in + (a * A + e) * plane);
+    wmat2<CAt<MT>>(m, o);
     const f32x4 bv = bias ? *(const f32x4*)(bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int a = 0; a < 2; ++a) {
-      const int yy = 2 * ty + a;
+    for (int a = 0; a < MT; ++a) {
+      const int yy = MT * ty + a;
       if (yy >= H) continue;
-      const f32x4 o0 = f[a][0] + f[a][1] + f[a][2] + bv;
-      const f32x4 o1 = f[a][1] - f[a][2] - f[a][3] + bv;
-      float* row = y + ((size_t)(b * H + yy) * W + 2 * tx) * ldy + c;
-      *(f32x4*)row = o0;
-      if (2 * tx + 1 < W) *(f32x4*)(row + ldy) = o1;
+      float* row = y + ((size_t)(b * H + yy) * W + MT * tx) * ldy + c;
+#pragma unroll
+      for (int e = 0; e < MT; ++e)
+        if (MT * tx + e < W) *(f32x4*)(row + (size_t)e * ldy) = o[a][e] + bv;
     }
   }
 }
 
-// dM[xi][t][n] = (A dY_t A^T): transpose of the output transform, 2x2 -> 4x4
+// dM[xi][t][n] = (A dY_t A^T): transpose of the output transform, m x m -> alpha x alpha
+template <int MT>
 __global__ void __launch_bounds__(256) wino_dout_kernel(const float* __restrict__ dy, int ld, int H,
                                                         int W, int N, int TH, int TW, long long T,
                                                         float* __restrict__ dM) {
+  constexpr int A = MT + 2;
   const int N4 = N / 4;
   const long long total = T * N4;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
@@ -869,74 +946,58 @@ __global__ void __launch_bounds__(256) wino_dout_kernel(const float* __restrict_
     const long long r = t / TW;
     const int ty = (int)(r % TH);
     const long long b = r / TH;
-    f32x4 g[2][2];
+    f32x4 g[MT][MT], s[A][A];
 #pragma unroll
-    for (int a = 0; a < 2; ++a)
+    for (int a = 0; a < MT; ++a)
 #pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const int yy = 2 * ty + a, xx = 2 * tx + e;
+      for (int e = 0; e < MT; ++e) {
+        const int yy = MT * ty + a, xx = MT * tx + e;
         g[a][e] = (yy < H && xx < W) ? *(const f32x4*)(dy + ((size_t)(b * H + yy) * W + xx) * ld + c)
                                      : f32x4{0.f, 0.f, 0.f, 0.f};
       }
-    f32x4 s[4][2];  // A dY
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      s[0][e] = g[0][e];
-      s[1][e] = g[0][e] + g[1][e];
-      s[2][e] = g[0][e] - g[1][e];
-      s[3][e] = -g[1][e];
-    }
+    wmat2<CA<MT>>(g, s);
     const size_t plane = (size_t)T * N;
     float* out = dM + (size_t)t * N + c;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      *(f32x4*)(out + (a * 4 + 0) * plane) = s[a][0];
-      *(f32x4*)(out + (a * 4 + 1) * plane) = s[a][0] + s[a][1];
-      *(f32x4*)(out + (a * 4 + 2) * plane) = s[a][0] - s[a][1];
-      *(f32x4*)(out + (a * 4 + 3) * plane) = -s[a][1];
-    }
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) *(f32x4*)(out + (a * A + e) * plane) = s[a][e];
   }
 }
 
 // dw[co][ci][3][3] = G^T (sum_s dU[xi][s][co][ci]) G, one thread per (co, ci)
+template <int MT>
 __global__ void __launch_bounds__(256) wino_wgrad_out_kernel(const float* __restrict__ slab,
                                                              int splits, int M, int N, int cin,
                                                              int cout, float* __restrict__ dw) {
+  constexpr int A = MT + 2;
   int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= cout * cin) return;
   const int ci = idx % cin, co = idx / cin;
   const size_t MN = (size_t)M * N;
   const float* src = slab + (size_t)co * N + ci;
-  float u[4][4];
+  float u[A][A], o[3][3];
 #pragma unroll
-  for (int x = 0; x < 16; ++x) {
+  for (int x = 0; x < A * A; ++x) {
     float s = 0.f;
     for (int k = 0; k < splits; ++k) s += src[((size_t)x * splits + k) * MN];
-    u[x / 4][x % 4] = s;
+    u[x / A][x % A] = s;
   }
-  float t[3][4];  // G^T dU
+  wmat2<CGt<MT>>(u, o);
+  float* out = dw + ((size_t)co * cin + ci) * 9;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    t[0][j] = u[0][j] + 0.5f * (u[1][j] + u[2][j]);
-    t[1][j] = 0.5f * (u[1][j] - u[2][j]);
-    t[2][j] = 0.5f * (u[1][j] + u[2][j]) + u[3][j];
-  }
-  float* o = dw + ((size_t)co * cin + ci) * 9;
+  for (int r = 0; r < 3; ++r)
 #pragma unroll
-  for (int r = 0; r < 3; ++r) {
-    o[r * 3 + 0] = t[r][0] + 0.5f * (t[r][1] + t[r][2]);
-    o[r * 3 + 1] = 0.5f * (t[r][1] - t[r][2]);
-    o[r * 3 + 2] = 0.5f * (t[r][1] + t[r][2]) + t[r][3];
-  }
+    for (int e = 0; e < 3; ++e) out[r * 3 + e] = o[r][e];
 }
 
 template <int BM, int BN, int WM, int WN>
 static int launch_wino_gemm(const RowsKP& ap, const RowsKP& bp, const EpiStoreP& ep, int M, int N,
-                            int K, hipStream_t s) {
+                            int K, int nb, hipStream_t s) {
   constexpr int NT = WM * WN * 64;
   using AL = RowsKLoader<BM, NT>;
   using BL = RowsKLoader<BN, NT>;
-  dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 16);
+  dim3 grid(ceil_div(M, BM), ceil_div(N, BN), nb);
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiStore, RowsKP, RowsKP>), grid,
                      dim3(NT), 0, s, ap, bp, ep, M, N, K, K, 1);
   NSM_LAUNCH_CHECK("wino_gemm");
@@ -1101,76 +1162,109 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
   return 0;
 }
 
-extern "C" size_t nsm_wino_ws(int B, int H, int W, int cin_p, int cout_p) {
-  const long long T = (long long)B * ((H + 1) / 2) * ((W + 1) / 2);
-  return (size_t)16 * T * (cin_p + cout_p);
+// ---- Winograd host side: tile in {2, 4} selects F(2x2,3x3) / F(4x4,3x3) -------
+struct WinoGeom {
+  int m, alpha2, TH, TW;
+  long long T;
+};
+
+static bool wino_geom(int tile, int B, int H, int W, WinoGeom& g) {
+  if (tile != 2 && tile != 4) return false;
+  g.m = tile;
+  g.alpha2 = (tile + 2) * (tile + 2);
+  g.TH = (H + tile - 1) / tile;
+  g.TW = (W + tile - 1) / tile;
+  g.T = (long long)B * g.TH * g.TW;
+  return B > 0 && H > 0 && W > 0 && g.T < (1ll << 30);
+}
+
+extern "C" size_t nsm_wino_ws(int B, int H, int W, int cin_p, int cout_p, int tile) {
+  WinoGeom g;
+  if (!wino_geom(tile, B, H, W, g)) return 0;
+  return (size_t)g.alpha2 * g.T * (cin_p + cout_p);
 }
 
 extern "C" int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k_p, int flip,
-                               float* U, void* stream) {
+                               int tile, float* U, void* stream) {
   NSM_CHECK_ARG(w && U && n_p % 32 == 0 && k_p % 32 == 0, "wino_weight: bad args");
+  NSM_CHECK_ARG(tile == 2 || tile == 4, "wino_weight: tile must be 2 or 4");
   NSM_CHECK_ARG(flip ? (n_p >= cin && k_p >= cout) : (n_p >= cout && k_p >= cin),
                 "wino_weight: padded dims too small");
-  hipLaunchKernelGGL(wino_weight_kernel, dim3(ceil_div(n_p * k_p, 256)), dim3(256), 0,
-                     as_stream(stream), w, cout, cin, n_p, k_p, flip, U);
+  dim3 grid(ceil_div(n_p * k_p, 256));
+  if (tile == 2)
+    hipLaunchKernelGGL(wino_weight_kernel<2>, grid, dim3(256), 0, as_stream(stream), w, cout, cin,
+                       n_p, k_p, flip, U);
+  else
+    hipLaunchKernelGGL(wino_weight_kernel<4>, grid, dim3(256), 0, as_stream(stream), w, cout, cin,
+                       n_p, k_p, flip, U);
   NSM_LAUNCH_CHECK("wino_weight");
   return 0;
 }
 
-extern "C" int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, float* V,
-                              void* stream) {
+extern "C" int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile,
+                              float* V, void* stream) {
   NSM_CHECK_ARG(x && V && cin_p % 32 == 0 && ldx % 4 == 0, "wino_input: bad args");
-  const int TH = (H + 1) / 2, TW = (W + 1) / 2;
-  const long long T = (long long)B * TH * TW;
-  NSM_CHECK_ARG(T < (1ll << 30), "wino_input: too many tiles");
-  hipLaunchKernelGGL(wino_input_kernel, dim3(grid_1d(T * cin_p / 4)), dim3(256), 0,
-                     as_stream(stream), x, ldx, H, W, cin_p, TH, TW, T, V);
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input: bad tile or shape");
+  dim3 grid(grid_1d(g.T * cin_p / 4));
+  if (tile == 2)
+    hipLaunchKernelGGL(wino_input_kernel<2>, grid, dim3(256), 0, as_stream(stream), x, ldx, H, W,
+                       cin_p, g.TH, g.TW, g.T, V);
+  else
+    hipLaunchKernelGGL(wino_input_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, ldx, H, W,
+                       cin_p, g.TH, g.TW, g.T, V);
   NSM_LAUNCH_CHECK("wino_input");
   return 0;
 }
 
 extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p,
-                             int cout_p, float* Mb, void* stream) {
+                             int cout_p, int tile, float* Mb, void* stream) {
   NSM_CHECK_ARG(V && U && Mb && cin_p % 32 == 0 && cout_p % 32 == 0, "wino_gemm: bad args");
-  const long long T = (long long)B * ((H + 1) / 2) * ((W + 1) / 2);
-  NSM_CHECK_ARG(T < (1ll << 30), "wino_gemm: too many tiles");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_gemm: bad tile or shape");
   hipStream_t s = as_stream(stream);
-  RowsKP ap{V, cin_p, (int)T, T * cin_p};
+  RowsKP ap{V, cin_p, (int)g.T, g.T * cin_p};
   RowsKP bp{U, cin_p, cout_p, (long long)cout_p * cin_p};
-  EpiStoreP ep{Mb, cout_p, nullptr, nullptr, T * cout_p};
-  const int M = (int)T, N = cout_p, K = cin_p;
+  EpiStoreP ep{Mb, cout_p, nullptr, nullptr, g.T * cout_p};
+  const int M = (int)g.T, N = cout_p, K = cin_p, nb = g.alpha2;
   long long mb128 = ceil_div(M, 128);
   if (N >= 128)
-    return (mb128 * ceil_div(N, 128) * 16 >= 1024)
-               ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, s)
-               : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, s);
-  if (N >= 64) return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, s);
-  return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, s);
+    return (mb128 * ceil_div(N, 128) * nb >= 1024)
+               ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s)
+               : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s);
+  if (N >= 64) return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, nb, s);
+  return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, nb, s);
 }
 
-extern "C" int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, const float* bias,
-                               float* y, int ldy, void* stream) {
+extern "C" int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, int tile,
+                               const float* bias, float* y, int ldy, void* stream) {
   NSM_CHECK_ARG(Mb && y && cout_p % 32 == 0 && ldy % 4 == 0, "wino_output: bad args");
-  const int TH = (H + 1) / 2, TW = (W + 1) / 2;
-  const long long T = (long long)B * TH * TW;
-  hipLaunchKernelGGL(wino_output_kernel, dim3(grid_1d(T * cout_p / 4)), dim3(256), 0,
-                     as_stream(stream), Mb, cout_p, H, W, TH, TW, T, bias, y, ldy);
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output: bad tile or shape");
+  dim3 grid(grid_1d(g.T * cout_p / 4));
+  if (tile == 2)
+    hipLaunchKernelGGL(wino_output_kernel<2>, grid, dim3(256), 0, as_stream(stream), Mb, cout_p, H,
+                       W, g.TH, g.TW, g.T, bias, y, ldy);
+  else
+    hipLaunchKernelGGL(wino_output_kernel<4>, grid, dim3(256), 0, as_stream(stream), Mb, cout_p, H,
+                       W, g.TH, g.TW, g.T, bias, y, ldy);
   NSM_LAUNCH_CHECK("wino_output");
   return 0;
 }
 
 extern "C" int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p,
-                                const float* U, const float* bias, int cout_p, float* y, int ldy,
-                                float* ws, size_t ws_floats, void* stream) {
+                                const float* U, const float* bias, int cout_p, int tile, float* y,
+                                int ldy, float* ws, size_t ws_floats, void* stream) {
   NSM_CHECK_ARG(x && U && y && ws, "conv3x3_wino: null pointer");
-  if (ws_floats < nsm_wino_ws(B, H, W, cin_p, cout_p))
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "conv3x3_wino: bad tile or shape");
+  if (ws_floats < nsm_wino_ws(B, H, W, cin_p, cout_p, tile))
     return fail(NSM_E_WS, "conv3x3_wino: workspace too small");
-  const long long T = (long long)B * ((H + 1) / 2) * ((W + 1) / 2);
   float* V = ws;
-  float* Mb = ws + (size_t)16 * T * cin_p;
-  int rc = nsm_wino_input(x, ldx, B, H, W, cin_p, V, stream);
-  if (!rc) rc = nsm_wino_gemm(V, U, B, H, W, cin_p, cout_p, Mb, stream);
-  if (!rc) rc = nsm_wino_output(Mb, B, H, W, cout_p, bias, y, ldy, stream);
+  float* Mb = ws + (size_t)g.alpha2 * g.T * cin_p;
+  int rc = nsm_wino_input(x, ldx, B, H, W, cin_p, tile, V, stream);
+  if (!rc) rc = nsm_wino_gemm(V, U, B, H, W, cin_p, cout_p, tile, Mb, stream);
+  if (!rc) rc = nsm_wino_output(Mb, B, H, W, cout_p, tile, bias, y, ldy, stream);
   return rc;
 }
 
@@ -1180,11 +1274,11 @@ struct WinoWgradPlan {
   size_t slab_floats, dm_floats;
 };
 
-static WinoWgradPlan plan_wino_wgrad(long long T, int cin_p, int cout_p) {
+static WinoWgradPlan plan_wino_wgrad(long long T, int cin_p, int cout_p, int nb) {
   WinoWgradPlan p;
   p.BM = cout_p >= 128 ? 128 : (cout_p >= 64 ? 64 : 32);
   p.BN = cin_p >= 128 ? 128 : (cin_p >= 64 ? 64 : 32);
-  long long tiles = (long long)ceil_div(cout_p, p.BM) * ceil_div(cin_p, p.BN) * 16;
+  long long tiles = (long long)ceil_div(cout_p, p.BM) * ceil_div(cin_p, p.BN) * nb;
   long long want = (4096 + tiles - 1) / tiles;
   long long maxs = (T + 255) / 256;
   long long sp = want < maxs ? want : maxs;
@@ -1195,24 +1289,25 @@ static WinoWgradPlan plan_wino_wgrad(long long T, int cin_p, int cout_p) {
   sp = (T + kc - 1) / kc;
   p.splits = (int)sp;
   p.kchunk = (int)kc;
-  p.slab_floats = (size_t)16 * sp * cout_p * cin_p;
-  p.dm_floats = (size_t)16 * T * cout_p;
+  p.slab_floats = (size_t)nb * sp * cout_p * cin_p;
+  p.dm_floats = (size_t)nb * T * cout_p;
   return p;
 }
 
-extern "C" size_t nsm_wino_wgrad_ws(int B, int H, int W, int cin_p, int cout_p) {
-  const long long T = (long long)B * ((H + 1) / 2) * ((W + 1) / 2);
-  WinoWgradPlan p = plan_wino_wgrad(T, cin_p, cout_p);
+extern "C" size_t nsm_wino_wgrad_ws(int B, int H, int W, int cin_p, int cout_p, int tile) {
+  WinoGeom g;
+  if (!wino_geom(tile, B, H, W, g)) return 0;
+  WinoWgradPlan p = plan_wino_wgrad(g.T, cin_p, cout_p, g.alpha2);
   return p.slab_floats + p.dm_floats;
 }
 
 template <int BM, int BN, int WM, int WN>
 static int launch_wino_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& ep, int M,
-                             int N, int K, int kchunk, int splits, hipStream_t s) {
+                             int N, int K, int kchunk, int splits, int nb, hipStream_t s) {
   constexpr int NT = WM * WN * 64;
   using AL = PixRowsLoader<BM, NT, false, false>;
   using BL = PixRowsLoader<BN, NT, false, false>;
-  dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 16 * splits);
+  dim3 grid(ceil_div(M, BM), ceil_div(N, BN), nb * splits);
   hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlab, PixRowsP, PixRowsP>), grid,
                      dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, splits);
   NSM_LAUNCH_CHECK("wino_wgrad_gemm");
@@ -1220,22 +1315,27 @@ static int launch_wino_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSl
 }
 
 extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int H,
-                                      int W, int cin_p, int cout_p, int cin, int cout, float* dw,
-                                      float* ws, size_t ws_floats, void* stream) {
+                                      int W, int cin_p, int cout_p, int cin, int cout, int tile,
+                                      float* dw, float* ws, size_t ws_floats, void* stream) {
   NSM_CHECK_ARG(dy && V && dw && ws, "conv3x3_wgrad_wino: null pointer");
   NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0 && lddy % 4 == 0 && cin <= cin_p &&
                     cout <= cout_p, "conv3x3_wgrad_wino: bad channels");
-  const int TH = (H + 1) / 2, TW = (W + 1) / 2;
-  const long long T = (long long)B * TH * TW;
-  NSM_CHECK_ARG(T < (1ll << 30), "conv3x3_wgrad_wino: too many tiles");
-  WinoWgradPlan pl = plan_wino_wgrad(T, cin_p, cout_p);
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "conv3x3_wgrad_wino: bad tile or shape");
+  const int nb = g.alpha2;
+  WinoWgradPlan pl = plan_wino_wgrad(g.T, cin_p, cout_p, nb);
   if (ws_floats < pl.slab_floats + pl.dm_floats)
     return fail(NSM_E_WS, "conv3x3_wgrad_wino: workspace too small");
   hipStream_t s = as_stream(stream);
   float* slab = ws;
   float* dM = ws + pl.slab_floats;
-  hipLaunchKernelGGL(wino_dout_kernel, dim3(grid_1d(T * cout_p / 4)), dim3(256), 0, s, dy, lddy, H,
-                     W, cout_p, TH, TW, T, dM);
+  dim3 g1(grid_1d(g.T * cout_p / 4));
+  if (tile == 2)
+    hipLaunchKernelGGL(wino_dout_kernel<2>, g1, dim3(256), 0, s, dy, lddy, H, W, cout_p, g.TH, g.TW,
+                       g.T, dM);
+  else
+    hipLaunchKernelGGL(wino_dout_kernel<4>, g1, dim3(256), 0, s, dy, lddy, H, W, cout_p, g.TH, g.TW,
+                       g.T, dM);
   NSM_LAUNCH_CHECK("wino_dout");
   PixRowsP ap{};
   ap.x = dM;
@@ -1244,22 +1344,22 @@ extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V,
   ap.cin = 0;
   ap.H = 1;
   ap.W = 1;
-  ap.M = (int)T;
+  ap.M = (int)g.T;
   ap.ksize = 1;
   ap.fdW = make_fastdiv(1);
   ap.fdH = make_fastdiv(1);
-  ap.bstride = T * cout_p;
+  ap.bstride = g.T * cout_p;
   PixRowsP bp = ap;
   bp.x = V;
   bp.ld = cin_p;
   bp.ncols = cin_p;
-  bp.bstride = T * cin_p;
+  bp.bstride = g.T * cin_p;
   EpiSlabP ep{slab};
-  const int M = cout_p, N = cin_p, K = (int)T;
+  const int M = cout_p, N = cin_p, K = (int)g.T;
   int rc;
 #define NSM_WW(bm, bn, wm, wn) \
   if (pl.BM == bm && pl.BN == bn) \
-    rc = launch_wino_wgrad<bm, bn, wm, wn>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, s); \
+    rc = launch_wino_wgrad<bm, bn, wm, wn>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, nb, s); \
   else
   NSM_WW(128, 128, 2, 2)
   NSM_WW(128, 64, 2, 2)
@@ -1269,11 +1369,16 @@ extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V,
   NSM_WW(32, 128, 1, 4)
   NSM_WW(64, 32, 2, 1)
   NSM_WW(32, 64, 1, 2)
-  rc = launch_wino_wgrad<32, 32, 1, 1>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, s);
+  rc = launch_wino_wgrad<32, 32, 1, 1>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, nb, s);
 #undef NSM_WW
   if (rc) return rc;
-  hipLaunchKernelGGL(wino_wgrad_out_kernel, dim3(ceil_div(cout * cin, 256)), dim3(256), 0, s, slab,
-                     pl.splits, M, N, cin, cout, dw);
+  dim3 g2(ceil_div(cout * cin, 256));
+  if (tile == 2)
+    hipLaunchKernelGGL(wino_wgrad_out_kernel<2>, g2, dim3(256), 0, s, slab, pl.splits, M, N, cin,
+                       cout, dw);
+  else
+    hipLaunchKernelGGL(wino_wgrad_out_kernel<4>, g2, dim3(256), 0, s, slab, pl.splits, M, N, cin,
+                       cout, dw);
   NSM_LAUNCH_CHECK("wino_wgrad_out");
   return 0;
 }

@@ -27,14 +27,14 @@ _SIGS = {
     "nsm_conv_fwd": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P]),
     "nsm_conv_stat_rows": (I, [I, I, I, I]),
     "nsm_conv_fwd_stats": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
-    "nsm_wino_ws": (Z, [I, I, I, I, I]),
-    "nsm_wino_weight": (I, [P, I, I, I, I, I, P, P]),
-    "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, P, I, P, Z, P]),
-    "nsm_wino_input": (I, [P, I, I, I, I, I, P, P]),
-    "nsm_wino_gemm": (I, [P, P, I, I, I, I, I, P, P]),
-    "nsm_wino_output": (I, [P, I, I, I, I, P, P, I, P]),
-    "nsm_wino_wgrad_ws": (Z, [I, I, I, I, I]),
-    "nsm_conv3x3_wgrad_wino": (I, [P, I, P, I, I, I, I, I, I, I, P, P, Z, P]),
+    "nsm_wino_ws": (Z, [I, I, I, I, I, I]),
+    "nsm_wino_weight": (I, [P, I, I, I, I, I, I, P, P]),
+    "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, Z, P]),
+    "nsm_wino_input": (I, [P, I, I, I, I, I, I, P, P]),
+    "nsm_wino_gemm": (I, [P, P, I, I, I, I, I, I, P, P]),
+    "nsm_wino_output": (I, [P, I, I, I, I, I, P, P, I, P]),
+    "nsm_wino_wgrad_ws": (Z, [I, I, I, I, I, I]),
+    "nsm_conv3x3_wgrad_wino": (I, [P, I, P, I, I, I, I, I, I, I, I, P, P, Z, P]),
     "nsm_conv_wgrad_ws": (Z, [I, I, I, I, I, I]),
     "nsm_conv_wgrad": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
     "nsm_reduce_chunks": (I, [I, I]),

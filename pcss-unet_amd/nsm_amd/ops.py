@@ -111,43 +111,47 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
     return y, part
 
 
-def wino_weight(w, n_p, k_p, flip):
-    """Winograd-domain filters U[16][n_p][k_p] of a 3x3 conv weight
+def wino_tiles(B, H, W, tile):
+    return B * ((H + tile - 1) // tile) * ((W + tile - 1) // tile)
+
+
+def wino_weight(w, n_p, k_p, flip, tile=4):
+    """Winograd-domain filters U[(tile+2)^2][n_p][k_p] of a 3x3 conv weight
     (flip=False: forward; flip=True: input-gradient of that conv)."""
     cout, cin = w.shape[0], w.shape[1]
-    U = empty(16 * n_p * k_p, device=w.device)
-    call("nsm_wino_weight", ptr(w), cout, cin, n_p, k_p, int(flip), ptr(U), stream())
+    U = empty((tile + 2) ** 2 * n_p * k_p, device=w.device)
+    call("nsm_wino_weight", ptr(w), cout, cin, n_p, k_p, int(flip), tile, ptr(U), stream())
     return U
 
 
-def conv3x3_wino(x, B, H, W, U, bias, cout_p, tag=None, keep_v=False):
-    """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(2x2,3x3).
-    keep_v=True also returns the transformed input V [16][T][cin_p], reused by
-    the Winograd weight gradient."""
+def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False):
+    """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(tile x tile, 3x3).
+    keep_v=True also returns the transformed input V [(tile+2)^2][T][cin_p],
+    reused by the Winograd weight gradient."""
     M, cin_p = x.shape
-    T = B * ((H + 1) // 2) * ((W + 1) // 2)
-    V = empty(16 * T * cin_p, device=x.device)    # kept alive for the wgrad
-    Mb = empty(16 * T * cout_p, device=x.device)
+    nb, T = (tile + 2) ** 2, wino_tiles(B, H, W, tile)
+    V = empty(nb * T * cin_p, device=x.device)    # kept alive for the wgrad
+    Mb = empty(nb * T * cout_p, device=x.device)
     y = empty(M, cout_p, device=x.device)
     st = stream()
-    call("nsm_wino_input", ptr(x), x.stride(0), B, H, W, cin_p, ptr(V), st)
+    call("nsm_wino_input", ptr(x), x.stride(0), B, H, W, cin_p, tile, ptr(V), st)
     ev = _probe(tag)      # the probe times the batched MFMA GEMM alone
-    call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, cin_p, cout_p, ptr(Mb), st)
+    call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb), st)
     if ev is not None:
         ev.record()
-    call("nsm_wino_output", ptr(Mb), B, H, W, cout_p, ptr(bias), ptr(y), y.stride(0), st)
+    call("nsm_wino_output", ptr(Mb), B, H, W, cout_p, tile, ptr(bias), ptr(y), y.stride(0), st)
     return (y, V) if keep_v else y
 
 
-def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tag=None):
-    """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino)."""
+def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None):
+    """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino, same tile)."""
     from ._lib import lib
     cout_p = dy.shape[1]
-    n = int(lib.nsm_wino_wgrad_ws(B, H, W, cin_p, cout_p))
+    n = int(lib.nsm_wino_wgrad_ws(B, H, W, cin_p, cout_p, tile))
     ws = empty(n, device=dy.device)
     ev = _probe(tag)
     call("nsm_conv3x3_wgrad_wino", ptr(dy), dy.stride(0), ptr(V), B, H, W, cin_p, cout_p, cin, cout,
-         ptr(dw), ptr(ws), n, stream())
+         tile, ptr(dw), ptr(ws), n, stream())
     if ev is not None:
         ev.record()
 

@@ -28,9 +28,11 @@ import os
 
 SLOPE = 0.2
 # 3x3 convolutions with at least this many (padded) input channels use the
-# Winograd F(2x2,3x3) path for forward and input-gradient (MFMA-bound layers);
-# NSM_WINOGRAD=0 disables it (direct implicit GEMM everywhere).
+# Winograd F(m x m, 3x3) path for forward, input- and weight-gradient
+# (MFMA-bound layers); NSM_WINOGRAD=0 disables it (direct implicit GEMM
+# everywhere), NSM_WINO_TILE=2 selects F(2x2,3x3) instead of F(4x4,3x3).
 WINOGRAD_MIN_CHANNELS = 256 if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30
+WINO_TILE = int(os.environ.get("NSM_WINO_TILE", "4"))
 ENCODER = (2, 3, 4, 5)
 DECODER = (6, 7, 8, 9)
 SKIP_OF = {6: 4, 7: 3, 8: 2}          # merge_k = conv_k(...) + c_skip  (Unetmodel.py:125,131,137)
@@ -138,8 +140,9 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     b1 = ops.pad_vec(c0.bias.detach(), cip)
     V = None
     if cip >= WINOGRAD_MIN_CHANNELS:
-        U1 = ops.wino_weight(c0.weight.detach(), cip, cip, flip=False)
-        Y1, V = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tag=name + ".conv.0.fwd", keep_v=True)
+        U1 = ops.wino_weight(c0.weight.detach(), cip, cip, flip=False, tile=WINO_TILE)
+        Y1, V = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tile=WINO_TILE, tag=name + ".conv.0.fwd",
+                                 keep_v=True)
         part1 = ops.bn_partials(Y1) if training else None
     else:
         w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD)
@@ -179,7 +182,7 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
                    pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
     dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias], g[c0.bias])
     if s.V is not None:
-        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight],
+        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=WINO_TILE,
                                tag=name + ".conv.0.wgrad")
         s.V = None
     else:
@@ -187,8 +190,9 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
     if not need_dx:
         return None
     if s.cip >= WINOGRAD_MIN_CHANNELS:
-        U1d = ops.wino_weight(c0.weight.detach(), s.cip, s.cip, flip=True)
-        return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tag=name + ".conv.0.dgrad")
+        U1d = ops.wino_weight(c0.weight.detach(), s.cip, s.cip, flip=True, tile=WINO_TILE)
+        return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=WINO_TILE,
+                                tag=name + ".conv.0.dgrad")
     w1d = ops.pack_conv_weight(c0.weight.detach(), s.cip, s.cip, ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
 

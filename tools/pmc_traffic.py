@@ -1,7 +1,7 @@
 """Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes for the dominant kernel
-(the Winograd batched GEMM of conv6.conv.0 forward and its dgrad twin:
-gemm_f32_kernel<128,128> RowsK x RowsK, grid 64x8x16 of 256-thread blocks at
-B=8) into a traffic JSON.
+(the Winograd F(4x4,3x3) batched GEMM of conv6.conv.0 forward and its dgrad
+twin: gemm_f32_kernel<128,128> RowsK x RowsK, grid 16x8x36 of 256-thread
+blocks at B=8, T = 8*16*16 tiles) into a traffic JSON.
 
 Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half
 the bytes of a 16-B/lane coalesced stream on gfx950 -> x2; WRITE_SIZE (KB) is
@@ -23,7 +23,7 @@ def pick(rs, counter):
     vals = [float(r["Counter_Value"]) for r in rs
             if r["Counter_Name"] == counter
             and r["Kernel_Name"].count("RowsKLoader<128, 256>") == 2
-            and "EpiStore" in r["Kernel_Name"] and r["Grid_Size"] == str(64 * 8 * 16 * 256)]
+            and "EpiStore" in r["Kernel_Name"] and r["Grid_Size"] == str(16 * 8 * 36 * 256)]
     return vals
 
 
@@ -31,13 +31,13 @@ f = pick(rows(sys.argv[1]), "FETCH_SIZE")
 w = pick(rows(sys.argv[2]), "WRITE_SIZE")
 fetch_kb = sum(f) / len(f)
 write_kb = sum(w) / len(w)
-T = 8 * 32 * 32
+T, NB = 8 * 16 * 16, 36
 out = {"kernel": "gemm_f32_kernel<128,128,2,2,RowsKLoader<128,256>,RowsKLoader<128,256>,EpiStore> "
-                  "grid 64x8x16 (Winograd GEMM of conv6.conv.0 fwd + dgrad, B=8)",
+                  "grid 16x8x36 (Winograd F(4x4) GEMM of conv6.conv.0 fwd + dgrad, B=8)",
        "launches_sampled": len(f), "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb,
        "fetch_bytes_corrected": fetch_kb * 1024 * 2, "write_bytes": write_kb * 1024,
        "traffic_bytes_per_launch": fetch_kb * 1024 * 2 + write_kb * 1024,
-       "algorithmic_bytes_per_launch": 16 * (2 * T * 1024 + 1024 * 1024) * 4,
+       "algorithmic_bytes_per_launch": NB * (2 * T * 1024 + 1024 * 1024) * 4,
        "note": "FETCH_SIZE doubled per the gfx950 calibration (16-B/lane loads); includes "
                "Infinity-Cache hits, which the counter does not exclude"}
 json.dump(out, open(sys.argv[3], "w"), indent=1)
