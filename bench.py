@@ -5,6 +5,7 @@ MI355X, data-parallel over N GPUs (one process per GPU, RCCL over xGMI).
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
+    python bench.py --workload infer1080     # configs[4]: 1080p eval fwd, hipGraph
 
 Workload (BASELINE.json configs[1]): batch 8 per GPU, 7x512x512 fp32
 synthetic G-buffers (x ~ N(0,1), labels integers(0,256)/255), random-init
@@ -58,16 +59,17 @@ def unet_fwd_flops(in_ch, H, W):
 STAGES = ["conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv8", "conv9", "head"]
 
 
-def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=256, tile=4):
-    """Per stage and train step: (algorithmic FLOPs, executed MFMA FLOPs, HBM bytes).
+def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=128, tile=4, passes=3):
+    """Per stage: (algorithmic FLOPs, executed MFMA FLOPs, HBM bytes) of one
+    train step (passes=3: fwd + dgrad + wgrad) or one forward (passes=1).
 
-    Algorithmic = SURVEY.md §8(d): conv FLOPs 2*H*W*Cin*Cout*k^2, backward =
-    2x forward; bytes = (Cin+Cout)*H*W*s + weights*s per conv, x3. Executed
-    counts what the MFMA units really do: 3x3 convs with Cin >= wino_min run
-    Winograd F(m x m,3x3), m = tile ((m+2)^2 GEMMs of T = B*ceil(h/m)*ceil(w/m)
-    rows for fwd, dgrad and wgrad: 2*(m+2)^2*T*Cin*Cout instead of
-    18*B*h*w*Cin*Cout), and conv5's
-    forward runs twice (checkpoint recompute, Unetmodel.py:118)."""
+    Algorithmic = SURVEY.md §8(d): conv FLOPs 2*H*W*Cin*Cout*k^2 per pass;
+    bytes = (Cin+Cout)*H*W*s + weights*s per conv and pass. Executed counts
+    what the MFMA units really do: 3x3 convs with Cin >= wino_min run Winograd
+    F(m x m,3x3), m = tile ((m+2)^2 GEMMs of T = B*ceil(h/m)*ceil(w/m) rows per
+    pass: 2*(m+2)^2*T*Cin*Cout instead of 18*B*h*w*Cin*Cout). conv5's
+    checkpoint recompute (Unetmodel.py:118) is not executed: its activations
+    are kept (the double BN running-stat update is reproduced)."""
     R = (H // 2, W // 2)
     ch = {2: (4 * in_ch, 64), 3: (64, 128), 4: (128, 512), 5: (512, 1024),
           6: (1024, 512), 7: (512, 128), 8: (128, 64), 9: (64, 16)}
@@ -79,15 +81,38 @@ def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=256, tile=4):
         px = B * h * w
         f = 2.0 * px * (ci * ci * 9 + ci * co)
         T = B * ((h + tile - 1) // tile) * ((w + tile - 1) // tile)
-        f3 = 2.0 * (tile + 2) ** 2 * T * ci * ci if ci >= wino_min else 18.0 * px * ci * ci
+        cp = (ci + 31) // 32 * 32
+        f3 = 2.0 * (tile + 2) ** 2 * T * ci * ci if cp >= wino_min else 18.0 * px * ci * ci
         f1 = 2.0 * px * ci * co
-        ex = (4 if k == 5 else 3) * (f3 + f1)
         by = ((ci + ci) * px + 9 * ci * ci + (ci + co) * px + ci * co) * bytes_per
-        out[f"conv{k}"] = (3 * f, ex, 3 * by)
+        out[f"conv{k}"] = (passes * f, passes * (f3 + f1), passes * by)
     px = B * R[0] * R[1]
     fh = 2.0 * px * 16 * 4
-    out["head"] = (3 * fh, 3 * fh, 3 * (16 * px + 4 * px) * bytes_per)
+    out["head"] = (passes * fh, passes * fh, passes * (16 * px + 4 * px) * bytes_per)
     return out
+
+
+def stage_table(work, times_ms):
+    rows = []
+    for st in STAGES:
+        if st not in times_ms:
+            continue
+        t_ms = times_ms[st]
+        fl, ex, by = work[st]
+        tf = fl / (t_ms * 1e-3) / 1e12
+        mf = ex / (t_ms * 1e-3) / 1e12
+        gbs = by / (t_ms * 1e-3) / 1e9
+        ai = ex / by
+        rows.append({"stage": st, "ms": round(float(t_ms), 3), "tflops": round(tf, 2),
+                     "mfma_tflops": round(mf, 2),
+                     "mfma_frac": round(mf / FP32_PEAK_TFLOPS, 3), "gbs": round(gbs, 1),
+                     "hbm_frac": round(gbs / HBM_PEAK_GBS, 3), "flop_per_byte": round(ai, 1),
+                     "bound": "mfma" if ai > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9) else "hbm"})
+    return rows
+
+
+def mean_ms(evs):
+    return float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else float("nan")
 
 
 def load_traffic():
@@ -102,23 +127,28 @@ def load_traffic():
     return t.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(in_ch, H, W, frames=4, reps=5):
-    """Oracle restatement (same ATen ops as the reference) fp32 fwd+bwd on the
-    host cores: frames/s on a bounded sample (`frames` frames x `reps`)."""
+def cpu_baseline(in_ch, H, W, frames=4, reps=5, train=True):
+    """Oracle restatement (same ATen ops as the reference) fp32 on the host
+    cores: frames/s of the train step (fwd+L1+bwd) or of the eval forward
+    (infer.py's per-frame work), on a bounded sample (`frames` x `reps`)."""
     from oracle import unet_ref as O
     from oracle.weights import make_state, synthetic_batch
     cores = len(os.sched_getaffinity(0))
     # the box grants this job a CPU share (OMP_NUM_THREADS, 16 per GPU); use it
     share = int(os.environ.get("OMP_NUM_THREADS", cores))
     torch.set_num_threads(max(1, min(cores, share)))
-    sd = O.torch_state(make_state(in_ch, 42), requires_grad=True)
+    sd = O.torch_state(make_state(in_ch, 42), requires_grad=train)
     x_np, y_np = synthetic_batch(frames, in_ch, H, W)
     y = torch.from_numpy(y_np)
 
     def step():
-        x = torch.from_numpy(x_np).requires_grad_(True)
-        out, _ = O.forward(sd, x, True, None, 0.0)
-        O.custom_loss(out, y, 0.9).backward()
+        if train:
+            x = torch.from_numpy(x_np).requires_grad_(True)
+            out, _ = O.forward(sd, x, True, None, 0.0)
+            O.custom_loss(out, y, 0.9).backward()
+        else:
+            with torch.no_grad():
+                O.forward(sd, torch.from_numpy(x_np), False)
 
     step()
     ts = []
@@ -127,34 +157,66 @@ def cpu_baseline(in_ch, H, W, frames=4, reps=5):
         step()
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
+    what = "train step (fwd+L1+bwd)" if train else "eval forward (no_grad)"
     return {"value": frames / t, "unit": "frames/s", "cores": torch.get_num_threads(),
             "kind": "port",
-            "sample": f"{frames} frame(s) {in_ch}x{H}x{W} fp32 train step (fwd+L1+bwd), "
+            "sample": f"{frames} frame(s) {in_ch}x{H}x{W} fp32 {what}, "
                       f"oracle/unet_ref.py on PyTorch CPU, median of {reps} after 1 warmup, "
                       f"{ts and round(sum(ts), 2)} s timed"}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=8, help="per-GPU batch")
-    ap.add_argument("--in-ch", type=int, default=7)
-    ap.add_argument("--res", type=int, default=512)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    args = ap.parse_args()
+def dominant_roofline(B, H, W, kern_ms, launches, wino_tile):
+    """Roofline object of the Winograd batched GEMM of conv6.conv.0 forward."""
+    Rh, Rw = H // 2, W // 2
+    m, nb = wino_tile, (wino_tile + 2) ** 2
+    h6, w6 = Rh // 4, Rw // 4                     # conv6 runs at (H/8, W/8)
+    T6 = B * ((h6 + m - 1) // m) * ((w6 + m - 1) // m)
+    k_flops = nb * 2.0 * T6 * 1024 * 1024
+    k_bytes = nb * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
+    achieved = k_flops / (kern_ms * 1e-3) / 1e12
+    return {"kernel": f"conv6.conv.0.fwd Winograd F({m}x{m},3x3) batched MFMA GEMM "
+                      f"(nsm_wino_gemm: {nb} x M={T6} N=1024 K=1024)",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
+            "avg_launch_ms": round(kern_ms, 4), "launches": launches,
+            "algorithmic_flops_per_launch": k_flops, "algorithmic_bytes_per_launch": k_bytes}
 
+
+def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    return world, rank, torch.device("cuda", local)
 
+
+def timed(fn, steps, world):
+    """Barrier + synchronize on both sides, max over ranks."""
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=torch.device("cuda", torch.cuda.current_device()),
+                         dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
+def run_train(args):
+    world, rank, dev = init_dist()
     import nsm_amd
     from nsm_amd import ops as nops
+    from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
 
     torch.manual_seed(1234 + rank)
     B, C, H, W = args.batch, args.in_ch, args.res, args.res
@@ -189,56 +251,24 @@ def main():
     for st in STAGES:
         nops.PROBES[st + ".fwd"] = []
         nops.PROBES[st + ".bwd"] = []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(step, args.steps, world)
     evs = nops.PROBES.pop(probe_tag)
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else float("nan")
-    stage_rows = []
-    from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
-    work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE)
+    kern_ms = mean_ms(evs)
+    times = {}
     for st in STAGES:
-        fw = nops.PROBES.pop(st + ".fwd")
-        bw = nops.PROBES.pop(st + ".bwd")
-        if not fw or not bw:
-            continue
-        t_ms = (np.mean([a.elapsed_time(b) for a, b in fw]) + np.mean([a.elapsed_time(b) for a, b in bw]))
-        fl, ex, by = work[st]
-        tf = fl / (t_ms * 1e-3) / 1e12
-        mf = ex / (t_ms * 1e-3) / 1e12
-        gbs = by / (t_ms * 1e-3) / 1e9
-        ai = ex / by
-        stage_rows.append({"stage": st, "ms": round(float(t_ms), 3), "tflops": round(tf, 2),
-                           "mfma_tflops": round(mf, 2),
-                           "mfma_frac": round(mf / FP32_PEAK_TFLOPS, 3), "gbs": round(gbs, 1),
-                           "hbm_frac": round(gbs / HBM_PEAK_GBS, 3), "flop_per_byte": round(ai, 1),
-                           "bound": "mfma" if ai > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9) else "hbm"})
+        fw, bw = nops.PROBES.pop(st + ".fwd"), nops.PROBES.pop(st + ".bwd")
+        if fw and bw:
+            times[st] = mean_ms(fw) + mean_ms(bw)
+    work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE)
     traffic, traffic_src = load_traffic()
+    roof = dominant_roofline(B, H, W, kern_ms, len(evs), WINO_TILE)
+    roof.update({"traffic": traffic, "traffic_source": traffic_src})
 
     frames = world * B * args.steps
-    value = frames / elapsed
-    Rh = H // 2
-    m, nb = WINO_TILE, (WINO_TILE + 2) ** 2
-    T6 = B * ((Rh // 4 + m - 1) // m) ** 2       # conv6 runs at (H/8, W/8) in m x m tiles
-    k_flops = nb * 2.0 * T6 * 1024 * 1024
-    k_bytes = nb * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
-    achieved = k_flops / (kern_ms * 1e-3) / 1e12
     step_flops = 3 * unet_fwd_flops(C, H, W) * B
     res = {
         "metric": "frames/sec 7x512x512 U-Net fwd+bwd (train step)",
-        "value": round(value, 3),
+        "value": round(frames / elapsed, 3),
         "unit": "frames/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -254,15 +284,8 @@ def main():
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"dp{world}"},
         "model_tflops_per_s": round(step_flops * args.steps / elapsed / 1e12 / world, 2),
-        "roofline": {"kernel": f"{probe_tag} Winograd F({m}x{m},3x3) batched MFMA GEMM "
-                               f"(nsm_wino_gemm: {nb} x M={T6} N=1024 K=1024)",
-                     "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-                     "avg_launch_ms": round(kern_ms, 4), "launches": len(evs),
-                     "algorithmic_flops_per_launch": k_flops,
-                     "algorithmic_bytes_per_launch": k_bytes,
-                     "traffic": traffic, "traffic_source": traffic_src},
-        "stages": stage_rows,
+        "roofline": roof,
+        "stages": stage_table(work, times),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(C, H, W)
@@ -271,6 +294,90 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_infer(args):
+    """configs[4]: 1x7x1080x1920 eval forward, hipGraph-captured (replicas only
+    for N > 1: frames are independent, no collective)."""
+    world, rank, dev = init_dist()
+    import nsm_amd
+    from nsm_amd import ops as nops
+    from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
+
+    torch.manual_seed(1234 + rank)
+    B, C, H, W = args.batch, args.in_ch, 1080, 1920
+    model = nsm_amd.Unet(in_ch=C, dropout_rate=0.2).to(dev).eval()
+    g = torch.Generator(device=dev).manual_seed(rank)
+    x = torch.randn(B, C, H, W, device=dev, generator=g)
+    graphed = nsm_amd.GraphedUnet(model, x)
+    for _ in range(args.warmup):
+        graphed.replay()
+    torch.cuda.synchronize()
+    elapsed = timed(graphed.replay, args.steps, world)
+
+    # kernel/stage timing from eager forwards of the same shape (HIP events
+    # cannot be read back from inside a replayed graph)
+    probe_tag = "conv6.conv.0.fwd"
+    nops.PROBES[probe_tag] = []
+    for st in STAGES:
+        nops.PROBES[st + ".fwd"] = []
+    with torch.no_grad():
+        for _ in range(args.steps):
+            model(x)
+    torch.cuda.synchronize()
+    evs = nops.PROBES.pop(probe_tag)
+    times = {st: mean_ms(nops.PROBES.pop(st + ".fwd")) for st in STAGES}
+    work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE, passes=1)
+    roof = dominant_roofline(B, H, W, mean_ms(evs), len(evs), WINO_TILE)
+    roof.update({"traffic": None, "traffic_source": None})
+    frames = world * B * args.steps
+    res = {
+        "metric": "frames/sec 7x1080x1920 U-Net inference (eval fwd, hipGraph)",
+        "value": round(frames / elapsed, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (x~N(0,1)), random-init weights, eval-mode BN (running stats)",
+        "config": {"workload": f"configs[4]: batch={B}/GPU {C}x{H}x{W} fp32 eval forward, "
+                               "one hipGraph replay per step",
+                   "global_batch": world * B, "in_ch": C, "res": [H, W],
+                   "parallelism": f"replicas{world}"},
+        "model_tflops_per_s": round(unet_fwd_flops(C, H, W) * frames / elapsed / 1e12 / world, 2),
+        "roofline": roof,
+        "stages": stage_table(work, times),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(C, H, W, frames=1, reps=3, train=False)
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (train 8, infer 1)")
+    ap.add_argument("--in-ch", type=int, default=7)
+    ap.add_argument("--res", type=int, default=512)
+    ap.add_argument("--workload", choices=["train", "infer1080"], default="train")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    if args.workload == "train":
+        args.batch = args.batch or 8
+        run_train(args)
+    else:
+        args.batch = args.batch or 1
+        run_infer(args)
 
 
 if __name__ == "__main__":

@@ -8,5 +8,6 @@ from ._lib import LIB_PATH, NsmError, lib  # noqa: F401  (loads the HIP library)
 from .unet import DoubleConv, Unet  # noqa: F401
 from .losses import CustomLoss, L1Loss, PerturbationLoss, l1_loss  # noqa: F401
 from .optim import FlatAdamW, allreduce_grads, flat_grad  # noqa: F401
+from .infer import GraphedUnet  # noqa: F401
 
 __version__ = "0.1.0"

@@ -31,7 +31,7 @@ SLOPE = 0.2
 # Winograd F(m x m, 3x3) path for forward, input- and weight-gradient
 # (MFMA-bound layers); NSM_WINOGRAD=0 disables it (direct implicit GEMM
 # everywhere), NSM_WINO_TILE=2 selects F(2x2,3x3) instead of F(4x4,3x3).
-WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "256"))
+WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "128"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
 WINO_TILE = int(os.environ.get("NSM_WINO_TILE", "4"))
 ENCODER = (2, 3, 4, 5)

@@ -156,3 +156,19 @@ def test_eval_1080p_vs_oracle(device):
         ref, _ = O.forward(O.torch_state(np_sd), torch.from_numpy(x_np), training=False)
     assert out.shape == (1, 1, 1080, 1920)
     assert (out - ref).abs().max().item() <= OUT_ABS
+
+
+@pytest.mark.gpu
+def test_graphed_inference_matches_eager(device):
+    """config 5 path: the hipGraph-captured eval forward equals the eager one bitwise
+    and follows new inputs on replay."""
+    import nsm_amd
+    np_sd = make_state(7, 42)
+    m = build(device, 7, 0.2, np_sd).eval()
+    x1 = torch.from_numpy(synthetic_batch(1, 7, 96, 160)[0]).to(device)
+    x2 = torch.randn(1, 7, 96, 160, device=device)
+    g = nsm_amd.GraphedUnet(m, x1)
+    with torch.no_grad():
+        e1, e2 = m(x1), m(x2)
+    assert torch.equal(g(x1), e1)
+    assert torch.equal(g(x2), e2)
