@@ -56,6 +56,19 @@ def unet_fwd_flops(in_ch, H, W):
     return f
 
 
+def vgg_fwd_flops(H, W):
+    """VGG19 features[:31] on one 3xHxW image, incremental (97.1 GMAC at 512^2)."""
+    cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M", 512, 512]
+    f, c, h, w = 0.0, 3, H, W
+    for v in cfg:
+        if v == "M":
+            h, w = h // 2, w // 2
+        else:
+            f += conv_flops(1, h, w, c, v, 3)
+            c = v
+    return f
+
+
 STAGES = ["conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv8", "conv9", "head"]
 
 
@@ -227,7 +240,7 @@ def run_train(args):
                 dist.broadcast(p, 0)
     opt = nsm_amd.FlatAdamW(model.parameters(), lr=7e-4, weight_decay=1e-3, max_grad_norm=1.0,
                             world_size=world)
-    crit = nsm_amd.CustomLoss(dev, alpha=0.9)
+    crit = nsm_amd.CustomLoss(dev, alpha=0.9, vgg_weights="random" if args.vgg else None)
     g = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(B, C, H, W, device=dev, generator=g).requires_grad_(True)
     y = (torch.randint(0, 256, (B, 1, H, W), device=dev, generator=g).float() / 255.0)
@@ -251,9 +264,11 @@ def run_train(args):
     for st in STAGES:
         nops.PROBES[st + ".fwd"] = []
         nops.PROBES[st + ".bwd"] = []
+    nops.PROBES["vgg.fwd"] = []
     elapsed = timed(step, args.steps, world)
     evs = nops.PROBES.pop(probe_tag)
     kern_ms = mean_ms(evs)
+    vgg_evs = nops.PROBES.pop("vgg.fwd")
     times = {}
     for st in STAGES:
         fw, bw = nops.PROBES.pop(st + ".fwd"), nops.PROBES.pop(st + ".bwd")
@@ -280,13 +295,20 @@ def run_train(args):
         "dtype": "f32",
         "data": "synthetic (x~N(0,1), labels integers(0,256)/255), random-init weights",
         "config": {"workload": f"configs[1]: batch={B}/GPU {C}x{H}x{W} fp32 train step "
-                               "(fwd + 0.9*L1 + bwd + RCCL grad all-reduce + clip + AdamW)",
+                               "(fwd + 0.9*L1" + (" + 0.1*VGG19 perceptual (random-init weights)"
+                                                   if args.vgg else "")
+                               + " + bwd + RCCL grad all-reduce + clip + AdamW)",
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"dp{world}"},
         "model_tflops_per_s": round(step_flops * args.steps / elapsed / 1e12 / world, 2),
         "roofline": roof,
         "stages": stage_table(work, times),
     }
+    if vgg_evs:
+        vfl = 2 * B * vgg_fwd_flops(H, W)
+        vms = mean_ms(vgg_evs)
+        res["vgg_perceptual"] = {"ms": round(vms, 3), "direct_equiv_gflop": round(vfl / 1e9, 1),
+                                 "tflops": round(vfl / (vms * 1e-3) / 1e12, 2)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(C, H, W)
     if rank == 0:
@@ -371,6 +393,8 @@ def main():
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--workload", choices=["train", "infer1080"], default="train")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--vgg", action="store_true",
+                    help="train: include CustomLoss's VGG19 perceptual term (customLoss.py:7-90)")
     args = ap.parse_args()
     if args.workload == "train":
         args.batch = args.batch or 8

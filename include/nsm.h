@@ -51,10 +51,12 @@ int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
  * nsm_conv_fwd: y[p][co] = bias[co] + sum_{tap,ci} pro(x[p+off(tap)][ci]) * W
  *   Replaces F.conv2d 3x3 pad 1 / 1x1 of DoubleConv (Unetmodel.py:21,26) and,
  *   with NSM_PACK_DGRAD weights and bias=NULL, its input-gradient (autograd
- *   ConvolutionBackward dgrad).  Optional prologue (1x1 only, pro_scale!=NULL):
- *   pro(v) = lrelu(v*scale[ci]+shift[ci], slope) * mask[b*cin_p+ci] — the
- *   BN-apply + LeakyReLU + Dropout2d between the two convs
- *   (Unetmodel.py:22-24) fused into the operand load. mask may be NULL. */
+ *   ConvolutionBackward dgrad).  Optional prologue (pro_scale!=NULL):
+ *   pro(v) = lrelu(v*scale[ci]+shift[ci], slope) * mask[b*cin_p+ci] on
+ *   in-bounds pixels (3x3 halo stays 0) — the BN-apply + LeakyReLU +
+ *   Dropout2d between the two convs (Unetmodel.py:22-24) fused into the
+ *   operand load; with scale 1, shift 0, slope 0 it is the ReLU between the
+ *   VGG19 convs (customLoss.py:20). mask may be NULL. */
 int nsm_conv_fwd(const float* x, int ldx, int B, int H, int W, int cin_p, const float* wpk,
                  const float* bias, int cout_p, int ksize, float* y, int ldy, const float* pro_scale,
                  const float* pro_shift, const float* pro_mask, float slope, void* stream);
@@ -82,12 +84,13 @@ size_t nsm_wino_ws(int B, int H, int W, int cin_p, int cout_p, int tile);
 int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k_p, int flip, int tile,
                     float* U, void* stream);
 int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p, const float* U,
-                     const float* bias, int cout_p, int tile, float* y, int ldy, float* ws,
-                     size_t ws_floats, void* stream);
-/* the three stages of nsm_conv3x3_wino: V[alpha^2][T][cin_p] = B^T d B;
+                     const float* bias, int cout_p, int tile, int relu, float* y, int ldy,
+                     float* ws, size_t ws_floats, void* stream);
+/* the three stages of nsm_conv3x3_wino: V[alpha^2][T][cin_p] = B^T d B
+ * (relu != 0: d = max(x, 0), the pending ReLU of a VGG feature map);
  * Mb[alpha^2][T][cout_p] = V . U^T (batched MFMA GEMMs); y = A^T Mb A + bias */
-int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile, float* V,
-                   void* stream);
+int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile, int relu,
+                   float* V, void* stream);
 int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
                   int tile, float* Mb, void* stream);
 int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, int tile, const float* bias,
@@ -203,6 +206,15 @@ int nsm_clip_coef(const float* sumsq, float inv_world, float max_norm, float* co
 int nsm_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                    float beta2, float eps, float weight_decay, int step, const float* gcoef,
                    void* stream);
+
+/* ---- VGG19 perceptual loss (customLoss.py:7-90, forward only) ------------
+ * nsm_vgg_prep: out[2B*H*W][32] NHWC = (nan_to_num(clamp(v,0,1)) - mean)/denom
+ * repeated into channels 0-2 (customLoss.py:44-62), images 0..B-1 from
+ * `output`, B..2B-1 from `target` (both [B,1,H,W]); channels 3..31 zero.
+ * nsm_maxpool2_fwd: nn.MaxPool2d(2,2) on NHWC [B*H*W][C] (VGG features 4,9,18,27). */
+int nsm_vgg_prep(const float* output, const float* target, int B, int H, int W, float mean,
+                 float denom, float* out, void* stream);
+int nsm_maxpool2_fwd(const float* x, int B, int H, int W, int C, float* y, void* stream);
 
 #ifdef __cplusplus
 }

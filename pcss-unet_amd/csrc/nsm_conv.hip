@@ -49,7 +49,7 @@ struct ConvActP {  // im2col of NHWC activations; rows = pixels, K = (tap, chann
   const float* x;
   int ld, cin, H, W, M, ksize;
   FastDiv fdW, fdH;
-  const float* scale;  // prologue (1x1 fwd only): lrelu(v*scale+shift)*mask
+  const float* scale;  // prologue: lrelu(v*scale+shift)*mask on in-bounds pixels; halo stays 0
   const float* shift;
   const float* mask;
   int mask_ld, mask_on;
@@ -855,7 +855,9 @@ __global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int ci
     for (int b = 0; b < A; ++b) U[(a * A + b) * plane + (size_t)n * k_p + k] = u[a][b];
 }
 
-template <int MT>
+// RELU: the input is a pre-activation tensor whose consumer applies max(x, 0)
+// (VGG19 feature stack: ReLU folded into the next conv's operand load)
+template <int MT, bool RELU>
 __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict__ x, int ld, int H,
                                                          int W, int C, int TH, int TW, long long T,
                                                          float* __restrict__ V) {
@@ -880,6 +882,12 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
         d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
                       ? *(const f32x4*)(x + ((size_t)(b * H + yy) * W + xx) * ld + c)
                       : f32x4{0.f, 0.f, 0.f, 0.f};
+        if (RELU) {
+          d[a][e].x = fmaxf(d[a][e].x, 0.f);
+          d[a][e].y = fmaxf(d[a][e].y, 0.f);
+          d[a][e].z = fmaxf(d[a][e].z, 0.f);
+          d[a][e].w = fmaxf(d[a][e].w, 0.f);
+        }
       }
     }
     f32x4 v[A][A];
@@ -1057,7 +1065,7 @@ extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, 
   NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0, "conv_fwd: channels must be multiples of 32");
   NSM_CHECK_ARG(ldx >= cin_p && ldx % 4 == 0 && ldy >= cout_p, "conv_fwd: bad leading dims");
   NSM_CHECK_ARG(ksize == 1 || ksize == 3, "conv_fwd: ksize %d", ksize);
-  NSM_CHECK_ARG(!pro_scale || (pro_shift && ksize == 1), "conv_fwd: prologue needs 1x1 + shift");
+  NSM_CHECK_ARG(!pro_scale || pro_shift, "conv_fwd: prologue needs scale and shift");
   NSM_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)wpk % 16) == 0, "conv_fwd: 16B alignment");
   long long Ml = (long long)B * H * W;
   NSM_CHECK_ARG(Ml < (1ll << 30), "conv_fwd: too many pixels");
@@ -1202,17 +1210,21 @@ extern "C" int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k
 }
 
 extern "C" int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile,
-                              float* V, void* stream) {
+                              int relu, float* V, void* stream) {
   NSM_CHECK_ARG(x && V && cin_p % 32 == 0 && ldx % 4 == 0, "wino_input: bad args");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input: bad tile or shape");
   dim3 grid(grid_1d(g.T * cin_p / 4));
-  if (tile == 2)
-    hipLaunchKernelGGL(wino_input_kernel<2>, grid, dim3(256), 0, as_stream(stream), x, ldx, H, W,
-                       cin_p, g.TH, g.TW, g.T, V);
-  else
-    hipLaunchKernelGGL(wino_input_kernel<4>, grid, dim3(256), 0, as_stream(stream), x, ldx, H, W,
-                       cin_p, g.TH, g.TW, g.T, V);
+  hipStream_t s = as_stream(stream);
+#define NSM_WI(m, r)                                                                            \
+  hipLaunchKernelGGL((wino_input_kernel<m, r>), grid, dim3(256), 0, s, x, ldx, H, W, cin_p, g.TH, \
+                     g.TW, g.T, V)
+  if (tile == 2) {
+    if (relu) NSM_WI(2, true); else NSM_WI(2, false);
+  } else {
+    if (relu) NSM_WI(4, true); else NSM_WI(4, false);
+  }
+#undef NSM_WI
   NSM_LAUNCH_CHECK("wino_input");
   return 0;
 }
@@ -1253,8 +1265,8 @@ extern "C" int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p,
 }
 
 extern "C" int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p,
-                                const float* U, const float* bias, int cout_p, int tile, float* y,
-                                int ldy, float* ws, size_t ws_floats, void* stream) {
+                                const float* U, const float* bias, int cout_p, int tile, int relu,
+                                float* y, int ldy, float* ws, size_t ws_floats, void* stream) {
   NSM_CHECK_ARG(x && U && y && ws, "conv3x3_wino: null pointer");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "conv3x3_wino: bad tile or shape");
@@ -1262,7 +1274,7 @@ extern "C" int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, in
     return fail(NSM_E_WS, "conv3x3_wino: workspace too small");
   float* V = ws;
   float* Mb = ws + (size_t)g.alpha2 * g.T * cin_p;
-  int rc = nsm_wino_input(x, ldx, B, H, W, cin_p, tile, V, stream);
+  int rc = nsm_wino_input(x, ldx, B, H, W, cin_p, tile, relu, V, stream);
   if (!rc) rc = nsm_wino_gemm(V, U, B, H, W, cin_p, cout_p, tile, Mb, stream);
   if (!rc) rc = nsm_wino_output(Mb, B, H, W, cout_p, tile, bias, y, ldy, stream);
   return rc;

@@ -1193,3 +1193,74 @@ extern "C" int nsm_adamw_step(float* p, const float* g, float* m, float* v, int6
   NSM_LAUNCH_CHECK("adamw");
   return 0;
 }
+
+// ===========================================================================
+// VGG19 perceptual-loss feature stack (customLoss.py:7-90), forward only.
+// ===========================================================================
+// out[img][pixel][0..31]: channels 0-2 = (nan_to_num(clamp(v, 0, 1)) - mean) / denom
+// (the 1-channel image repeated x3, customLoss.py:44-62), channels 3..31 = 0.
+// Images 0..B-1 come from `a`, B..2B-1 from `b` (output and target batched).
+__global__ void vgg_prep_kernel(const float* __restrict__ a, const float* __restrict__ b, int B,
+                                long long HW, float mean, float denom, float* __restrict__ out) {
+  long long total = 2ll * B * HW;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long half = (long long)B * HW;
+    float v = i < half ? a[i] : b[i - half];
+    // torch.clamp keeps NaN; nan_to_num(nan=0.5) then maps it (inf cannot survive the clamp)
+    v = v != v ? 0.5f : fminf(fmaxf(v, 0.f), 1.f);
+    const float n = (v - mean) / denom;
+    f32x4* row = (f32x4*)(out + (size_t)i * 32);
+    row[0] = f32x4{n, n, n, 0.f};
+#pragma unroll
+    for (int k = 1; k < 8; ++k) row[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// 2x2/2 max pool on NHWC (nn.MaxPool2d(2, 2), floor); NaN propagates as in ATen
+__device__ __forceinline__ float nanmax(float m, float v) { return (v > m || v != v) ? v : m; }
+
+__global__ void maxpool2_fwd_kernel(const float* __restrict__ x, int B, int H, int W, int C4,
+                                    float* __restrict__ y) {
+  const int Ho = H / 2, Wo = W / 2;
+  long long total = (long long)B * Ho * Wo * C4;
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
+    int c = (int)(i % C4);
+    long long t = i / C4;
+    int ox = (int)(t % Wo);
+    t /= Wo;
+    int oy = (int)(t % Ho);
+    int b = (int)(t / Ho);
+    const float* base = x + (((size_t)b * H + 2 * oy) * W + 2 * ox) * (C4 * 4) + c * 4;
+    size_t rs = (size_t)W * C4 * 4, cs = (size_t)C4 * 4;
+    f32x4 m = *(const f32x4*)base;
+    const f32x4 v1 = *(const f32x4*)(base + cs), v2 = *(const f32x4*)(base + rs),
+                v3 = *(const f32x4*)(base + rs + cs);
+    m.x = nanmax(nanmax(nanmax(m.x, v1.x), v2.x), v3.x);
+    m.y = nanmax(nanmax(nanmax(m.y, v1.y), v2.y), v3.y);
+    m.z = nanmax(nanmax(nanmax(m.z, v1.z), v2.z), v3.z);
+    m.w = nanmax(nanmax(nanmax(m.w, v1.w), v2.w), v3.w);
+    *(f32x4*)(y + (size_t)i * 4) = m;
+  }
+}
+
+extern "C" int nsm_vgg_prep(const float* output, const float* target, int B, int H, int W,
+                            float mean, float denom, float* out, void* stream) {
+  NSM_CHECK_ARG(output && target && out && B > 0 && H > 0 && W > 0, "vgg_prep: bad args");
+  long long work = 2ll * B * H * W;
+  hipLaunchKernelGGL(vgg_prep_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), output,
+                     target, B, (long long)H * W, mean, denom, out);
+  NSM_LAUNCH_CHECK("vgg_prep");
+  return 0;
+}
+
+extern "C" int nsm_maxpool2_fwd(const float* x, int B, int H, int W, int C, float* y,
+                                void* stream) {
+  NSM_CHECK_ARG(x && y && C % 4 == 0 && H >= 2 && W >= 2, "maxpool2_fwd: bad args");
+  long long work = (long long)B * (H / 2) * (W / 2) * (C / 4);
+  hipLaunchKernelGGL(maxpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), x,
+                     B, H, W, C / 4, y);
+  NSM_LAUNCH_CHECK("maxpool2_fwd");
+  return 0;
+}

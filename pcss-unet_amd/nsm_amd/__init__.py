@@ -9,5 +9,6 @@ from .unet import DoubleConv, Unet  # noqa: F401
 from .losses import CustomLoss, L1Loss, PerturbationLoss, l1_loss  # noqa: F401
 from .optim import FlatAdamW, allreduce_grads, flat_grad  # noqa: F401
 from .infer import GraphedUnet  # noqa: F401
+from .vgg import MultiLayerVGGLoss  # noqa: F401
 
 __version__ = "0.1.0"

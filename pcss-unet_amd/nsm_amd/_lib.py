@@ -29,8 +29,8 @@ _SIGS = {
     "nsm_conv_fwd_stats": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
     "nsm_wino_ws": (Z, [I, I, I, I, I, I]),
     "nsm_wino_weight": (I, [P, I, I, I, I, I, I, P, P]),
-    "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, Z, P]),
-    "nsm_wino_input": (I, [P, I, I, I, I, I, I, P, P]),
+    "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, I, I, P, I, P, Z, P]),
+    "nsm_wino_input": (I, [P, I, I, I, I, I, I, I, P, P]),
     "nsm_wino_gemm": (I, [P, P, I, I, I, I, I, I, P, P]),
     "nsm_wino_output": (I, [P, I, I, I, I, I, P, P, I, P]),
     "nsm_wino_wgrad_ws": (Z, [I, I, I, I, I, I]),
@@ -65,6 +65,8 @@ _SIGS = {
     "nsm_sumsq": (I, [P, L, P, P, P]),
     "nsm_clip_coef": (I, [P, F, F, P, P]),
     "nsm_adamw_step": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P]),
+    "nsm_vgg_prep": (I, [P, P, I, I, I, F, F, P, P]),
+    "nsm_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
 }
 
 

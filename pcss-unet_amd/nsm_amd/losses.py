@@ -4,10 +4,12 @@
 * `CustomLoss(device, alpha=0.9)`: returns alpha*L1 + (1-alpha)*vgg
   (customLoss.py:129-193). The reference's VGG term is a DETACHED constant
   (`torch.tensor(total_loss, requires_grad=True)`, customLoss.py:90), so the
-  gradient is exactly alpha*sign(o-t)/N. The VGG19 perceptual value needs
-  ImageNet weights the reference downloads at construction; offline, pass
-  `vgg=<callable(out, target) -> float tensor>` to supply it, otherwise the
-  term is 0 (value parity-unpinned).
+  gradient is exactly alpha*sign(o-t)/N. The VGG19 perceptual value
+  (`nsm_amd.vgg.MultiLayerVGGLoss`, on the libnsm kernels) needs ImageNet
+  weights the reference downloads at construction; offline pass
+  `vgg_weights=<local torchvision vgg19 .pth | state_dict | MultiLayerVGGLoss
+  | "random">` (or any `vgg=<callable(out, target)>`). With neither, the term
+  is 0 (the gradient is unchanged either way).
 * `PerturbationLoss(perturbation_count=3)`: pert_loss.py:7-90 — three
   no-grad forwards of the model on inputs perturbed by per-channel
   std * 0.01 Gaussian noise, mean L1 to the original output.
@@ -56,10 +58,21 @@ class L1Loss(nn.Module):
 
 
 class CustomLoss(nn.Module):
-    def __init__(self, device=None, alpha=0.9, vgg=None, check_range=True):
+    def __init__(self, device=None, alpha=0.9, vgg=None, vgg_weights=None, check_range=True):
         super().__init__()
         self.alpha = alpha
         self.l1 = L1Loss()
+        if vgg_weights is not None:
+            from .vgg import MultiLayerVGGLoss
+            if isinstance(vgg_weights, MultiLayerVGGLoss):
+                self.vgg_loss = vgg_weights
+            elif isinstance(vgg_weights, str) and vgg_weights == "random":
+                self.vgg_loss = MultiLayerVGGLoss(device)
+            elif isinstance(vgg_weights, str):
+                self.vgg_loss = MultiLayerVGGLoss.from_torchvision_checkpoint(vgg_weights, device)
+            else:
+                self.vgg_loss = MultiLayerVGGLoss(device, state_dict=vgg_weights)
+            vgg = self.vgg_loss
         self.vgg = vgg
         self.device = device
         self.check_range = check_range

@@ -82,19 +82,21 @@ class stage:
         return False
 
 
-def conv_fwd(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None):
-    """x: [B*H*W, cin_p]; returns y [B*H*W, cout_p]. pro=(scale, shift, mask|None)."""
-    return conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro, out, tag, stats=False)[0]
+def conv_fwd(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None, slope=0.2):
+    """x: [B*H*W, cin_p]; returns y [B*H*W, cout_p]. pro=(scale, shift, mask|None):
+    the operand loader applies lrelu(x*scale+shift, slope)*mask."""
+    return conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro, out, tag, stats=False,
+                       slope=slope)[0]
 
 
-def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None, stats=True):
+def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None, stats=True,
+                slope=0.2):
     """conv_fwd returning (y, Partials|None): with stats=True the GEMM epilogue
     also emits the BN batch-statistics partials of y."""
     from ._lib import lib
     M, cin_p = x.shape
     y = out if out is not None else empty(M, cout_p, device=x.device)
     sc = sh = mk = None
-    slope = 0.2
     if pro is not None:
         sc, sh, mk = pro
     part = None
@@ -124,7 +126,7 @@ def wino_weight(w, n_p, k_p, flip, tile=4):
     return U
 
 
-def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False):
+def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, relu=False):
     """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(tile x tile, 3x3).
     keep_v=True also returns the transformed input V [(tile+2)^2][T][cin_p],
     reused by the Winograd weight gradient."""
@@ -134,7 +136,7 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False):
     Mb = empty(nb * T * cout_p, device=x.device)
     y = empty(M, cout_p, device=x.device)
     st = stream()
-    call("nsm_wino_input", ptr(x), x.stride(0), B, H, W, cin_p, tile, ptr(V), st)
+    call("nsm_wino_input", ptr(x), x.stride(0), B, H, W, cin_p, tile, int(relu), ptr(V), st)
     ev = _probe(tag)      # the probe times the batched MFMA GEMM alone
     call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb), st)
     if ev is not None:
@@ -345,3 +347,31 @@ def head_bwd(gout, out, z, B, Rh, Rw, w10, dw10, db10):
     call("nsm_head_bwd", ptr(gout), ptr(out), ptr(z), z.stride(0), B, Rh, Rw, ptr(w10), ptr(dz),
          ptr(partial), ptr(dw10), ptr(db10), stream())
     return dz
+
+
+# ---- VGG19 perceptual loss ----------------------------------------------------
+def vgg_prep(output, target, mean, denom):
+    """[2B*H*W, 32] NHWC input of the VGG stack (output images, then target)."""
+    B, _, H, W = output.shape
+    out = empty(2 * B * H * W, 32, device=output.device)
+    call("nsm_vgg_prep", ptr(output), ptr(target), B, H, W, float(mean), float(denom), ptr(out),
+         stream())
+    return out
+
+
+def maxpool2(x, B, H, W):
+    C = x.shape[1]
+    y = empty(B * (H // 2) * (W // 2), C, device=x.device)
+    call("nsm_maxpool2_fwd", ptr(x), B, H, W, C, ptr(y), stream())
+    return y
+
+
+def l1_mean(a, b, alpha=1.0):
+    """alpha * mean|a - b| over all elements, as a 0-dim device tensor."""
+    from ._lib import lib
+    n = a.numel()
+    assert b.numel() == n and a.is_contiguous() and b.is_contiguous()
+    partial = empty(int(lib.nsm_loss_blocks(n)), device=a.device)
+    out = torch.empty((), dtype=F32, device=a.device)
+    call("nsm_l1_loss_fwd", ptr(a), ptr(b), n, float(alpha), ptr(partial), ptr(out), stream())
+    return out

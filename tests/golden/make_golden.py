@@ -234,6 +234,34 @@ def perturb_case(name, in_ch=4, B=1, H=64, W=64, seed_w=42, noise_seed=77):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **rec)
 
 
+def vgg_case(name, B, H, W, seed=11):
+    """MultiLayerVGGLoss (customLoss.py:7-90) value and per-layer L1 terms on the
+    stand-in VGG19 weights (install_stubs), for sigmoid-range images."""
+    import customLoss
+    vl = customLoss.MultiLayerVGGLoss("cpu")
+    g = torch.Generator().manual_seed(seed)
+    o = torch.sigmoid(torch.randn(B, 1, H, W, generator=g) * 2)
+    t = torch.randint(0, 256, (B, 1, H, W), generator=g).float() / 255.0
+    o[0, 0, 0, :3] = torch.tensor([-0.5, 1.5, float("nan")])   # clamp / nan_to_num paths
+    val = vl(o, t)
+    per = []
+    with torch.no_grad():
+        on = (torch.nan_to_num(torch.clamp(o, 0, 1), nan=0.5).repeat(1, 3, 1, 1) - vl.mean) / (vl.std + 1e-8)
+        tn = (torch.clamp(t, 0, 1).repeat(1, 3, 1, 1) - vl.mean) / (vl.std + 1e-8)
+        for ext in vl.feature_extractors:
+            per.append(torch.nn.functional.l1_loss(ext(on), ext(tn)).item())
+    from oracle import vgg_ref as V
+    sd = V.standin_state()
+    ov = V.vgg_loss(sd, o, t).item()
+    oper = [v.item() for v in V.layer_losses(sd, o, t)]
+    print(f"{name}: vgg ref {val.item():.8e} oracle {ov:.8e} per-layer max|d| "
+          f"{max(abs(a - b) for a, b in zip(per, oper)):.3e}")
+    assert abs(ov - val.item()) <= 1e-6 * abs(val.item())
+    rec = {"output": o.numpy(), "target": t.numpy(), "vgg": np.array(val.item()),
+           "layer_l1": np.array(per), "weights": vl.weights.numpy()}
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **rec)
+
+
 def dataset_case(name="mmap_norm"):
     """MmapLiverDataset.__getitem__ normalisation (setdata.py:296-328)."""
     import tempfile
@@ -269,6 +297,10 @@ def dataset_case(name="mmap_norm"):
 if __name__ == "__main__":
     torch.set_num_threads(8)
     install_stubs()
+    if sys.argv[1:] == ["vgg"]:
+        vgg_case("vgg_b2_96x128", 2, 96, 128)
+        vgg_case("vgg_b1_40x72", 1, 40, 72)
+        sys.exit(0)
     eval_case("eval_c4_b2_64", 4, 2, 64, 64)
     eval_case("eval_c7_b1_odd_41x73", 7, 1, 41, 73)
     train_case("train_c7_p0_b2_64", 7, 2, 64, 64, 0.0)
@@ -276,3 +308,5 @@ if __name__ == "__main__":
     train_case("train_c4_p0_b1_40x72", 4, 1, 40, 72, 0.0)
     perturb_case("perturb_c4_b1_64")
     dataset_case()
+    vgg_case("vgg_b2_96x128", 2, 96, 128)
+    vgg_case("vgg_b1_40x72", 1, 40, 72)

@@ -88,3 +88,23 @@ def test_l1_grad_is_alpha_sign_over_n():
     O.custom_loss(o, t, 0.9, float(fx["vgg"])).backward()
     ref = 0.9 * torch.sign(o.detach() - t) / o.numel()
     assert torch.equal(o.grad, ref)
+
+
+@pytest.mark.parametrize("name", ["vgg_b2_96x128", "vgg_b1_40x72"])
+def test_oracle_vgg_loss_vs_reference(name):
+    """oracle/vgg_ref.py restates MultiLayerVGGLoss: bitwise on the fixtures."""
+    from oracle import vgg_ref as V
+    fx = load(name)
+    sd = V.standin_state()
+    o, t = torch.from_numpy(fx["output"]), torch.from_numpy(fx["target"])
+    assert V.vgg_loss(sd, o, t).item() == float(fx["vgg"])
+    per = [v.item() for v in V.layer_losses(sd, o, t)]
+    assert per == list(fx["layer_l1"])
+
+
+def test_oracle_vgg_matches_train_fixture_vgg_term():
+    """the stand-in VGG term inside the reference's CustomLoss (train fixture)."""
+    from oracle import vgg_ref as V
+    fx = load("train_c7_p0_b2_64")
+    v = V.vgg_loss(V.standin_state(), torch.from_numpy(fx["out"]), torch.from_numpy(fx["y"])).item()
+    assert abs(v - float(fx["vgg"])) <= 1e-6 * abs(v)
