@@ -238,6 +238,7 @@ def run_train(args):
         with torch.no_grad():
             for p in model.parameters():
                 dist.broadcast(p, 0)
+        model.overlap_grad_allreduce()   # decoder bucket reduces under the encoder backward
     opt = nsm_amd.FlatAdamW(model.parameters(), lr=7e-4, weight_decay=1e-3, max_grad_norm=1.0,
                             world_size=world)
     crit = nsm_amd.CustomLoss(dev, alpha=0.9, vgg_weights="random" if args.vgg else None)

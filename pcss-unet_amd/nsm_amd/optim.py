@@ -33,11 +33,45 @@ def flat_grad(params):
         st, base.storage_offset(), (total,), (1,))
 
 
+# Gradient all-reduces already in flight for a flat gradient buffer, issued by
+# the Unet backward as soon as a contiguous bucket of it is final:
+# {storage ptr: (flat tensor kept alive, [async work handles])}. Only one
+# step's buffer is ever outstanding.
+_PENDING = {}
+
+
+def allreduce_async(flat, lo, hi, group=None):
+    """Start the (sum) all-reduce of flat[lo:hi] on RCCL's stream, ordered after
+    the work already queued on the current stream; allreduce_grads() waits."""
+    key = flat.untyped_storage().data_ptr()
+    ent = _PENDING.get(key)
+    if ent is None or ent[0] is not flat:
+        _PENDING.clear()
+        ent = _PENDING[key] = (flat, [])
+    ent[1].append(dist.all_reduce(flat[lo:hi], group=group, async_op=True))
+    spans = getattr(flat, "_nsm_spans", None)
+    if spans is None:
+        spans = flat._nsm_spans = []
+    spans.append((lo, hi))
+
+
 def allreduce_grads(params, group=None):
     """Sum grads over ranks (RCCL over xGMI); averaging is folded into the
-    optimizer's clip coefficient (inv_world)."""
+    optimizer's clip coefficient (inv_world). If the backward already put the
+    buckets of this flat buffer in flight (Unet.overlap_grad_allreduce), this
+    only makes the current stream wait for them."""
     params = list(params)
     g = flat_grad(params)
+    if g is not None:
+        ent = _PENDING.pop(g.untyped_storage().data_ptr(), None)
+        if ent is not None:
+            flat, works = ent
+            covered = sum(w_hi - w_lo for w_lo, w_hi in getattr(flat, "_nsm_spans", []))
+            for w in works:
+                w.wait()
+            if covered == g.numel():
+                return
+            raise RuntimeError("pending gradient buckets do not cover the flat buffer")
     if g is None:
         for p in params:
             if p.grad is not None:

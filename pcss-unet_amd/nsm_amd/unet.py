@@ -21,7 +21,7 @@ launched on the current HIP stream (see DESIGN.md for the kernel list).
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import ops, optim
 from ._lib import require_gpu
 
 import os
@@ -85,6 +85,18 @@ class Unet(nn.Module):
         self._inject_masks = None
         # when True, conv5's BNs get the reference's checkpoint-recompute update in backward
         self.emulate_checkpoint_bn = True
+        # data parallel: (group,) when the backward launches its own grad all-reduces
+        self._grad_allreduce = None
+
+    def overlap_grad_allreduce(self, group=None, enable=True):
+        """Data-parallel overlap: the backward starts the RCCL
+        all-reduce of the decoder+head gradient bucket (conv6..conv10, 80 % of
+        the 60 MiB, contiguous at the end of the flat buffer) as soon as the
+        decoder backward is queued, so it runs on RCCL's stream under the
+        encoder backward; the encoder bucket follows at the end.
+        nsm_amd.allreduce_grads() then only waits for them."""
+        self._grad_allreduce = (group,) if enable else None
+        return self
 
     # reference helpers (Unetmodel.py:65-88)
     def rearrange_to_channels(self, x):
@@ -271,12 +283,15 @@ class _UnetFn(torch.autograd.Function):
         total = sum(p.numel() for p in params)
         flat = torch.empty(total, dtype=torch.float32, device=dev)
         grads, off = {}, 0
-        views = []
+        views, offset_of = [], {}
         for p in params:
             v = flat[off:off + p.numel()].view_as(p)
             grads[p] = v
             views.append(v)
+            offset_of[id(p)] = off
             off += p.numel()
+        dp = mod._grad_allreduce
+        split = offset_of.get(id(mod.conv6.conv[0].weight)) if dp is not None else None
 
         gout = gout.contiguous().to(torch.float32)
         with ops.stage("head.bwd"):
@@ -297,6 +312,8 @@ class _UnetFn(torch.autograd.Function):
             if k - 1 in SKIP_OF:
                 skip_grad[SKIP_OF[k - 1]] = dprev
             G = dprev
+        if split is not None:   # conv6..conv10 grads are final: overlap their all-reduce
+            optim.allreduce_async(flat, split, total, dp[0])
         # encoder: G is now d c5
         need_x = ctx.needs_input_grad[0]
         for k in (5, 4, 3, 2):
@@ -318,6 +335,8 @@ class _UnetFn(torch.autograd.Function):
             else:
                 G = dX
             st.__exit__(None, None, None)
+        if split is not None:
+            optim.allreduce_async(flat, 0, split, dp[0])
         dx = None
         if need_x:
             dx = ops.input_grad(G, B, C, H, W)

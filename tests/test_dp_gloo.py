@@ -37,7 +37,7 @@ def shard_grads(x_np, y_np, lo, hi):
     return [sd[k].grad.detach().clone() for k in keys]
 
 
-def _worker(rank, world, port, x_np, y_np, q):
+def _worker(rank, world, port, x_np, y_np, q, overlap=False):
     sys.path[:0] = [ROOT, os.path.join(ROOT, "pcss-unet_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.set_num_threads(2)
@@ -56,6 +56,12 @@ def _worker(rank, world, port, x_np, y_np, q):
         params.append(p)
         off += g.numel()
     assert flat_grad(params) is not None
+    if overlap:
+        # what the Unet backward does: two buckets in flight, then a wait
+        from nsm_amd.optim import allreduce_async
+        split = sum(g.numel() for g in grads[:len(grads) // 2])
+        allreduce_async(flat, split, total)
+        allreduce_async(flat, 0, split)
     allreduce_grads(params)
     if rank == 0:
         q.put([p.grad.clone().numpy() for p in params])
@@ -74,14 +80,16 @@ def test_shard_range_partitions():
 
 
 @pytest.mark.timeout(600)
-def test_dp_allreduce_matches_sum_of_shards():
+@pytest.mark.parametrize("overlap", [False, True])
+def test_dp_allreduce_matches_sum_of_shards(overlap):
     from oracle.weights import synthetic_batch
     x_np, y_np = synthetic_batch(4, 7, 32, 32)
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, x_np, y_np, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, x_np, y_np, q, overlap))
+             for r in range(world)]
     for p in procs:
         p.start()
     got = q.get(timeout=500)

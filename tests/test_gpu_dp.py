@@ -1,0 +1,74 @@
+"""Data-parallel backward with the overlapped gradient all-reduce
+(Unet.overlap_grad_allreduce) on the real HIP path: two ranks share the one
+GPU of the test box and talk over gloo (RCCL needs one GPU per rank; the
+RCCL path is the same torch.distributed call). The reduced flat gradient must
+equal the sum of the two ranks' local gradients."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pcss-unet_amd"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import nsm_amd
+    from nsm_amd.optim import flat_grad
+    from oracle.weights import make_state, synthetic_batch
+    dev = torch.device("cuda", 0)
+    m = nsm_amd.Unet(in_ch=7, dropout_rate=0.0).to(dev).train()
+    m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in make_state(7, 42).items()})
+    x_np, y_np = synthetic_batch(4, 7, 64, 64)
+    lo, hi = 2 * rank, 2 * rank + 2
+    x = torch.from_numpy(x_np[lo:hi]).to(dev)
+    y = torch.from_numpy(y_np[lo:hi]).to(dev)
+    crit = nsm_amd.CustomLoss(dev, 0.9)
+
+    def step():
+        for p in m.parameters():
+            p.grad = None
+        crit(m(x), y, x).backward()
+
+    step()                                   # local gradients
+    local = flat_grad(list(m.parameters())).clone().cpu()
+    m.overlap_grad_allreduce()
+    step()                                   # buckets reduced inside the backward
+    nsm_amd.allreduce_grads(m.parameters())  # waits
+    red = flat_grad(list(m.parameters())).clone().cpu()
+    q.put((rank, local.numpy(), red.numpy()))   # by value: the worker exits right after
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_overlapped_grad_allreduce_two_ranks():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=500) for _ in range(2)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    want = res[0][0] + res[1][0]
+    assert (res[0][1] == want).all()
+    assert (res[1][1] == want).all()
+    assert abs(want).sum() > 0
