@@ -34,6 +34,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak (spec)
+BF16_PEAK_TFLOPS = 2516.6  # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (~2.5 PF)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -105,7 +106,7 @@ def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=128, tile=4, passes=3):
     return out
 
 
-def stage_table(work, times_ms):
+def stage_table(work, times_ms, peak=FP32_PEAK_TFLOPS):
     rows = []
     for st in STAGES:
         if st not in times_ms:
@@ -118,9 +119,9 @@ def stage_table(work, times_ms):
         ai = ex / by
         rows.append({"stage": st, "ms": round(float(t_ms), 3), "tflops": round(tf, 2),
                      "mfma_tflops": round(mf, 2),
-                     "mfma_frac": round(mf / FP32_PEAK_TFLOPS, 3), "gbs": round(gbs, 1),
+                     "mfma_frac": round(mf / peak, 3), "gbs": round(gbs, 1),
                      "hbm_frac": round(gbs / HBM_PEAK_GBS, 3), "flop_per_byte": round(ai, 1),
-                     "bound": "mfma" if ai > FP32_PEAK_TFLOPS * 1e12 / (HBM_PEAK_GBS * 1e9) else "hbm"})
+                     "bound": "mfma" if ai > peak * 1e12 / (HBM_PEAK_GBS * 1e9) else "hbm"})
     return rows
 
 
@@ -195,6 +196,21 @@ def dominant_roofline(B, H, W, kern_ms, launches, wino_tile):
             "algorithmic_flops_per_launch": k_flops, "algorithmic_bytes_per_launch": k_bytes}
 
 
+def direct_roofline(B, H, W, kern_ms, launches):
+    """Roofline object of conv6.conv.0 forward as one bf16 implicit GEMM
+    (M = B*(H/8)*(W/8) pixels, N = 1024, K = 9*1024)."""
+    M = B * (H // 8) * (W // 8)
+    k_flops = conv_flops(B, H // 8, W // 8, 1024, 1024, 3)
+    k_bytes = (2 * M * 1024 + 9 * 1024 * 1024) * 2
+    achieved = k_flops / (kern_ms * 1e-3) / 1e12
+    return {"kernel": f"conv6.conv.0.fwd bf16 implicit-GEMM 3x3 (nsm_conv_fwd_bf16: M={M} "
+                      f"N=1024 K=9216)",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+            "avg_launch_ms": round(kern_ms, 4), "launches": launches,
+            "algorithmic_flops_per_launch": k_flops, "algorithmic_bytes_per_launch": k_bytes}
+
+
 def init_dist():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -233,7 +249,10 @@ def run_train(args):
 
     torch.manual_seed(1234 + rank)
     B, C, H, W = args.batch, args.in_ch, args.res, args.res
+    bf16 = args.dtype == "bf16"
     model = nsm_amd.Unet(in_ch=C, dropout_rate=0.2).to(dev).train()
+    if bf16:
+        model.set_compute_dtype(torch.bfloat16)
     if world > 1:  # identical initial weights on every rank (DDP semantics)
         with torch.no_grad():
             for p in model.parameters():
@@ -275,10 +294,15 @@ def run_train(args):
         fw, bw = nops.PROBES.pop(st + ".fwd"), nops.PROBES.pop(st + ".bwd")
         if fw and bw:
             times[st] = mean_ms(fw) + mean_ms(bw)
-    work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE)
-    traffic, traffic_src = load_traffic()
-    roof = dominant_roofline(B, H, W, kern_ms, len(evs), WINO_TILE)
-    roof.update({"traffic": traffic, "traffic_source": traffic_src})
+    if bf16:
+        work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30)
+        roof = direct_roofline(B, H, W, kern_ms, len(evs))
+        roof.update({"traffic": None, "traffic_source": None})
+    else:
+        work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE)
+        traffic, traffic_src = load_traffic()
+        roof = dominant_roofline(B, H, W, kern_ms, len(evs), WINO_TILE)
+        roof.update({"traffic": traffic, "traffic_source": traffic_src})
 
     frames = world * B * args.steps
     step_flops = 3 * unet_fwd_flops(C, H, W) * B
@@ -293,17 +317,19 @@ def run_train(args):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16" if bf16 else "f32",
         "data": "synthetic (x~N(0,1), labels integers(0,256)/255), random-init weights",
-        "config": {"workload": f"configs[1]: batch={B}/GPU {C}x{H}x{W} fp32 train step "
-                               "(fwd + 0.9*L1" + (" + 0.1*VGG19 perceptual (random-init weights)"
+        "config": {"workload": (f"configs[2]: batch={B}/GPU {C}x{H}x{W} bf16 (fp32 accumulate, "
+                                "BN stats, params, grads) train step " if bf16 else
+                                f"configs[1]: batch={B}/GPU {C}x{H}x{W} fp32 train step ")
+                               + "(fwd + 0.9*L1" + (" + 0.1*VGG19 perceptual (random-init weights)"
                                                    if args.vgg else "")
                                + " + bwd + RCCL grad all-reduce + clip + AdamW)",
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"dp{world}"},
         "model_tflops_per_s": round(step_flops * args.steps / elapsed / 1e12 / world, 2),
         "roofline": roof,
-        "stages": stage_table(work, times),
+        "stages": stage_table(work, times, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS),
     }
     if vgg_evs:
         vfl = 2 * B * vgg_fwd_flops(H, W)
@@ -312,6 +338,8 @@ def run_train(args):
                                  "tflops": round(vfl / (vms * 1e-3) / 1e12, 2)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(C, H, W)
+        if bf16:
+            res["cpu_baseline"]["sample"] += " (fp32: the reference's CPU path)"
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -329,7 +357,10 @@ def run_infer(args):
 
     torch.manual_seed(1234 + rank)
     B, C, H, W = args.batch, args.in_ch, 1080, 1920
+    bf16 = args.dtype == "bf16"
     model = nsm_amd.Unet(in_ch=C, dropout_rate=0.2).to(dev).eval()
+    if bf16:
+        model.set_compute_dtype(torch.bfloat16)
     g = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(B, C, H, W, device=dev, generator=g)
     graphed = nsm_amd.GraphedUnet(model, x)
@@ -350,8 +381,12 @@ def run_infer(args):
     torch.cuda.synchronize()
     evs = nops.PROBES.pop(probe_tag)
     times = {st: mean_ms(nops.PROBES.pop(st + ".fwd")) for st in STAGES}
-    work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE, passes=1)
-    roof = dominant_roofline(B, H, W, mean_ms(evs), len(evs), WINO_TILE)
+    if bf16:
+        work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30, passes=1)
+        roof = direct_roofline(B, H, W, mean_ms(evs), len(evs))
+    else:
+        work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE, passes=1)
+        roof = dominant_roofline(B, H, W, mean_ms(evs), len(evs), WINO_TILE)
     roof.update({"traffic": None, "traffic_source": None})
     frames = world * B * args.steps
     res = {
@@ -365,15 +400,15 @@ def run_infer(args):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "bf16" if bf16 else "f32",
         "data": "synthetic (x~N(0,1)), random-init weights, eval-mode BN (running stats)",
-        "config": {"workload": f"configs[4]: batch={B}/GPU {C}x{H}x{W} fp32 eval forward, "
+        "config": {"workload": f"configs[4]: batch={B}/GPU {C}x{H}x{W} {args.dtype} eval forward, "
                                "one hipGraph replay per step",
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"replicas{world}"},
         "model_tflops_per_s": round(unet_fwd_flops(C, H, W) * frames / elapsed / 1e12 / world, 2),
         "roofline": roof,
-        "stages": stage_table(work, times),
+        "stages": stage_table(work, times, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(C, H, W, frames=1, reps=3, train=False)
@@ -393,6 +428,8 @@ def main():
     ap.add_argument("--in-ch", type=int, default=7)
     ap.add_argument("--res", type=int, default=512)
     ap.add_argument("--workload", choices=["train", "infer1080"], default="train")
+    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32",
+                    help="bf16: configs[2] (use --batch 64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--vgg", action="store_true",
                     help="train: include CustomLoss's VGG19 perceptual term (customLoss.py:7-90)")

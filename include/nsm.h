@@ -33,6 +33,11 @@ extern "C" {
 #define NSM_E_HIP 2 /* HIP launch error */
 #define NSM_E_WS 3  /* workspace too small */
 
+/* storage type of activation / activation-gradient buffers (void* args):
+ * every elementwise entry point below that takes `int dtype` reads and writes
+ * its NHWC tensors in that type and computes in fp32 */
+#define NSM_F32 0
+#define NSM_BF16 1
 #define NSM_PACK_FWD 0   /* w[co][ci][k][k] -> [co_p][tap][ci_p]            */
 #define NSM_PACK_DGRAD 1 /* w[co][ci][k][k] -> [ci_p][tap'][co_p], tap'=k*k-1-tap */
 
@@ -119,7 +124,8 @@ int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx, int B, in
 int nsm_reduce_chunks(int M, int C); /* partial-buffer rows for the two below */
 int nsm_reduce_rows(int M, int C);   /* rows per chunk of that plan */
 /* per-channel chunk partials {sum, M2 about chunk mean}: partial[nchunk][2][C] */
-int nsm_bn_stats(const float* y, int ld, int M, int C, float* partial, int nchunk, void* stream);
+int nsm_bn_stats(const void* y, int ld, int M, int C, float* partial, int nchunk, int dtype,
+                 void* stream);
 /* merge partials; batch mean/biased var normalise; unbiased var feeds running
  * stats, applied n_updates times (2 for conv5: checkpoint recompute,
  * Unetmodel.py:114-116); num_batches_tracked += n_updates.
@@ -134,54 +140,58 @@ int nsm_bn_finalize_eval(const float* run_mean, const float* run_var, const floa
                          float* invstd, float* scale, float* shift, void* stream);
 /* out = lrelu(y*scale+shift, slope) (+ res): BN apply + LeakyReLU
  * (Unetmodel.py:27-28) fused with the additive skip (Unetmodel.py:125,131,137) */
-int nsm_bn_act(const float* y, int ldy, int M, int C, const float* scale, const float* shift,
-               float slope, const float* res, int ldres, float* out, int ldo, void* stream);
+int nsm_bn_act(const void* y, int ldy, int M, int C, const float* scale, const float* shift,
+               float slope, const void* res, int ldres, void* out, int ldo, int dtype,
+               void* stream);
 /* backward of  z = lrelu(mask * ... ) chains around a train-mode BN:
  *   dz = g * mask[b][c] * lrelu'(y*scale+shift); partial {sum dz, sum dz*xhat}. */
-int nsm_bn_bwd_reduce(const float* g, int ldg, const float* y, int ldy, int M, int C, int HW,
+int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy, int M, int C, int HW,
                       const float* scale, const float* shift, float slope, const float* mask,
                       const float* mean, const float* invstd, float* partial, int nchunk,
-                      void* stream);
+                      int dtype, void* stream);
 /* dgamma, dbeta (real channels), bias grad of the producing conv
  * (analytically 0 in train mode), coef[3][C] for nsm_bn_bwd_apply. */
 int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int C, int c_real,
                         const float* gamma, const float* invstd, float* dgamma, float* dbeta,
                         float* dbias_prev, float* coef, void* stream);
 /* dy = coef0*dz + coef1*(y-mean) + coef2 */
-int nsm_bn_bwd_apply(const float* g, int ldg, const float* y, int ldy, int M, int C, int HW,
+int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, int M, int C, int HW,
                      const float* scale, const float* shift, float slope, const float* mask,
-                     const float* mean, const float* coef, float* dy, int lddy, void* stream);
+                     const float* mean, const float* coef, void* dy, int lddy, int dtype,
+                     void* stream);
 
 /* ---- resampling -------------------------------------------------------------
  * AvgPool2d(2) (Unetmodel.py:40,43,46): floor mode. bwd: dx = skip + dy/4. */
-int nsm_avgpool2_fwd(const float* x, int B, int H, int W, int C, float* y, void* stream);
-int nsm_avgpool2_bwd_add(const float* dy, int B, int H, int W, int C, const float* skip,
-                         float* dx, void* stream);
+int nsm_avgpool2_fwd(const void* x, int B, int H, int W, int C, void* y, int dtype, void* stream);
+int nsm_avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, const void* skip, void* dx,
+                         int dtype, void* stream);
 /* bilinear, align_corners=True: nn.Upsample(x2) and _upsample_and_match
  * (Unetmodel.py:51-60,118-119). bwd is a deterministic gather. */
-int nsm_resize_fwd(const float* x, int B, int Hi, int Wi, int C, float* y, int Ho, int Wo,
+int nsm_resize_fwd(const void* x, int B, int Hi, int Wi, int C, void* y, int Ho, int Wo, int dtype,
                    void* stream);
-int nsm_resize_bwd(const float* dy, int B, int Hi, int Wi, int C, float* dx, int Ho, int Wo,
-                   void* stream);
+int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho, int Wo,
+                   int dtype, void* stream);
 
 /* up x2 then resize to (th,tw) in one pass (Unetmodel.py:140-141: up9 then
  * _upsample_and_match back to the skip size); no 4x intermediate. */
-int nsm_up2_resize_fwd(const float* x, int B, int h, int w, int C, float* y, int th, int tw,
-                       void* stream);
-int nsm_up2_resize_bwd(const float* dy, int B, int h, int w, int C, float* dx, int th, int tw,
-                       void* stream);
+int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, void* y, int th, int tw,
+                       int dtype, void* stream);
+int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th, int tw,
+                       int dtype, void* stream);
 
 /* ---- model boundary ---------------------------------------------------------
  * pixel_unshuffle(2) + NCHW->NHWC + channel pad (Unetmodel.py:65-67,101) */
-int nsm_input_prep(const float* x, int B, int C, int H, int W, float* out, int cp, void* stream);
-int nsm_input_grad(const float* dX, int B, int C, int H, int W, int cp, float* dx, void* stream);
+int nsm_input_prep(const float* x, int B, int C, int H, int W, void* out, int cp, int dtype,
+                   void* stream);
+int nsm_input_grad(const void* dX, int B, int C, int H, int W, int cp, float* dx, int dtype,
+                   void* stream);
 /* conv10 1x1 16->4 + pixel_shuffle(2) + sigmoid (Unetmodel.py:63,143-148) */
-int nsm_head_fwd(const float* z, int ldz, int B, int Rh, int Rw, const float* w10,
-                 const float* b10, float* out, void* stream);
+int nsm_head_fwd(const void* z, int ldz, int B, int Rh, int Rw, const float* w10,
+                 const float* b10, float* out, int dtype, void* stream);
 int nsm_head_bwd_blocks(int B, int Rh, int Rw);
-int nsm_head_bwd(const float* gout, const float* out, const float* z, int ldz, int B, int Rh,
-                 int Rw, const float* w10, float* dz, float* partial, float* dw10, float* db10,
-                 void* stream);
+int nsm_head_bwd(const float* gout, const float* out, const void* z, int ldz, int B, int Rh,
+                 int Rw, const float* w10, void* dz, float* partial, float* dw10, float* db10,
+                 int dtype, void* stream);
 
 /* ---- losses -----------------------------------------------------------------
  * nn.L1Loss (customLoss.py:96,134) scaled by alpha (customLoss.py:160);
@@ -206,6 +216,23 @@ int nsm_clip_coef(const float* sumsq, float inv_world, float max_norm, float* co
 int nsm_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, float lr, float beta1,
                    float beta2, float eps, float weight_decay, int step, const float* gcoef,
                    void* stream);
+
+/* ---- bf16 convolutions (BASELINE config 3) ---------------------------------
+ * Same contracts as nsm_pack_conv_weight / nsm_conv_fwd_stats / nsm_conv_wgrad
+ * with bf16 activations and packed weights (v_mfma_f32_32x32x16_bf16, fp32
+ * accumulation). y = bf16(acc + bias); the fused BN partials are taken on the
+ * rounded values (what BatchNorm reads under autocast); dw stays fp32. */
+int nsm_pack_conv_weight_bf16(const float* w, int cout, int cin, int ksize, int cout_p, int cin_p,
+                              int mode, void* out, void* stream);
+int nsm_conv_fwd_bf16(const void* x, int ldx, int B, int H, int W, int cin_p, const void* wpk,
+                      const float* bias, int cout_p, int ksize, void* y, int ldy,
+                      const float* pro_scale, const float* pro_shift, const float* pro_mask,
+                      float slope, float* stats, void* stream);
+size_t nsm_conv_wgrad_bf16_ws(int B, int H, int W, int cin_p, int cout_p, int ksize);
+int nsm_conv_wgrad_bf16(const void* dy, int lddy, const void* x, int ldx, int B, int H, int W,
+                        int cin_p, int cout_p, int ksize, const float* pro_scale,
+                        const float* pro_shift, const float* pro_mask, float slope, float* ws,
+                        size_t ws_floats, int cin, int cout, float* dw, void* stream);
 
 /* ---- VGG19 perceptual loss (customLoss.py:7-90, forward only) ------------
  * nsm_vgg_prep: out[2B*H*W][32] NHWC = (nan_to_num(clamp(v,0,1)) - mean)/denom

@@ -70,6 +70,35 @@ __device__ __forceinline__ float lrelu_grad(float z, float slope) {
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// ---- bf16 storage (NSM_BF16 tensors): raw 16-bit words, fp32 arithmetic ------
+typedef unsigned short bf16_t;
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float bf_lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  bf16x2 v = __builtin_convertvector((f32x2){a, b}, bf16x2);  // v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, v);
+}
+__device__ __forceinline__ float round_bf(float a) { return bf_lo(pack_bf2(a, 0.f)); }
+
+// 4 consecutive elements of a T = float | bf16_t buffer as / from f32x4
+__device__ __forceinline__ f32x4 ld4(const float* p) { return *(const f32x4*)p; }
+__device__ __forceinline__ f32x4 ld4(const bf16_t* p) {
+  const u32x2 w = *(const u32x2*)p;
+  return f32x4{bf_lo(w.x), bf_hi(w.x), bf_lo(w.y), bf_hi(w.y)};
+}
+__device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
+__device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
+  *(u32x2*)p = u32x2{pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
+}
+__device__ __forceinline__ float ld1(const float* p) { return *p; }
+__device__ __forceinline__ float ld1(const bf16_t* p) { return __uint_as_float((uint32_t)*p << 16); }
+__device__ __forceinline__ void st1(float* p, float v) { *p = v; }
+__device__ __forceinline__ void st1(bf16_t* p, float v) { *p = (bf16_t)(pack_bf2(v, 0.f) & 0xFFFFu); }
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace nsm

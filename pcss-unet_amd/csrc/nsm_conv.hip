@@ -338,7 +338,14 @@ struct EpiStore {
       }
     }
     if (!e.stats) return;
-    // ---- fused BatchNorm batch statistics of this block's rows (two-pass) ----
+    stats_only<TM, TN, WM, WN>(e, acc, cx, M, N);
+  }
+  // fused BatchNorm batch statistics of this block's rows (two-pass); also
+  // used by the bf16 store epilogue on its rounded values
+  template <int TM, int TN, int WM, int WN>
+  __device__ static void stats_only(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M,
+                                    int N) {
+    const int col = cx.lane & 31, h = cx.lane >> 5;
     constexpr int BN = WN * TN * 32;
     float* red = cx.lds;  // [WM][BN]
     const int cnt = min(M - cx.m0, WM * TM * 32);
@@ -699,6 +706,28 @@ __global__ void __launch_bounds__(256) splitsum_kernel(const float* __restrict__
   }
   if (s < s1) a += p[(size_t)s * L4];
   ((f32x4*)dst)[(size_t)g * L4 + i] = a + b;
+}
+
+// split-K slabs -> dw (reference layout): optional 16-way first stage, then
+// the transposing reduction
+static int wgrad_finish(float* ws, const WgradPlan& pl, int M, int N, int cin_p, int taps, int cin,
+                        int cout, float* dw, hipStream_t s) {
+  const float* red_src = ws;
+  int red_splits = pl.splits;
+  if (pl.splits > 16) {
+    const int per = 16, groups = ceil_div(pl.splits, per);
+    long long L4 = (long long)M * N / 4;
+    float* stage = ws + (size_t)pl.splits * M * N;
+    hipLaunchKernelGGL(splitsum_kernel, dim3(ceil_div(L4, 256), groups), dim3(256), 0, s, ws,
+                       pl.splits, L4, per, stage);
+    NSM_LAUNCH_CHECK("conv_wgrad splitsum");
+    red_src = stage;
+    red_splits = groups;
+  }
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(cin, 64), cout), dim3(256), 0, s, red_src,
+                     red_splits, M, N, cin_p, taps, cin, cout, dw);
+  NSM_LAUNCH_CHECK("conv_wgrad reduce");
+  return 0;
 }
 
 __global__ void pack_weight_kernel(const float* __restrict__ w, int cout, int cin, int taps,
@@ -1149,25 +1178,7 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
   else
     rc = dispatch_wgrad<false, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
   if (rc) return rc;
-  int taps = ksize * ksize;
-  const float* red_src = ws;
-  int red_splits = pl.splits;
-  if (pl.splits > 16) {
-    // two-stage reduction: groups of 16 splits summed in parallel into the
-    // tail of the workspace (planned by plan_wgrad), then the transposing pass
-    const int per = 16, groups = ceil_div(pl.splits, per);
-    long long L4 = (long long)M * N / 4;
-    float* stage = ws + (size_t)pl.splits * M * N;
-    hipLaunchKernelGGL(splitsum_kernel, dim3(ceil_div(L4, 256), groups), dim3(256), 0, s, ws,
-                       pl.splits, L4, per, stage);
-    NSM_LAUNCH_CHECK("conv_wgrad splitsum");
-    red_src = stage;
-    red_splits = groups;
-  }
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(ceil_div(cin, 64), cout), dim3(256), 0, s, red_src,
-                     red_splits, M, N, cin_p, taps, cin, cout, dw);
-  NSM_LAUNCH_CHECK("conv_wgrad reduce");
-  return 0;
+  return wgrad_finish(ws, pl, M, N, cin_p, ksize * ksize, cin, cout, dw, s);
 }
 
 // ---- Winograd host side: tile in {2, 4} selects F(2x2,3x3) / F(4x4,3x3) -------
@@ -1394,3 +1405,6 @@ extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V,
   NSM_LAUNCH_CHECK("wino_wgrad_out");
   return 0;
 }
+
+namespace nsm {
+#include "nsm_conv_bf16.inc"

@@ -50,7 +50,8 @@ __device__ __forceinline__ void col_tree_reduce(f32x4* red, int cl, int rl, int 
   __syncthreads();
 }
 
-__global__ void __launch_bounds__(256) bn_stats_kernel(const float* __restrict__ y, int ld, int M,
+template <typename T>
+__global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ y, int ld, int M,
                                                        int C, int cl, int rl, int rpc,
                                                        float* __restrict__ partial) {
   __shared__ f32x4 red[256];
@@ -58,7 +59,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const float* __restrict__
   const int c = (blockIdx.x * cl + tc) * 4;
   const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  for (int r = r0 + tr; r < r1; r += rl) s += *(const f32x4*)(y + (size_t)r * ld + c);
+  for (int r = r0 + tr; r < r1; r += rl) s += ld4(y + (size_t)r * ld + c);
   red[tid] = s;
   col_tree_reduce(red, cl, rl, tid);
   const float n = (float)max(r1 - r0, 1);
@@ -67,7 +68,7 @@ __global__ void __launch_bounds__(256) bn_stats_kernel(const float* __restrict__
   __syncthreads();
   f32x4 s2 = {0.f, 0.f, 0.f, 0.f};
   for (int r = r0 + tr; r < r1; r += rl) {
-    f32x4 d = *(const f32x4*)(y + (size_t)r * ld + c) - mean;
+    f32x4 d = ld4(y + (size_t)r * ld + c) - mean;
     s2 += d * d;
   }
   red[tid] = s2;
@@ -163,23 +164,24 @@ __global__ void bn_finalize_eval_kernel(const float* __restrict__ rm, const floa
   shift_o[c] = beta[c] - m * sc;
 }
 
-__global__ void bn_act_kernel(const float* __restrict__ y, int ldy, int M, int C4,
+template <typename T>
+__global__ void bn_act_kernel(const T* __restrict__ y, int ldy, int M, int C4,
                               const float* __restrict__ scale, const float* __restrict__ shift,
-                              float slope, const float* __restrict__ res, int ldres,
-                              float* __restrict__ out, int ldo) {
+                              float slope, const T* __restrict__ res, int ldres,
+                              T* __restrict__ out, int ldo) {
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long total = (long long)M * C4;
   for (; i < total; i += (long long)gridDim.x * blockDim.x) {
     int p = (int)(i / C4), c = (int)(i - (long long)p * C4) * 4;
-    f32x4 v = *(const f32x4*)(y + (size_t)p * ldy + c);
+    f32x4 v = ld4(y + (size_t)p * ldy + c);
     f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
     f32x4 o;
     o.x = lrelu(v.x * sc.x + sh.x, slope);
     o.y = lrelu(v.y * sc.y + sh.y, slope);
     o.z = lrelu(v.z * sc.z + sh.z, slope);
     o.w = lrelu(v.w * sc.w + sh.w, slope);
-    if (res) o += *(const f32x4*)(res + (size_t)p * ldres + c);
-    *(f32x4*)(out + (size_t)p * ldo + c) = o;
+    if (res) o += ld4(res + (size_t)p * ldres + c);
+    st4(out + (size_t)p * ldo + c, o);
   }
 }
 
@@ -198,8 +200,9 @@ __device__ __forceinline__ f32x4 bn_dz(const f32x4 g, const f32x4 v, const f32x4
   return d;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
-    const float* __restrict__ g, int ldg, const float* __restrict__ y, int ldy, int M, int C,
+    const T* __restrict__ g, int ldg, const T* __restrict__ y, int ldy, int M, int C,
     FastDiv fdHW, const float* __restrict__ scale, const float* __restrict__ shift, float slope,
     const float* __restrict__ mask, const float* __restrict__ mean,
     const float* __restrict__ invstd, int cl, int rl, int rpc, float* __restrict__ partial) {
@@ -211,8 +214,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   const f32x4 mu = *(const f32x4*)(mean + c), is = *(const f32x4*)(invstd + c);
   f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
   for (int r = r0 + tr; r < r1; r += rl) {
-    f32x4 v = *(const f32x4*)(y + (size_t)r * ldy + c);
-    f32x4 gg = *(const f32x4*)(g + (size_t)r * ldg + c);
+    f32x4 v = ld4(y + (size_t)r * ldy + c);
+    f32x4 gg = ld4(g + (size_t)r * ldg + c);
     int b = mask ? (int)fdiv((uint32_t)r, fdHW) : 0;
     f32x4 dz = bn_dz(gg, v, sc, sh, slope, mask, b, C, c);
     s1 += dz;
@@ -269,34 +272,36 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
   }
 }
 
-__global__ void bn_bwd_apply_kernel(const float* __restrict__ g, int ldg,
-                                    const float* __restrict__ y, int ldy, int M, int C,
+template <typename T>
+__global__ void bn_bwd_apply_kernel(const T* __restrict__ g, int ldg,
+                                    const T* __restrict__ y, int ldy, int M, int C,
                                     FastDiv fdHW, const float* __restrict__ scale,
                                     const float* __restrict__ shift, float slope,
                                     const float* __restrict__ mask, const float* __restrict__ mean,
-                                    const float* __restrict__ coef, float* __restrict__ dy,
+                                    const float* __restrict__ coef, T* __restrict__ dy,
                                     int lddy) {
   const int C4 = C / 4;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   long long total = (long long)M * C4;
   for (; i < total; i += (long long)gridDim.x * blockDim.x) {
     int p = (int)(i / C4), c = (int)(i - (long long)p * C4) * 4;
-    f32x4 v = *(const f32x4*)(y + (size_t)p * ldy + c);
-    f32x4 gg = *(const f32x4*)(g + (size_t)p * ldg + c);
+    f32x4 v = ld4(y + (size_t)p * ldy + c);
+    f32x4 gg = ld4(g + (size_t)p * ldg + c);
     f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
     int b = mask ? (int)fdiv((uint32_t)p, fdHW) : 0;
     f32x4 dz = bn_dz(gg, v, sc, sh, slope, mask, b, C, c);
     f32x4 k1 = *(const f32x4*)(coef + c), k2 = *(const f32x4*)(coef + C + c),
           k3 = *(const f32x4*)(coef + 2 * C + c), mu = *(const f32x4*)(mean + c);
-    *(f32x4*)(dy + (size_t)p * lddy + c) = k1 * dz + k2 * (v - mu) + k3;
+    st4(dy + (size_t)p * lddy + c, k1 * dz + k2 * (v - mu) + k3);
   }
 }
 
 // ---------------------------------------------------------------------------
 // AvgPool2d(2), floor mode
 // ---------------------------------------------------------------------------
-__global__ void avgpool2_fwd_kernel(const float* __restrict__ x, int B, int H, int W, int C4,
-                                    float* __restrict__ y) {
+template <typename T>
+__global__ void avgpool2_fwd_kernel(const T* __restrict__ x, int B, int H, int W, int C4,
+                                    T* __restrict__ y) {
   const int Ho = H / 2, Wo = W / 2;
   long long total = (long long)B * Ho * Wo * C4;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -307,18 +312,19 @@ __global__ void avgpool2_fwd_kernel(const float* __restrict__ x, int B, int H, i
     t /= Wo;
     int oy = (int)(t % Ho);
     int b = (int)(t / Ho);
-    const float* base = x + (((size_t)b * H + 2 * oy) * W + 2 * ox) * (C4 * 4) + c * 4;
+    const T* base = x + (((size_t)b * H + 2 * oy) * W + 2 * ox) * (C4 * 4) + c * 4;
     size_t rs = (size_t)W * C4 * 4, cs = (size_t)C4 * 4;
-    f32x4 s = *(const f32x4*)base;
-    s += *(const f32x4*)(base + cs);
-    s += *(const f32x4*)(base + rs);
-    s += *(const f32x4*)(base + rs + cs);
-    *(f32x4*)(y + (size_t)i * 4) = s * 0.25f;
+    f32x4 s = ld4(base);
+    s += ld4(base + cs);
+    s += ld4(base + rs);
+    s += ld4(base + rs + cs);
+    st4(y + (size_t)i * 4, s * 0.25f);
   }
 }
 
-__global__ void avgpool2_bwd_add_kernel(const float* __restrict__ dy, int B, int H, int W, int C4,
-                                        const float* __restrict__ skip, float* __restrict__ dx) {
+template <typename T>
+__global__ void avgpool2_bwd_add_kernel(const T* __restrict__ dy, int B, int H, int W, int C4,
+                                        const T* __restrict__ skip, T* __restrict__ dx) {
   const int Ho = H / 2, Wo = W / 2;
   long long total = (long long)B * H * W * C4;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -329,11 +335,10 @@ __global__ void avgpool2_bwd_add_kernel(const float* __restrict__ dy, int B, int
     t /= W;
     int yy = (int)(t % H);
     int b = (int)(t / H);
-    f32x4 v = skip ? *(const f32x4*)(skip + (size_t)i * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 v = skip ? ld4(skip + (size_t)i * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
     int oy = yy >> 1, ox = xx >> 1;
-    if (oy < Ho && ox < Wo)
-      v += *(const f32x4*)(dy + ((((size_t)b * Ho + oy) * Wo + ox) * C4 + c) * 4) * 0.25f;
-    *(f32x4*)(dx + (size_t)i * 4) = v;
+    if (oy < Ho && ox < Wo) v += ld4(dy + ((((size_t)b * Ho + oy) * Wo + ox) * C4 + c) * 4) * 0.25f;
+    st4(dx + (size_t)i * 4, v);
   }
 }
 
@@ -358,9 +363,9 @@ static inline float ac_scale(int in, int out) {
   return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
 }
 
-template <bool VEC>
-__global__ void resize_fwd_kernel(const float* __restrict__ x, int B, int Hi, int Wi, int C,
-                                  float* __restrict__ y, int Ho, int Wo, float sh, float sw) {
+template <bool VEC, typename T>
+__global__ void resize_fwd_kernel(const T* __restrict__ x, int B, int Hi, int Wi, int C,
+                                  T* __restrict__ y, int Ho, int Wo, float sh, float sw) {
   const int CV = VEC ? C / 4 : C;
   long long total = (long long)B * Ho * Wo * CV;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -377,17 +382,18 @@ __global__ void resize_fwd_kernel(const float* __restrict__ x, int B, int Hi, in
     lin_idx(sw, ox, Wi, x0, x1, lx0, lx1);
     const size_t rb = (size_t)b * Hi;
     if constexpr (VEC) {
-      const float* p00 = x + ((rb + y0) * Wi + x0) * C + c * 4;
-      const float* p01 = x + ((rb + y0) * Wi + x1) * C + c * 4;
-      const float* p10 = x + ((rb + y1) * Wi + x0) * C + c * 4;
-      const float* p11 = x + ((rb + y1) * Wi + x1) * C + c * 4;
-      f32x4 v = ly0 * (lx0 * *(const f32x4*)p00 + lx1 * *(const f32x4*)p01) +
-                ly1 * (lx0 * *(const f32x4*)p10 + lx1 * *(const f32x4*)p11);
-      *(f32x4*)(y + (size_t)i * 4) = v;
+      const T* p00 = x + ((rb + y0) * Wi + x0) * C + c * 4;
+      const T* p01 = x + ((rb + y0) * Wi + x1) * C + c * 4;
+      const T* p10 = x + ((rb + y1) * Wi + x0) * C + c * 4;
+      const T* p11 = x + ((rb + y1) * Wi + x1) * C + c * 4;
+      f32x4 v = ly0 * (lx0 * ld4(p00) + lx1 * ld4(p01)) + ly1 * (lx0 * ld4(p10) + lx1 * ld4(p11));
+      st4(y + (size_t)i * 4, v);
     } else {
-      float v = ly0 * (lx0 * x[((rb + y0) * Wi + x0) * C + c] + lx1 * x[((rb + y0) * Wi + x1) * C + c]) +
-                ly1 * (lx0 * x[((rb + y1) * Wi + x0) * C + c] + lx1 * x[((rb + y1) * Wi + x1) * C + c]);
-      y[i] = v;
+      float v = ly0 * (lx0 * ld1(x + ((rb + y0) * Wi + x0) * C + c) +
+                       lx1 * ld1(x + ((rb + y0) * Wi + x1) * C + c)) +
+                ly1 * (lx0 * ld1(x + ((rb + y1) * Wi + x0) * C + c) +
+                       lx1 * ld1(x + ((rb + y1) * Wi + x1) * C + c));
+      st1(y + i, v);
     }
   }
 }
@@ -410,9 +416,9 @@ __device__ __forceinline__ void cand_range(float scale, int i, int out, int& lo,
   hi = min(out - 1, (int)ceilf((float)(i + 1) / scale) + 1);
 }
 
-template <bool VEC>
-__global__ void resize_bwd_kernel(const float* __restrict__ dy, int B, int Hi, int Wi, int C,
-                                  float* __restrict__ dx, int Ho, int Wo, float sh, float sw) {
+template <bool VEC, typename T>
+__global__ void resize_bwd_kernel(const T* __restrict__ dy, int B, int Hi, int Wi, int C,
+                                  T* __restrict__ dx, int Ho, int Wo, float sh, float sw) {
   const int CV = VEC ? C / 4 : C;
   long long total = (long long)B * Hi * Wi * CV;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -434,20 +440,20 @@ __global__ void resize_bwd_kernel(const float* __restrict__ dy, int B, int Hi, i
     for (int oy = ylo; oy <= yhi; ++oy) {
       float wy = lin_w(sh, oy, Hi, iy);
       if (wy == 0.f) continue;
-      const float* row = dy + ((size_t)b * Ho + oy) * Wo * C;
+      const T* row = dy + ((size_t)b * Ho + oy) * Wo * C;
       for (int k = 0; k < nx; ++k) {
         float w = wxs[k];
         if (w == 0.f) continue;
         if constexpr (VEC)
-          acc4 += (wy * w) * *(const f32x4*)(row + (size_t)(xs0 + k) * C + c * 4);
+          acc4 += (wy * w) * ld4(row + (size_t)(xs0 + k) * C + c * 4);
         else
-          acc += (wy * w) * row[(size_t)(xs0 + k) * C + c];
+          acc += (wy * w) * ld1(row + (size_t)(xs0 + k) * C + c);
       }
     }
     if constexpr (VEC)
-      *(f32x4*)(dx + (size_t)i * 4) = acc4;
+      st4(dx + (size_t)i * 4, acc4);
     else
-      dx[i] = acc;
+      st1(dx + i, acc);
   }
 }
 
@@ -458,21 +464,23 @@ __global__ void resize_bwd_kernel(const float* __restrict__ dy, int B, int Hi, i
 // two-step path rounds them (fp32 per intermediate sample); backward uses the
 // separable combined weights W[o->i] = sum_m w2(o->m) w1(m->i).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ f32x4 up_sample4(const float* __restrict__ x, size_t rb, int h, int w,
+template <typename T>
+__device__ __forceinline__ f32x4 up_sample4(const T* __restrict__ x, size_t rb, int h, int w,
                                             int C, int c4, float s1h, float s1w, int my, int mx) {
   int y0, y1, x0, x1;
   float a0, a1, b0, b1;
   lin_idx(s1h, my, h, y0, y1, a0, a1);
   lin_idx(s1w, mx, w, x0, x1, b0, b1);
-  const f32x4 v00 = *(const f32x4*)(x + ((rb + y0) * w + x0) * C + c4 * 4);
-  const f32x4 v01 = *(const f32x4*)(x + ((rb + y0) * w + x1) * C + c4 * 4);
-  const f32x4 v10 = *(const f32x4*)(x + ((rb + y1) * w + x0) * C + c4 * 4);
-  const f32x4 v11 = *(const f32x4*)(x + ((rb + y1) * w + x1) * C + c4 * 4);
+  const f32x4 v00 = ld4(x + ((rb + y0) * w + x0) * C + c4 * 4);
+  const f32x4 v01 = ld4(x + ((rb + y0) * w + x1) * C + c4 * 4);
+  const f32x4 v10 = ld4(x + ((rb + y1) * w + x0) * C + c4 * 4);
+  const f32x4 v11 = ld4(x + ((rb + y1) * w + x1) * C + c4 * 4);
   return a0 * (b0 * v00 + b1 * v01) + a1 * (b0 * v10 + b1 * v11);
 }
 
-__global__ void up2_resize_fwd_kernel(const float* __restrict__ x, int B, int h, int w, int C,
-                                      float* __restrict__ y, int th, int tw, float s1h, float s1w,
+template <typename T>
+__global__ void up2_resize_fwd_kernel(const T* __restrict__ x, int B, int h, int w, int C,
+                                      T* __restrict__ y, int th, int tw, float s1h, float s1w,
                                       float s2h, float s2w) {
   const int C4 = C / 4, h2 = 2 * h, w2 = 2 * w;
   long long total = (long long)B * th * tw * C4;
@@ -493,7 +501,7 @@ __global__ void up2_resize_fwd_kernel(const float* __restrict__ x, int B, int h,
     f32x4 u01 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m0, n1);
     f32x4 u10 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m1, n0);
     f32x4 u11 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m1, n1);
-    *(f32x4*)(y + (size_t)i * 4) = l0 * (k0 * u00 + k1 * u01) + l1 * (k0 * u10 + k1 * u11);
+    st4(y + (size_t)i * 4, l0 * (k0 * u00 + k1 * u01) + l1 * (k0 * u10 + k1 * u11));
   }
 }
 
@@ -508,8 +516,9 @@ __device__ __forceinline__ float comb_w(float s2, int o, int n2, float s1, int n
   return wgt;
 }
 
-__global__ void up2_resize_bwd_kernel(const float* __restrict__ dy, int B, int h, int w, int C,
-                                      float* __restrict__ dx, int th, int tw, float s1h, float s1w,
+template <typename T>
+__global__ void up2_resize_bwd_kernel(const T* __restrict__ dy, int B, int h, int w, int C,
+                                      T* __restrict__ dx, int th, int tw, float s1h, float s1w,
                                       float s2h, float s2w) {
   const int C4 = C / 4, h2 = 2 * h, w2 = 2 * w;
   long long total = (long long)B * h * w * C4;
@@ -541,13 +550,13 @@ __global__ void up2_resize_bwd_kernel(const float* __restrict__ dy, int B, int h
     for (int oy = olo; oy <= ohi; ++oy) {
       float wy = comb_w(s2h, oy, h2, s1h, h, iy);
       if (wy == 0.f) continue;
-      const float* row = dy + ((size_t)b * th + oy) * tw * C + c * 4;
+      const T* row = dy + ((size_t)b * th + oy) * tw * C + c * 4;
       for (int k = 0; k < nx; ++k) {
         if (wx[k] == 0.f) continue;
-        acc += (wy * wx[k]) * *(const f32x4*)(row + (size_t)(plo + k) * C);
+        acc += (wy * wx[k]) * ld4(row + (size_t)(plo + k) * C);
       }
     }
-    *(f32x4*)(dx + (size_t)i * 4) = acc;
+    st4(dx + (size_t)i * 4, acc);
   }
 }
 
@@ -555,8 +564,9 @@ __global__ void up2_resize_bwd_kernel(const float* __restrict__ dy, int B, int h
 // Model boundary: pixel_unshuffle(2) + NCHW->NHWC (+ zero channel pad), and its
 // inverse for the input gradient.
 // ---------------------------------------------------------------------------
+template <typename T>
 __global__ void input_prep_kernel(const float* __restrict__ x, int B, int C, int H, int W,
-                                  float* __restrict__ out, int cp) {
+                                  T* __restrict__ out, int cp) {
   const int Rh = H / 2, Rw = W / 2;
   long long total = (long long)B * Rh * Rw * cp;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -572,11 +582,12 @@ __global__ void input_prep_kernel(const float* __restrict__ x, int B, int C, int
       int c = ch >> 2, di = (ch >> 1) & 1, dj = ch & 1;
       v = x[(((size_t)b * C + c) * H + 2 * ry + di) * W + 2 * rx + dj];
     }
-    out[i] = v;
+    st1(out + i, v);
   }
 }
 
-__global__ void input_grad_kernel(const float* __restrict__ dX, int B, int C, int H, int W, int cp,
+template <typename T>
+__global__ void input_grad_kernel(const T* __restrict__ dX, int B, int C, int H, int W, int cp,
                                   float* __restrict__ dx) {
   // thread per (b, c, ry, rx): one float4 of dX (channels 4c..4c+3 of pixel
   // (ry,rx)) -> the 2x2 block of plane c; rx fastest so stores coalesce.
@@ -590,9 +601,8 @@ __global__ void input_grad_kernel(const float* __restrict__ dX, int B, int C, in
     t /= Rh;
     int c = (int)(t % C);
     int b = (int)(t / C);
-    f32x4 v = *(const f32x4*)(dX + (((size_t)b * Rh + ry) * Rw + rx) * cp + 4 * c);
+    f32x4 v = ld4(dX + (((size_t)b * Rh + ry) * Rw + rx) * cp + 4 * c);
     float* o = dx + (((size_t)b * C + c) * H + 2 * ry) * W + 2 * rx;
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
     *(f32x2*)o = f32x2{v.x, v.y};
     *(f32x2*)(o + W) = f32x2{v.z, v.w};
   }
@@ -601,7 +611,8 @@ __global__ void input_grad_kernel(const float* __restrict__ dX, int B, int C, in
 // ---------------------------------------------------------------------------
 // Head: conv10 (1x1, 16->4, bias) -> pixel_shuffle(2) -> sigmoid
 // ---------------------------------------------------------------------------
-__global__ void head_fwd_kernel(const float* __restrict__ z, int ldz, int B, int Rh, int Rw,
+template <typename T>
+__global__ void head_fwd_kernel(const T* __restrict__ z, int ldz, int B, int Rh, int Rw,
                                 const float* __restrict__ w10, const float* __restrict__ b10,
                                 float* __restrict__ out) {
   __shared__ float w[68];
@@ -612,10 +623,10 @@ __global__ void head_fwd_kernel(const float* __restrict__ z, int ldz, int B, int
   for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < npix;
        p += (long long)gridDim.x * blockDim.x) {
     float zz[16];
-    const float* zr = z + (size_t)p * ldz;
+    const T* zr = z + (size_t)p * ldz;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      f32x4 v = *(const f32x4*)(zr + 4 * q);
+      f32x4 v = ld4(zr + 4 * q);
       zz[4 * q] = v.x;
       zz[4 * q + 1] = v.y;
       zz[4 * q + 2] = v.z;
@@ -644,9 +655,10 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+template <typename T>
 __global__ void __launch_bounds__(256) head_bwd_kernel(
-    const float* __restrict__ gout, const float* __restrict__ out, const float* __restrict__ z,
-    int ldz, int B, int Rh, int Rw, const float* __restrict__ w10, float* __restrict__ dz,
+    const float* __restrict__ gout, const float* __restrict__ out, const T* __restrict__ z,
+    int ldz, int B, int Rh, int Rw, const float* __restrict__ w10, T* __restrict__ dz,
     float* __restrict__ partial) {
   __shared__ float w[64];
   __shared__ float red[4][68];
@@ -670,11 +682,11 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(
       float ov = out[o];
       d[j] = gout[o] * (1.f - ov) * ov;  // ATen sigmoid_backward
     }
-    const float* zr = z + (size_t)p * ldz;
-    float* dzr = dz + (size_t)p * ldz;
+    const T* zr = z + (size_t)p * ldz;
+    T* dzr = dz + (size_t)p * ldz;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      f32x4 v = *(const f32x4*)(zr + 4 * q);
+      f32x4 v = ld4(zr + 4 * q);
       float zv[4] = {v.x, v.y, v.z, v.w};
       f32x4 g;
       float gv[4];
@@ -689,9 +701,9 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(
       g.y = gv[1];
       g.z = gv[2];
       g.w = gv[3];
-      *(f32x4*)(dzr + 4 * q) = g;
+      st4(dzr + 4 * q, g);
     }
-    for (int c = 16; c < ldz; c += 4) *(f32x4*)(dzr + c) = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 16; c < ldz; c += 4) st4(dzr + c, f32x4{0.f, 0.f, 0.f, 0.f});
 #pragma unroll
     for (int j = 0; j < 4; ++j) accw[64 + j] += d[j];
   }
@@ -889,13 +901,21 @@ extern "C" int nsm_reduce_chunks(int M, int C) {
   return colred_plan(M, C).nchunk;
 }
 
-extern "C" int nsm_bn_stats(const float* y, int ld, int M, int C, float* partial, int nchunk,
-                            void* stream) {
+#define NSM_T(T, p) ((T*)(p))
+#define NSM_CT(T, p) ((const T*)(p))
+
+extern "C" int nsm_bn_stats(const void* y, int ld, int M, int C, float* partial, int nchunk,
+                            int dtype, void* stream) {
   NSM_CHECK_ARG(y && partial && M > 0 && C % 4 == 0 && ld % 4 == 0, "bn_stats: bad args");
   ColRed r = colred_plan(M, C);
   NSM_CHECK_ARG(nchunk == r.nchunk, "bn_stats: nchunk %d != %d", nchunk, r.nchunk);
-  hipLaunchKernelGGL(bn_stats_kernel, dim3(r.gx, r.nchunk), dim3(256), 0, as_stream(stream), y, ld,
-                     M, C, r.cl, r.rl, r.rpc, partial);
+  dim3 g(r.gx, r.nchunk);
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, y), ld, M, C, r.cl, r.rl, r.rpc, partial);
+  else
+    hipLaunchKernelGGL(bn_stats_kernel<float>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, y), ld, M, C, r.cl, r.rl, r.rpc, partial);
   NSM_LAUNCH_CHECK("bn_stats");
   return 0;
 }
@@ -934,28 +954,41 @@ extern "C" int nsm_bn_finalize_eval(const float* run_mean, const float* run_var,
   return 0;
 }
 
-extern "C" int nsm_bn_act(const float* y, int ldy, int M, int C, const float* scale,
-                          const float* shift, float slope, const float* res, int ldres, float* out,
-                          int ldo, void* stream) {
+extern "C" int nsm_bn_act(const void* y, int ldy, int M, int C, const float* scale,
+                          const float* shift, float slope, const void* res, int ldres, void* out,
+                          int ldo, int dtype, void* stream) {
   NSM_CHECK_ARG(y && scale && shift && out && C % 4 == 0, "bn_act: bad args");
   long long work = (long long)M * (C / 4);
-  hipLaunchKernelGGL(bn_act_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), y, ldy,
-                     M, C / 4, scale, shift, slope, res, ldres, out, ldo);
+  dim3 g(grid_for(work));
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(bn_act_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, y), ldy, M, C / 4, scale, shift, slope, NSM_CT(bf16_t, res),
+                       ldres, NSM_T(bf16_t, out), ldo);
+  else
+    hipLaunchKernelGGL(bn_act_kernel<float>, g, dim3(256), 0, as_stream(stream), NSM_CT(float, y),
+                       ldy, M, C / 4, scale, shift, slope, NSM_CT(float, res), ldres,
+                       NSM_T(float, out), ldo);
   NSM_LAUNCH_CHECK("bn_act");
   return 0;
 }
 
-extern "C" int nsm_bn_bwd_reduce(const float* g, int ldg, const float* y, int ldy, int M, int C,
+extern "C" int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy, int M, int C,
                                  int HW, const float* scale, const float* shift, float slope,
                                  const float* mask, const float* mean, const float* invstd,
-                                 float* partial, int nchunk, void* stream) {
+                                 float* partial, int nchunk, int dtype, void* stream) {
   NSM_CHECK_ARG(g && y && scale && shift && mean && invstd && partial && C % 4 == 0,
                 "bn_bwd_reduce: bad args");
   ColRed r = colred_plan(M, C);
   NSM_CHECK_ARG(nchunk == r.nchunk, "bn_bwd_reduce: nchunk mismatch");
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(r.gx, r.nchunk), dim3(256), 0, as_stream(stream),
-                     g, ldg, y, ldy, M, C, make_fastdiv(HW), scale, shift, slope, mask, mean,
-                     invstd, r.cl, r.rl, r.rpc, partial);
+  dim3 gr(r.gx, r.nchunk);
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, gr, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, make_fastdiv(HW),
+                       scale, shift, slope, mask, mean, invstd, r.cl, r.rl, r.rpc, partial);
+  else
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, gr, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, make_fastdiv(HW), scale,
+                       shift, slope, mask, mean, invstd, r.cl, r.rl, r.rpc, partial);
   NSM_LAUNCH_CHECK("bn_bwd_reduce");
   return 0;
 }
@@ -971,59 +1004,80 @@ extern "C" int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int 
   return 0;
 }
 
-extern "C" int nsm_bn_bwd_apply(const float* g, int ldg, const float* y, int ldy, int M, int C,
+extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, int M, int C,
                                 int HW, const float* scale, const float* shift, float slope,
-                                const float* mask, const float* mean, const float* coef, float* dy,
-                                int lddy, void* stream) {
+                                const float* mask, const float* mean, const float* coef, void* dy,
+                                int lddy, int dtype, void* stream) {
   NSM_CHECK_ARG(g && y && scale && shift && mean && coef && dy && C % 4 == 0,
                 "bn_bwd_apply: bad args");
   long long work = (long long)M * (C / 4);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), g,
-                     ldg, y, ldy, M, C, make_fastdiv(HW), scale, shift, slope, mask, mean, coef, dy,
-                     lddy);
+  dim3 gr(grid_for(work));
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, gr, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, make_fastdiv(HW),
+                       scale, shift, slope, mask, mean, coef, NSM_T(bf16_t, dy), lddy);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, gr, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, make_fastdiv(HW), scale,
+                       shift, slope, mask, mean, coef, NSM_T(float, dy), lddy);
   NSM_LAUNCH_CHECK("bn_bwd_apply");
   return 0;
 }
 
-extern "C" int nsm_avgpool2_fwd(const float* x, int B, int H, int W, int C, float* y,
+extern "C" int nsm_avgpool2_fwd(const void* x, int B, int H, int W, int C, void* y, int dtype,
                                 void* stream) {
   NSM_CHECK_ARG(x && y && C % 4 == 0 && H >= 2 && W >= 2, "avgpool2_fwd: bad args");
   long long work = (long long)B * (H / 2) * (W / 2) * (C / 4);
-  hipLaunchKernelGGL(avgpool2_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), x,
-                     B, H, W, C / 4, y);
+  dim3 g(grid_for(work));
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(avgpool2_fwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, x), B, H, W, C / 4, NSM_T(bf16_t, y));
+  else
+    hipLaunchKernelGGL(avgpool2_fwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, x), B, H, W, C / 4, NSM_T(float, y));
   NSM_LAUNCH_CHECK("avgpool2_fwd");
   return 0;
 }
 
-extern "C" int nsm_avgpool2_bwd_add(const float* dy, int B, int H, int W, int C,
-                                    const float* skip, float* dx, void* stream) {
+extern "C" int nsm_avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, const void* skip,
+                                    void* dx, int dtype, void* stream) {
   NSM_CHECK_ARG(dy && dx && C % 4 == 0, "avgpool2_bwd: bad args");
   long long work = (long long)B * H * W * (C / 4);
-  hipLaunchKernelGGL(avgpool2_bwd_add_kernel, dim3(grid_for(work)), dim3(256), 0,
-                     as_stream(stream), dy, B, H, W, C / 4, skip, dx);
+  dim3 g(grid_for(work));
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(avgpool2_bwd_add_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, dy), B, H, W, C / 4, NSM_CT(bf16_t, skip), NSM_T(bf16_t, dx));
+  else
+    hipLaunchKernelGGL(avgpool2_bwd_add_kernel<float>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, dy), B, H, W, C / 4, NSM_CT(float, skip), NSM_T(float, dx));
   NSM_LAUNCH_CHECK("avgpool2_bwd");
   return 0;
 }
 
-extern "C" int nsm_resize_fwd(const float* x, int B, int Hi, int Wi, int C, float* y, int Ho,
-                              int Wo, void* stream) {
+extern "C" int nsm_resize_fwd(const void* x, int B, int Hi, int Wi, int C, void* y, int Ho, int Wo,
+                              int dtype, void* stream) {
   NSM_CHECK_ARG(x && y && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0,
                 "resize_fwd: bad args");
   float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
   bool vec = C % 4 == 0;
   long long work = (long long)B * Ho * Wo * (vec ? C / 4 : C);
-  if (vec)
-    hipLaunchKernelGGL(resize_fwd_kernel<true>, dim3(grid_for(work)), dim3(256), 0,
-                       as_stream(stream), x, B, Hi, Wi, C, y, Ho, Wo, sh, sw);
-  else
-    hipLaunchKernelGGL(resize_fwd_kernel<false>, dim3(grid_for(work)), dim3(256), 0,
-                       as_stream(stream), x, B, Hi, Wi, C, y, Ho, Wo, sh, sw);
+  dim3 g(grid_for(work));
+  hipStream_t s = as_stream(stream);
+#define NSM_RF(V, T)                                                                          \
+  hipLaunchKernelGGL((resize_fwd_kernel<V, T>), g, dim3(256), 0, s, NSM_CT(T, x), B, Hi, Wi, C, \
+                     NSM_T(T, y), Ho, Wo, sh, sw)
+  if (dtype == NSM_BF16) {
+    if (vec) NSM_RF(true, bf16_t); else NSM_RF(false, bf16_t);
+  } else {
+    if (vec) NSM_RF(true, float); else NSM_RF(false, float);
+  }
+#undef NSM_RF
   NSM_LAUNCH_CHECK("resize_fwd");
   return 0;
 }
 
-extern "C" int nsm_resize_bwd(const float* dy, int B, int Hi, int Wi, int C, float* dx, int Ho,
-                              int Wo, void* stream) {
+extern "C" int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho, int Wo,
+                              int dtype, void* stream) {
   NSM_CHECK_ARG(dy && dx && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0,
                 "resize_bwd: bad args");
   float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
@@ -1031,69 +1085,101 @@ extern "C" int nsm_resize_bwd(const float* dy, int B, int Hi, int Wi, int C, flo
   NSM_CHECK_ARG(sw == 0.f || (2.f / sw + 4.f) < 16.f, "resize_bwd: scale too small");
   bool vec = C % 4 == 0;
   long long work = (long long)B * Hi * Wi * (vec ? C / 4 : C);
-  if (vec)
-    hipLaunchKernelGGL(resize_bwd_kernel<true>, dim3(grid_for(work)), dim3(256), 0,
-                       as_stream(stream), dy, B, Hi, Wi, C, dx, Ho, Wo, sh, sw);
-  else
-    hipLaunchKernelGGL(resize_bwd_kernel<false>, dim3(grid_for(work)), dim3(256), 0,
-                       as_stream(stream), dy, B, Hi, Wi, C, dx, Ho, Wo, sh, sw);
+  dim3 g(grid_for(work));
+  hipStream_t s = as_stream(stream);
+#define NSM_RB(V, T)                                                                           \
+  hipLaunchKernelGGL((resize_bwd_kernel<V, T>), g, dim3(256), 0, s, NSM_CT(T, dy), B, Hi, Wi, C, \
+                     NSM_T(T, dx), Ho, Wo, sh, sw)
+  if (dtype == NSM_BF16) {
+    if (vec) NSM_RB(true, bf16_t); else NSM_RB(false, bf16_t);
+  } else {
+    if (vec) NSM_RB(true, float); else NSM_RB(false, float);
+  }
+#undef NSM_RB
   NSM_LAUNCH_CHECK("resize_bwd");
   return 0;
 }
 
-extern "C" int nsm_up2_resize_fwd(const float* x, int B, int h, int w, int C, float* y, int th,
-                                  int tw, void* stream) {
+extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, void* y, int th,
+                                  int tw, int dtype, void* stream) {
   NSM_CHECK_ARG(x && y && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 4 == 0,
                 "up2_resize_fwd: bad args");
   long long work = (long long)B * th * tw * (C / 4);
-  hipLaunchKernelGGL(up2_resize_fwd_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
-                     x, B, h, w, C, y, th, tw, ac_scale(h, 2 * h), ac_scale(w, 2 * w),
-                     ac_scale(2 * h, th), ac_scale(2 * w, tw));
+  dim3 g(grid_for(work));
+  const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
+              d = ac_scale(2 * w, tw);
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(up2_resize_fwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, x), B, h, w, C, NSM_T(bf16_t, y), th, tw, a, b, c, d);
+  else
+    hipLaunchKernelGGL(up2_resize_fwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, x), B, h, w, C, NSM_T(float, y), th, tw, a, b, c, d);
   NSM_LAUNCH_CHECK("up2_resize_fwd");
   return 0;
 }
 
-extern "C" int nsm_up2_resize_bwd(const float* dy, int B, int h, int w, int C, float* dx, int th,
-                                  int tw, void* stream) {
+extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th,
+                                  int tw, int dtype, void* stream) {
   NSM_CHECK_ARG(dy && dx && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 4 == 0,
                 "up2_resize_bwd: bad args");
   // the combined-weight gather assumes a downsizing second step of at most ~2x
   NSM_CHECK_ARG(th * 3 >= 2 * h && tw * 3 >= 2 * w, "up2_resize_bwd: target too small");
   long long work = (long long)B * h * w * (C / 4);
-  hipLaunchKernelGGL(up2_resize_bwd_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream),
-                     dy, B, h, w, C, dx, th, tw, ac_scale(h, 2 * h), ac_scale(w, 2 * w),
-                     ac_scale(2 * h, th), ac_scale(2 * w, tw));
+  dim3 g(grid_for(work));
+  const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
+              d = ac_scale(2 * w, tw);
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(up2_resize_bwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, dy), B, h, w, C, NSM_T(bf16_t, dx), th, tw, a, b, c, d);
+  else
+    hipLaunchKernelGGL(up2_resize_bwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, dy), B, h, w, C, NSM_T(float, dx), th, tw, a, b, c, d);
   NSM_LAUNCH_CHECK("up2_resize_bwd");
   return 0;
 }
 
-extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, float* out, int cp,
-                              void* stream) {
+extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, void* out, int cp,
+                              int dtype, void* stream) {
   NSM_CHECK_ARG(x && out && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C, "input_prep: bad args");
   long long work = (long long)B * (H / 2) * (W / 2) * cp;
-  hipLaunchKernelGGL(input_prep_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), x,
-                     B, C, H, W, out, cp);
+  dim3 g(grid_for(work));
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(input_prep_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
+                       NSM_T(bf16_t, out), cp);
+  else
+    hipLaunchKernelGGL(input_prep_kernel<float>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
+                       NSM_T(float, out), cp);
   NSM_LAUNCH_CHECK("input_prep");
   return 0;
 }
 
-extern "C" int nsm_input_grad(const float* dX, int B, int C, int H, int W, int cp, float* dx,
-                              void* stream) {
+extern "C" int nsm_input_grad(const void* dX, int B, int C, int H, int W, int cp, float* dx,
+                              int dtype, void* stream) {
   NSM_CHECK_ARG(dX && dx && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C && cp % 4 == 0,
                 "input_grad: bad args");
   long long work = (long long)B * C * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(input_grad_kernel, dim3(grid_for(work)), dim3(256), 0, as_stream(stream), dX,
-                     B, C, H, W, cp, dx);
+  dim3 g(grid_for(work));
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(input_grad_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, dX), B, C, H, W, cp, dx);
+  else
+    hipLaunchKernelGGL(input_grad_kernel<float>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, dX), B, C, H, W, cp, dx);
   NSM_LAUNCH_CHECK("input_grad");
   return 0;
 }
 
-extern "C" int nsm_head_fwd(const float* z, int ldz, int B, int Rh, int Rw, const float* w10,
-                            const float* b10, float* out, void* stream) {
+extern "C" int nsm_head_fwd(const void* z, int ldz, int B, int Rh, int Rw, const float* w10,
+                            const float* b10, float* out, int dtype, void* stream) {
   NSM_CHECK_ARG(z && w10 && b10 && out && ldz >= 16 && ldz % 4 == 0, "head_fwd: bad args");
   long long npix = (long long)B * Rh * Rw;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3(grid_for(npix)), dim3(256), 0, as_stream(stream), z, ldz,
-                     B, Rh, Rw, w10, b10, out);
+  dim3 g(grid_for(npix));
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, z), ldz, B, Rh, Rw, w10, b10, out);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, z), ldz, B, Rh, Rw, w10, b10, out);
   NSM_LAUNCH_CHECK("head_fwd");
   return 0;
 }
@@ -1102,15 +1188,19 @@ extern "C" int nsm_head_bwd_blocks(int B, int Rh, int Rw) {
   return grid_for((long long)B * Rh * Rw, 256, 1024);
 }
 
-extern "C" int nsm_head_bwd(const float* gout, const float* out, const float* z, int ldz, int B,
-                            int Rh, int Rw, const float* w10, float* dz, float* partial,
-                            float* dw10, float* db10, void* stream) {
+extern "C" int nsm_head_bwd(const float* gout, const float* out, const void* z, int ldz, int B,
+                            int Rh, int Rw, const float* w10, void* dz, float* partial, float* dw10,
+                            float* db10, int dtype, void* stream) {
   NSM_CHECK_ARG(gout && out && z && w10 && dz && partial && dw10 && db10 && ldz % 4 == 0,
                 "head_bwd: bad args");
   int nblk = nsm_head_bwd_blocks(B, Rh, Rw);
   hipStream_t s = as_stream(stream);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(nblk), dim3(256), 0, s, gout, out, z, ldz, B, Rh, Rw,
-                     w10, dz, partial);
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, gout, out,
+                       NSM_CT(bf16_t, z), ldz, B, Rh, Rw, w10, NSM_T(bf16_t, dz), partial);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, gout, out,
+                       NSM_CT(float, z), ldz, B, Rh, Rw, w10, NSM_T(float, dz), partial);
   NSM_LAUNCH_CHECK("head_bwd");
   hipLaunchKernelGGL(head_reduce_kernel, dim3(68), dim3(256), 0, s, partial, nblk, dw10, db10);
   NSM_LAUNCH_CHECK("head_reduce");

@@ -39,24 +39,24 @@ _SIGS = {
     "nsm_conv_wgrad": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
     "nsm_reduce_chunks": (I, [I, I]),
     "nsm_reduce_rows": (I, [I, I]),
-    "nsm_bn_stats": (I, [P, I, I, I, P, I, P]),
+    "nsm_bn_stats": (I, [P, I, I, I, P, I, I, P]),
     "nsm_bn_finalize_train": (I, [P, I, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P]),
     "nsm_bn_finalize_eval": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
-    "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, P]),
-    "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, P]),
+    "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, I, P]),
+    "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
     "nsm_bn_bwd_finalize": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
-    "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, P]),
-    "nsm_avgpool2_fwd": (I, [P, I, I, I, I, P, P]),
-    "nsm_avgpool2_bwd_add": (I, [P, I, I, I, I, P, P, P]),
-    "nsm_resize_fwd": (I, [P, I, I, I, I, P, I, I, P]),
-    "nsm_resize_bwd": (I, [P, I, I, I, I, P, I, I, P]),
-    "nsm_up2_resize_fwd": (I, [P, I, I, I, I, P, I, I, P]),
-    "nsm_up2_resize_bwd": (I, [P, I, I, I, I, P, I, I, P]),
-    "nsm_input_prep": (I, [P, I, I, I, I, P, I, P]),
-    "nsm_input_grad": (I, [P, I, I, I, I, I, P, P]),
-    "nsm_head_fwd": (I, [P, I, I, I, I, P, P, P, P]),
+    "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
+    "nsm_avgpool2_fwd": (I, [P, I, I, I, I, P, I, P]),
+    "nsm_avgpool2_bwd_add": (I, [P, I, I, I, I, P, P, I, P]),
+    "nsm_resize_fwd": (I, [P, I, I, I, I, P, I, I, I, P]),
+    "nsm_resize_bwd": (I, [P, I, I, I, I, P, I, I, I, P]),
+    "nsm_up2_resize_fwd": (I, [P, I, I, I, I, P, I, I, I, P]),
+    "nsm_up2_resize_bwd": (I, [P, I, I, I, I, P, I, I, I, P]),
+    "nsm_input_prep": (I, [P, I, I, I, I, P, I, I, P]),
+    "nsm_input_grad": (I, [P, I, I, I, I, I, P, I, P]),
+    "nsm_head_fwd": (I, [P, I, I, I, I, P, P, P, I, P]),
     "nsm_head_bwd_blocks": (I, [I, I, I]),
-    "nsm_head_bwd": (I, [P, P, P, I, I, I, I, P, P, P, P, P, P]),
+    "nsm_head_bwd": (I, [P, P, P, I, I, I, I, P, P, P, P, P, I, P]),
     "nsm_loss_blocks": (I, [L]),
     "nsm_l1_loss_fwd": (I, [P, P, L, F, P, P, P]),
     "nsm_l1_loss_bwd": (I, [P, P, L, F, P, P, I, P]),
@@ -66,6 +66,10 @@ _SIGS = {
     "nsm_clip_coef": (I, [P, F, F, P, P]),
     "nsm_adamw_step": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P]),
     "nsm_vgg_prep": (I, [P, P, I, I, I, F, F, P, P]),
+    "nsm_pack_conv_weight_bf16": (I, [P, I, I, I, I, I, I, P, P]),
+    "nsm_conv_fwd_bf16": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
+    "nsm_conv_wgrad_bf16_ws": (Z, [I, I, I, I, I, I]),
+    "nsm_conv_wgrad_bf16": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
     "nsm_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
 }
 

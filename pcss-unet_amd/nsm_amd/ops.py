@@ -9,7 +9,22 @@ import torch
 from ._lib import call, ptr, stream
 
 F32 = torch.float32
+BF16 = torch.bfloat16
 PACK_FWD, PACK_DGRAD = 0, 1
+NSM_F32, NSM_BF16 = 0, 1
+
+
+def dt(t):
+    """C-ABI dtype code of an activation tensor (include/nsm.h NSM_F32/NSM_BF16)."""
+    if t.dtype == BF16:
+        return NSM_BF16
+    if t.dtype != F32:
+        raise TypeError(f"activations must be float32 or bfloat16, got {t.dtype}")
+    return NSM_F32
+
+
+def like(M, C, ref):
+    return torch.empty(M, C, dtype=ref.dtype, device=ref.device)
 
 
 def pad32(c):
@@ -21,11 +36,13 @@ def empty(*shape, device):
 
 
 # ---- parameters ------------------------------------------------------------
-def pack_conv_weight(w, cout_p, cin_p, mode):
+def pack_conv_weight(w, cout_p, cin_p, mode, dtype=F32):
+    """MFMA operand layout of a conv weight, in the activations' dtype."""
     cout, cin, k, _ = w.shape
     taps = k * k
-    out = empty(cout_p * taps * cin_p, device=w.device)
-    call("nsm_pack_conv_weight", ptr(w), cout, cin, k, cout_p, cin_p, mode, ptr(out), stream())
+    out = torch.empty(cout_p * taps * cin_p, dtype=dtype, device=w.device)
+    fn = "nsm_pack_conv_weight_bf16" if dtype == BF16 else "nsm_pack_conv_weight"
+    call(fn, ptr(w), cout, cin, k, cout_p, cin_p, mode, ptr(out), stream())
     return out
 
 
@@ -95,7 +112,9 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
     also emits the BN batch-statistics partials of y."""
     from ._lib import lib
     M, cin_p = x.shape
-    y = out if out is not None else empty(M, cout_p, device=x.device)
+    y = out if out is not None else like(M, cout_p, x)
+    if wpk.dtype != x.dtype or y.dtype != x.dtype:
+        raise TypeError("conv_fwd: activations, packed weights and output must share a dtype")
     sc = sh = mk = None
     if pro is not None:
         sc, sh, mk = pro
@@ -105,7 +124,8 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
         nchunk = -(-M // rpc)
         part = Partials(empty(nchunk * 2 * cout_p, device=x.device), nchunk, rpc)
     ev = _probe(tag)
-    call("nsm_conv_fwd_stats", ptr(x), x.stride(0), B, H, W, cin_p, ptr(wpk), ptr(bias), cout_p,
+    fn = "nsm_conv_fwd_bf16" if x.dtype == BF16 else "nsm_conv_fwd_stats"
+    call(fn, ptr(x), x.stride(0), B, H, W, cin_p, ptr(wpk), ptr(bias), cout_p,
          ksize, ptr(y), y.stride(0), ptr(sc), ptr(sh), ptr(mk), slope,
          ptr(part.buf) if part is not None else None, stream())
     if ev is not None:
@@ -160,15 +180,21 @@ def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None):
 
 def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None):
     """dw (reference layout [cout, cin, k, k], contiguous) <- sum_p dy (x) x."""
+    from ._lib import lib
     cout_p, cin_p = dy.shape[1], x.shape[1]
-    n = int(call_ws(B, H, W, cin_p, cout_p, ksize))
+    bf = dy.dtype == BF16
+    if x.dtype != dy.dtype:
+        raise TypeError("conv_wgrad: dy and x must share a dtype")
+    n = int((lib.nsm_conv_wgrad_bf16_ws if bf else lib.nsm_conv_wgrad_ws)(B, H, W, cin_p, cout_p,
+                                                                           ksize))
     ws = empty(max(n, 1), device=dy.device)
     sc = sh = mk = None
     if pro is not None:
         sc, sh, mk = pro
     ev = _probe(tag)
-    call("nsm_conv_wgrad", ptr(dy), dy.stride(0), ptr(x), x.stride(0), B, H, W, cin_p, cout_p, ksize,
-         ptr(sc), ptr(sh), ptr(mk), 0.2, ptr(ws), n, cin, cout, ptr(dw), stream())
+    call("nsm_conv_wgrad_bf16" if bf else "nsm_conv_wgrad", ptr(dy), dy.stride(0), ptr(x),
+         x.stride(0), B, H, W, cin_p, cout_p, ksize, ptr(sc), ptr(sh), ptr(mk), 0.2, ptr(ws), n,
+         cin, cout, ptr(dw), stream())
     if ev is not None:
         ev.record()
 
@@ -204,7 +230,7 @@ def bn_partials(y):
     M, C = y.shape
     nchunk, rpc = reduce_chunks(M, C), lib.nsm_reduce_rows(M, C)
     part = Partials(empty(nchunk * 2 * C, device=y.device), nchunk, rpc)
-    call("nsm_bn_stats", ptr(y), y.stride(0), M, C, ptr(part.buf), nchunk, stream())
+    call("nsm_bn_stats", ptr(y), y.stride(0), M, C, ptr(part.buf), nchunk, dt(y), stream())
     return part
 
 
@@ -251,9 +277,10 @@ def bn_eval(bn_mod, C, c_real, eps, device):
 
 def bn_act(y, st, slope=0.2, res=None, out=None):
     M, C = y.shape
-    o = out if out is not None else empty(M, C, device=y.device)
+    o = out if out is not None else like(M, C, y)
+    assert res is None or res.dtype == y.dtype
     call("nsm_bn_act", ptr(y), y.stride(0), M, C, ptr(st.scale), ptr(st.shift), slope, ptr(res),
-         res.stride(0) if res is not None else 0, ptr(o), o.stride(0), stream())
+         res.stride(0) if res is not None else 0, ptr(o), o.stride(0), dt(y), stream())
     return o
 
 
@@ -263,79 +290,84 @@ def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2):
     M, C = y.shape
     nchunk = reduce_chunks(M, C)
     partial = empty(nchunk * 2 * C, device=y.device)
+    assert g.dtype == y.dtype
     call("nsm_bn_bwd_reduce", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
          ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(st.invstd), ptr(partial), nchunk,
-         stream())
+         dt(y), stream())
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
          ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
-    dy = empty(M, C, device=y.device)
+    dy = like(M, C, y)
     call("nsm_bn_bwd_apply", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
-         ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy), dy.stride(0), stream())
+         ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy), dy.stride(0), dt(y),
+         stream())
     return dy
 
 
 # ---- resampling --------------------------------------------------------------
 def avgpool2(x, B, H, W):
     C = x.shape[1]
-    y = empty(B * (H // 2) * (W // 2), C, device=x.device)
-    call("nsm_avgpool2_fwd", ptr(x), B, H, W, C, ptr(y), stream())
+    y = like(B * (H // 2) * (W // 2), C, x)
+    call("nsm_avgpool2_fwd", ptr(x), B, H, W, C, ptr(y), dt(x), stream())
     return y
 
 
 def avgpool2_bwd_add(dy, B, H, W, skip):
     C = dy.shape[1]
-    dx = empty(B * H * W, C, device=dy.device)
-    call("nsm_avgpool2_bwd_add", ptr(dy), B, H, W, C, ptr(skip), ptr(dx), stream())
+    dx = like(B * H * W, C, dy)
+    assert skip is None or skip.dtype == dy.dtype
+    call("nsm_avgpool2_bwd_add", ptr(dy), B, H, W, C, ptr(skip), ptr(dx), dt(dy), stream())
     return dx
 
 
 def resize(x, B, Hi, Wi, Ho, Wo):
     C = x.shape[-1]
-    y = empty(B * Ho * Wo, C, device=x.device)
-    call("nsm_resize_fwd", ptr(x), B, Hi, Wi, C, ptr(y), Ho, Wo, stream())
+    y = like(B * Ho * Wo, C, x)
+    call("nsm_resize_fwd", ptr(x), B, Hi, Wi, C, ptr(y), Ho, Wo, dt(x), stream())
     return y
 
 
 def resize_bwd(dy, B, Hi, Wi, Ho, Wo):
     C = dy.shape[-1]
-    dx = empty(B * Hi * Wi, C, device=dy.device)
-    call("nsm_resize_bwd", ptr(dy), B, Hi, Wi, C, ptr(dx), Ho, Wo, stream())
+    dx = like(B * Hi * Wi, C, dy)
+    call("nsm_resize_bwd", ptr(dy), B, Hi, Wi, C, ptr(dx), Ho, Wo, dt(dy), stream())
     return dx
 
 
 def up2_resize(x, B, h, w, th, tw):
     """bilinear x2 (align_corners) then resize to (th, tw), one pass."""
     C = x.shape[-1]
-    y = empty(B * th * tw, C, device=x.device)
-    call("nsm_up2_resize_fwd", ptr(x), B, h, w, C, ptr(y), th, tw, stream())
+    y = like(B * th * tw, C, x)
+    call("nsm_up2_resize_fwd", ptr(x), B, h, w, C, ptr(y), th, tw, dt(x), stream())
     return y
 
 
 def up2_resize_bwd(dy, B, h, w, th, tw):
     C = dy.shape[-1]
-    dx = empty(B * h * w, C, device=dy.device)
-    call("nsm_up2_resize_bwd", ptr(dy), B, h, w, C, ptr(dx), th, tw, stream())
+    dx = like(B * h * w, C, dy)
+    call("nsm_up2_resize_bwd", ptr(dy), B, h, w, C, ptr(dx), th, tw, dt(dy), stream())
     return dx
 
 
 # ---- boundary ----------------------------------------------------------------
-def input_prep(x, cp):
+def input_prep(x, cp, dtype=F32):
+    """fp32 NCHW model input -> NHWC [B*H/2*W/2, cp] activations in `dtype`."""
     B, C, H, W = x.shape
-    out = empty(B * (H // 2) * (W // 2), cp, device=x.device)
-    call("nsm_input_prep", ptr(x), B, C, H, W, ptr(out), cp, stream())
+    out = torch.empty(B * (H // 2) * (W // 2), cp, dtype=dtype, device=x.device)
+    call("nsm_input_prep", ptr(x), B, C, H, W, ptr(out), cp, dt(out), stream())
     return out
 
 
 def input_grad(dX, B, C, H, W):
     dx = empty(B, C, H, W, device=dX.device)
-    call("nsm_input_grad", ptr(dX), B, C, H, W, dX.shape[1], ptr(dx), stream())
+    call("nsm_input_grad", ptr(dX), B, C, H, W, dX.shape[1], ptr(dx), dt(dX), stream())
     return dx
 
 
 def head_fwd(z, B, Rh, Rw, w10, b10):
     out = empty(B, 1, 2 * Rh, 2 * Rw, device=z.device)
-    call("nsm_head_fwd", ptr(z), z.stride(0), B, Rh, Rw, ptr(w10), ptr(b10), ptr(out), stream())
+    call("nsm_head_fwd", ptr(z), z.stride(0), B, Rh, Rw, ptr(w10), ptr(b10), ptr(out), dt(z),
+         stream())
     return out
 
 
@@ -343,9 +375,9 @@ def head_bwd(gout, out, z, B, Rh, Rw, w10, dw10, db10):
     from ._lib import lib
     nblk = lib.nsm_head_bwd_blocks(B, Rh, Rw)
     partial = empty(nblk * 68, device=z.device)
-    dz = empty(*z.shape, device=z.device)
+    dz = torch.empty(*z.shape, dtype=z.dtype, device=z.device)
     call("nsm_head_bwd", ptr(gout), ptr(out), ptr(z), z.stride(0), B, Rh, Rw, ptr(w10), ptr(dz),
-         ptr(partial), ptr(dw10), ptr(db10), stream())
+         ptr(partial), ptr(dw10), ptr(db10), dt(z), stream())
     return dz
 
 

@@ -87,6 +87,25 @@ class Unet(nn.Module):
         self.emulate_checkpoint_bn = True
         # data parallel: (group,) when the backward launches its own grad all-reduces
         self._grad_allreduce = None
+        # activation storage / MFMA dtype: None = fp32, or bf16 inside a
+        # torch.autocast(dtype=torch.bfloat16) region; set_compute_dtype() pins it
+        self.compute_dtype = None
+
+    def set_compute_dtype(self, dtype):
+        """torch.float32 (exact fp32 MFMA, Winograd for the deep convs) or
+        torch.bfloat16 (BASELINE config 3: bf16 activations and MFMA products,
+        fp32 accumulation / BN statistics / parameters / gradients)."""
+        if dtype not in (None, torch.float32, torch.bfloat16):
+            raise ValueError(f"unsupported compute dtype {dtype}")
+        self.compute_dtype = dtype
+        return self
+
+    def activation_dtype(self):
+        if self.compute_dtype is not None:
+            return self.compute_dtype
+        if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+            return torch.bfloat16
+        return torch.float32
 
     def overlap_grad_allreduce(self, group=None, enable=True):
         """Data-parallel overlap: the backward starts the RCCL
@@ -152,13 +171,14 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     assert X.shape[1] == cip, (X.shape, cip)
     b1 = ops.pad_vec(c0.bias.detach(), cip)
     V = None
-    if cip >= WINOGRAD_MIN_CHANNELS:
+    dtype = X.dtype
+    if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         U1 = ops.wino_weight(c0.weight.detach(), cip, cip, flip=False, tile=WINO_TILE)
         Y1, V = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tile=WINO_TILE, tag=name + ".conv.0.fwd",
                                  keep_v=True)
         part1 = ops.bn_partials(Y1) if training else None
     else:
-        w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD)
+        w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD, dtype)
         Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd",
                                     stats=training)
     eps1, eps2 = bn1m.eps, bn2m.eps
@@ -166,7 +186,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
         bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1)
     else:
         bn1 = ops.bn_eval(bn1m, cip, ci, eps1, X.device)
-    w2 = ops.pack_conv_weight(c4.weight.detach(), cop, cip, ops.PACK_FWD)
+    w2 = ops.pack_conv_weight(c4.weight.detach(), cop, cip, ops.PACK_FWD, dtype)
     b2 = ops.pad_vec(c4.bias.detach(), cop)
     Y2, part2 = ops.conv_fwd_bn(Y1, B, H, W, w2, b2, cop, 1, pro=(bn1.scale, bn1.shift, mask),
                              tag=name + ".conv.4.fwd", stats=training)
@@ -189,7 +209,8 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
     HW = H * W
     g = grads
     dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias])
-    w2d = ops.pack_conv_weight(c4.weight.detach(), s.cop, s.cip, ops.PACK_DGRAD)
+    dtype = G.dtype
+    w2d = ops.pack_conv_weight(c4.weight.detach(), s.cop, s.cip, ops.PACK_DGRAD, dtype)
     dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
     ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
                    pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
@@ -202,11 +223,11 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
         ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
     if not need_dx:
         return None
-    if s.cip >= WINOGRAD_MIN_CHANNELS:
+    if s.cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         U1d = ops.wino_weight(c0.weight.detach(), s.cip, s.cip, flip=True, tile=WINO_TILE)
         return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=WINO_TILE,
                                 tag=name + ".conv.0.dgrad")
-    w1d = ops.pack_conv_weight(c0.weight.detach(), s.cip, s.cip, ops.PACK_DGRAD)
+    w1d = ops.pack_conv_weight(c0.weight.detach(), s.cip, s.cip, ops.PACK_DGRAD, dtype)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
 
 
@@ -227,7 +248,8 @@ class _UnetFn(torch.autograd.Function):
         cin_p = ops.pad32(4 * C)
         assert mod.conv2.conv[0].in_channels == 4 * C, (
             f"Unet expects {mod.conv2.conv[0].in_channels // 4} input channels, got {C}")
-        X = ops.input_prep(x32, cin_p)
+        cdt = mod.activation_dtype()
+        X = ops.input_prep(x32, cin_p, cdt)
         masks = _masks_for(mod, B, dev, training)
 
         saved, c, shapes = {}, {}, {}

@@ -1,0 +1,140 @@
+"""GPU: the bf16 path (BASELINE config 3) kernel by kernel. References are the
+fp32 PyTorch-CPU ops applied to the SAME bf16-rounded inputs and weights (the
+products of two bf16 numbers are exact in fp32, so the GEMM references differ
+from the kernels only by fp32 summation order and the final bf16 rounding of
+the output), then rounded to bf16 where the kernel stores bf16."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from test_gpu_ops import nchw, nhwc, rel
+
+pytestmark = pytest.mark.gpu
+BF = torch.bfloat16
+
+
+def r(x):  # round to bf16 and back
+    return x.to(BF).float()
+
+
+@pytest.fixture(scope="module")
+def ops(device):
+    from nsm_amd import ops as O
+    return O
+
+
+def bf_close(got, ref, ulps=2.0):
+    """|got - ref| <= ulps * 2^-8 * max|ref|, element-wise bound from bf16 output rounding."""
+    tol = ulps * 2.0 ** -8 * max(ref.abs().max().item(), 1e-30)
+    err = (got.float() - ref).abs().max().item()
+    assert err <= tol, (err, tol)
+
+
+@pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 9, 11, 32, 64, 3), (1, 16, 16, 64, 32, 3),
+                                           (2, 8, 8, 128, 128, 3), (3, 7, 5, 32, 128, 1),
+                                           (2, 32, 32, 64, 512, 1), (1, 5, 67, 96, 32, 3),
+                                           (4, 32, 32, 256, 256, 3)])
+def test_conv_fwd_bf16(ops, device, B, H, W, ci, co, k):
+    g = torch.Generator().manual_seed(B * 1000 + H * 10 + ci + co + k)
+    x = r(torch.randn(B, ci, H, W, generator=g))
+    w = r(torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5)
+    b = torch.randn(co, generator=g)
+    ref = F.conv2d(x, w, b, padding=k // 2)
+    wp = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_FWD, BF)
+    y, part = ops.conv_fwd_bn(nhwc(x).to(device, BF), B, H, W, wp, b.to(device), co, k)
+    assert y.dtype == BF
+    bf_close(nchw(y.cpu(), B, H, W), ref)
+    # fused BN partials are taken on the rounded outputs
+    yr = y.float().cpu()
+    rpc, n = part.rpc, part.nchunk
+    sums = part.buf.view(n, 2, co)[:, 0].cpu().double().sum(0)
+    torch.testing.assert_close(sums, yr.double().sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 6, 7, 32, 64), (2, 16, 16, 128, 64)])
+def test_conv1x1_prologue_bf16(ops, device, B, H, W, ci, co):
+    g = torch.Generator().manual_seed(7)
+    y1 = r(torch.randn(B, ci, H, W, generator=g))
+    sc, sh = torch.rand(ci, generator=g) + 0.5, torch.randn(ci, generator=g)
+    mask = (torch.rand(B, ci, generator=g) > 0.2).float() / 0.8
+    w = r(torch.randn(co, ci, 1, 1, generator=g) / ci ** 0.5)
+    a = r(F.leaky_relu(y1 * sc[None, :, None, None] + sh[None, :, None, None], 0.2)
+          * mask[:, :, None, None])      # the loader rounds the activated operand to bf16
+    ref = F.conv2d(a, w)
+    wp = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_FWD, BF)
+    y = ops.conv_fwd(nhwc(y1).to(device, BF), B, H, W, wp, None, co, 1,
+                     pro=(sc.to(device), sh.to(device), mask.to(device)))
+    bf_close(nchw(y.cpu(), B, H, W), ref, ulps=3.0)
+
+
+@pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 9, 11, 32, 64, 3), (2, 8, 8, 64, 64, 3),
+                                           (2, 12, 12, 64, 128, 1)])
+def test_conv_dgrad_bf16(ops, device, B, H, W, ci, co, k):
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, ci, H, W, generator=g, requires_grad=True)
+    w = r(torch.randn(co, ci, k, k, generator=g) / (ci * k * k) ** 0.5)
+    dy = r(torch.randn(B, co, H, W, generator=g))
+    F.conv2d(x, w, padding=k // 2).backward(dy)
+    wd = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_DGRAD, BF)
+    dx = ops.conv_fwd(nhwc(dy).to(device, BF), B, H, W, wd, None, ci, k)
+    bf_close(nchw(dx.cpu(), B, H, W), x.grad)
+
+
+@pytest.mark.parametrize("B,H,W,ci,co,k,pro", [(2, 9, 11, 32, 64, 3, False),
+                                               (2, 16, 16, 64, 32, 3, False),
+                                               (1, 33, 35, 128, 128, 3, False),
+                                               (2, 8, 8, 32, 64, 1, True),
+                                               (2, 16, 16, 128, 512, 1, True),
+                                               (4, 64, 64, 32, 32, 3, False)])
+def test_conv_wgrad_bf16(ops, device, B, H, W, ci, co, k, pro):
+    g = torch.Generator().manual_seed(13)
+    x = r(torch.randn(B, ci, H, W, generator=g))
+    sc, sh = torch.rand(ci, generator=g) + 0.5, torch.randn(ci, generator=g)
+    mask = (torch.rand(B, ci, generator=g) > 0.2).float() / 0.8
+    a = (r(F.leaky_relu(x * sc[None, :, None, None] + sh[None, :, None, None], 0.2)
+           * mask[:, :, None, None]) if pro else x)
+    w = torch.zeros(co, ci, k, k, requires_grad=True)
+    dy = r(torch.randn(B, co, H, W, generator=g))
+    F.conv2d(a, w, padding=k // 2).backward(dy)
+    dw = torch.empty(co, ci, k, k, device=device)
+    ops.conv_wgrad(nhwc(dy).to(device, BF), nhwc(x).to(device, BF), B, H, W, k, ci, co, dw,
+                   pro=(sc.to(device), sh.to(device), mask.to(device)) if pro else None)
+    assert rel(dw.cpu(), w.grad) <= 2e-5
+
+
+def test_elementwise_bf16(ops, device):
+    """bn_act (+skip), avgpool, resize fwd/bwd, up2_resize, bn_bwd on bf16
+    tensors = the fp32 kernels on the upcast tensors, rounded to bf16."""
+    g = torch.Generator().manual_seed(5)
+    B, H, W, C = 2, 10, 14, 64
+    y = r(torch.randn(B * H * W, C, generator=g)).to(device)
+    res = r(torch.randn(B * H * W, C, generator=g)).to(device)
+    st = ops.BNState(C, device)
+    st.scale.copy_(torch.rand(C, generator=g) + 0.5)
+    st.shift.copy_(torch.randn(C, generator=g))
+    st.mean.copy_(torch.randn(C, generator=g))
+    st.invstd.copy_(torch.rand(C, generator=g) + 0.5)
+    st.gamma = (torch.rand(C, generator=g) + 0.5).to(device)
+    yb, rb = y.to(BF), res.to(BF)
+
+    def ulp1(a, b):
+        # same fp32 arithmetic, but the compiler may contract the weighted sums
+        # differently per instantiation: allow one bf16 rounding step
+        a, b = a.float(), b.to(BF).float()
+        assert ((a - b).abs() <= 2.0 ** -7 * b.abs() + 1e-6 * b.abs().max()).all()
+
+    torch.testing.assert_close(ops.bn_act(yb, st, res=rb).float(),
+                               ops.bn_act(y, st, res=res).to(BF).float(), rtol=0, atol=0)
+    torch.testing.assert_close(ops.avgpool2(yb, B, H, W).float(),
+                               ops.avgpool2(y, B, H, W).to(BF).float(), rtol=0, atol=0)
+    ulp1(ops.resize(yb, B, H, W, 2 * H, 2 * W), ops.resize(y, B, H, W, 2 * H, 2 * W))
+    ulp1(ops.up2_resize(yb, B, H, W, 2 * H - 3, 2 * W - 1),
+         ops.up2_resize(y, B, H, W, 2 * H - 3, 2 * W - 1))
+    dy = r(torch.randn(B * 2 * H * 2 * W, C, generator=g)).to(device)
+    ulp1(ops.resize_bwd(dy.to(BF), B, H, W, 2 * H, 2 * W), ops.resize_bwd(dy, B, H, W, 2 * H, 2 * W))
+    mask = ((torch.rand(B, C, generator=g) > 0.2).float() / 0.8).to(device)
+    z = [torch.zeros(C, device=device) for _ in range(6)]
+    dyb = ops.bn_bwd(rb, yb, st, H * W, mask, C, z[0], z[1], z[2])
+    dyf = ops.bn_bwd(res, y, st, H * W, mask, C, z[3], z[4], z[5])
+    torch.testing.assert_close(dyb.float(), dyf.to(BF).float(), rtol=0, atol=0)
+    torch.testing.assert_close(z[0], z[3], rtol=0, atol=0)

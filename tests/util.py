@@ -12,6 +12,13 @@ LOSS_REL = 1e-5       # fp32 loss
 GRAD_REL_L2 = 2e-2    # per-tensor gradient rel-L2
 PRE_BN_BIAS_ABS = 1e-6  # conv biases feeding train-mode BN: grad is 0 analytically
 RUN_TOL = 1e-4        # running stats
+# bf16 path (config 3) vs the fp32 reference: SURVEY.md §4.3 bf16 output bound
+# (CPU bf16-autocast vs fp32 measured 1.2e-3 at 1080p); gradients / losses see
+# bf16 rounding of every activation and activation gradient
+OUT_ABS_BF16 = 5e-3
+LOSS_REL_BF16 = 2e-3
+GRAD_REL_L2_BF16 = 6e-2
+PRE_BN_BIAS_ABS_BF16 = 1e-4
 
 
 def load(name):
@@ -27,9 +34,11 @@ def is_pre_bn_bias(key):
     return key.endswith(".0.bias") or key.endswith(".4.bias")
 
 
-def check_grads(named_grads, fx, report=None):
+def check_grads(named_grads, fx, report=None, rel=None, bias_abs=None):
     """Compare a list of (key, grad ndarray) in named_parameters order with a
     fixture's grad summary. Returns list of failures."""
+    GRAD_REL_L2_ = GRAD_REL_L2 if rel is None else rel
+    PRE_BN_BIAS_ABS_ = PRE_BN_BIAS_ABS if bias_abs is None else bias_abs
     fails = []
     for idx, (k, g) in enumerate(named_grads):
         g = np.asarray(g, np.float64).ravel()
@@ -37,10 +46,10 @@ def check_grads(named_grads, fx, report=None):
             r = fx["g/" + k].astype(np.float64)
             if is_pre_bn_bias(k):
                 err = np.abs(g - r).max()
-                ok = err <= PRE_BN_BIAS_ABS
+                ok = err <= PRE_BN_BIAS_ABS_
             else:
                 err = np.linalg.norm(g - r) / max(np.linalg.norm(r), 1e-30)
-                ok = err <= GRAD_REL_L2
+                ok = err <= GRAD_REL_L2_
         else:
             l2r = float(fx[f"g/{k}/l2"])
             l2 = np.sqrt((g * g).sum())
@@ -50,7 +59,7 @@ def check_grads(named_grads, fx, report=None):
             head = fx[f"g/{k}/head"].astype(np.float64)
             e3 = np.linalg.norm(g[:64] - head) / max(np.linalg.norm(head), 1e-30)
             err = max(e1, e2)
-            ok = e1 <= GRAD_REL_L2 and e2 <= 2 * GRAD_REL_L2 and e3 <= 5 * GRAD_REL_L2
+            ok = e1 <= GRAD_REL_L2_ and e2 <= 2 * GRAD_REL_L2_ and e3 <= 5 * GRAD_REL_L2_
         if report is not None:
             report.append((k, float(err)))
         if not ok:
