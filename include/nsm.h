@@ -135,6 +135,11 @@ int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_per_chunk, 
                           const float* gamma, const float* beta, float* run_mean, float* run_var,
                           int64_t* num_batches, float momentum, float eps, int n_updates,
                           float* mean, float* invstd, float* scale, float* shift, void* stream);
+/* merge groups of `group` consecutive partial chunks ({sum, M2} rows of
+ * rows_per_chunk rows) into ceil(nchunk/group) rows of rows_per_chunk*group
+ * rows (Chan, fixed order): keeps nsm_bn_finalize_train short on huge grids */
+int nsm_bn_partials_merge(const float* partial, int nchunk, int rows_per_chunk, int M, int C,
+                          int group, float* out, void* stream);
 int nsm_bn_finalize_eval(const float* run_mean, const float* run_var, const float* gamma,
                          const float* beta, int C, int c_real, float eps, float* mean,
                          float* invstd, float* scale, float* shift, void* stream);
@@ -228,6 +233,8 @@ int nsm_conv_fwd_bf16(const void* x, int ldx, int B, int H, int W, int cin_p, co
                       const float* bias, int cout_p, int ksize, void* y, int ldy,
                       const float* pro_scale, const float* pro_shift, const float* pro_mask,
                       float slope, float* stats, void* stream);
+/* rows per BN-partial chunk of nsm_conv_fwd_bf16 (its M tile) */
+int nsm_conv_stat_rows_bf16(int B, int H, int W, int cout_p);
 size_t nsm_conv_wgrad_bf16_ws(int B, int H, int W, int cin_p, int cout_p, int ksize);
 int nsm_conv_wgrad_bf16(const void* dy, int lddy, const void* x, int ldx, int B, int H, int W,
                         int cin_p, int cout_p, int ksize, const float* pro_scale,

@@ -298,6 +298,7 @@ struct EpiCtx {
   int mb, nb;  // this wave's tile origin
   int wm, wn, lane;
   float* lds;  // the GEMM's LDS array (free after the main loop)
+  int mblk;    // M-block index (BN-partial row)
 };
 
 struct EpiStoreP {
@@ -396,7 +397,7 @@ struct EpiStore {
       for (int tn = 0; tn < TN; ++tn) red[cx.wm * BN + cx.wn * TN * 32 + tn * 32 + col] = s[tn];
     __syncthreads();
     if (cx.wm == 0 && h == 0) {
-      float* pr = e.stats + (size_t)blockIdx.x * 2 * N;
+      float* pr = e.stats + (size_t)cx.mblk * 2 * N;
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         int n = cx.nb + tn * 32 + col;
@@ -548,7 +549,7 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
     __builtin_amdgcn_sched_group_barrier(0x200, 16, 0);
     __syncthreads();
   }
-  EpiCtx cx{m0, n0, m0 + arb, n0 + brb, wm, wn, lane, lds};
+  EpiCtx cx{m0, n0, m0 + arb, n0 + brb, wm, wn, lane, lds, (int)blockIdx.x};
   EP::template apply<TM, TN, WM, WN>(ep, acc, cx, M, N, split);
 }
 
@@ -1002,6 +1003,24 @@ __global__ void __launch_bounds__(256) wino_dout_kernel(const float* __restrict_
   }
 }
 
+// dst[b][i] = sum_s src[b][s][i] (float4 lanes, fixed order): the split-K
+// partials of a batched GEMM, one batch entry per grid.y
+__global__ void __launch_bounds__(256) batched_splitsum_kernel(const float* __restrict__ src,
+                                                               int splits, long long L4,
+                                                               float* __restrict__ dst) {
+  long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= L4) return;
+  const f32x4* p = (const f32x4*)src + (size_t)blockIdx.y * splits * L4 + i;
+  f32x4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 1 < splits; k += 2) {
+    a += p[(size_t)k * L4];
+    b += p[(size_t)(k + 1) * L4];
+  }
+  if (k < splits) a += p[(size_t)k * L4];
+  ((f32x4*)dst)[(size_t)blockIdx.y * L4 + i] = a + b;
+}
+
 // dw[co][ci][3][3] = G^T (sum_s dU[xi][s][co][ci]) G, one thread per (co, ci)
 template <int MT>
 __global__ void __launch_bounds__(256) wino_wgrad_out_kernel(const float* __restrict__ slab,
@@ -1313,6 +1332,7 @@ static WinoWgradPlan plan_wino_wgrad(long long T, int cin_p, int cout_p, int nb)
   p.splits = (int)sp;
   p.kchunk = (int)kc;
   p.slab_floats = (size_t)nb * sp * cout_p * cin_p;
+  if (sp > 1) p.slab_floats += (size_t)nb * cout_p * cin_p;  // split-summed dU
   p.dm_floats = (size_t)nb * T * cout_p;
   return p;
 }
@@ -1395,12 +1415,25 @@ extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V,
   rc = launch_wino_wgrad<32, 32, 1, 1>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, nb, s);
 #undef NSM_WW
   if (rc) return rc;
+  // split-K partials -> one dU per xi with a parallel, fixed-order sum (the
+  // transform kernel below then reads alpha^2 values per output weight)
+  const float* du = slab;
+  int du_splits = pl.splits;
+  if (pl.splits > 1) {
+    float* sum = slab + (size_t)nb * pl.splits * M * N;
+    const long long L4 = (long long)M * N / 4;
+    hipLaunchKernelGGL(batched_splitsum_kernel, dim3(ceil_div(L4, 256), nb), dim3(256), 0, s, slab,
+                       pl.splits, L4, sum);
+    NSM_LAUNCH_CHECK("wino_wgrad splitsum");
+    du = sum;
+    du_splits = 1;
+  }
   dim3 g2(ceil_div(cout * cin, 256));
   if (tile == 2)
-    hipLaunchKernelGGL(wino_wgrad_out_kernel<2>, g2, dim3(256), 0, s, slab, pl.splits, M, N, cin,
+    hipLaunchKernelGGL(wino_wgrad_out_kernel<2>, g2, dim3(256), 0, s, du, du_splits, M, N, cin,
                        cout, dw);
   else
-    hipLaunchKernelGGL(wino_wgrad_out_kernel<4>, g2, dim3(256), 0, s, slab, pl.splits, M, N, cin,
+    hipLaunchKernelGGL(wino_wgrad_out_kernel<4>, g2, dim3(256), 0, s, du, du_splits, M, N, cin,
                        cout, dw);
   NSM_LAUNCH_CHECK("wino_wgrad_out");
   return 0;

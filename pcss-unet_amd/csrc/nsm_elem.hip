@@ -147,6 +147,33 @@ __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
   }
 }
 
+// First level of the BN-partial merge for grids with many row chunks:
+// out[g] = Chan merge of chunks [g*G, (g+1)*G) (fixed order, double), one
+// thread per (group, channel), coalesced along channels.
+__global__ void bn_partials_merge_kernel(const float* __restrict__ partial, int nchunk, int rpc,
+                                         int M, int C, int G, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  const int g = blockIdx.y;
+  if (c >= C) return;
+  const int k0 = g * G, k1 = min(nchunk, k0 + G);
+  double s = 0.0;
+  long long n = 0;
+  for (int k = k0; k < k1; ++k) {
+    s += partial[(size_t)k * 2 * C + c];
+    n += max(0, min(M, (k + 1) * rpc) - k * rpc);
+  }
+  const double mean = n > 0 ? s / (double)n : 0.0;
+  double m2 = 0.0;
+  for (int k = k0; k < k1; ++k) {
+    const int nk = min(M, (k + 1) * rpc) - k * rpc;
+    if (nk <= 0) continue;
+    const double d = partial[(size_t)k * 2 * C + c] / nk - mean;
+    m2 += partial[(size_t)k * 2 * C + C + c] + nk * d * d;
+  }
+  out[(size_t)g * 2 * C + c] = (float)s;
+  out[(size_t)g * 2 * C + C + c] = (float)m2;
+}
+
 __global__ void bn_finalize_eval_kernel(const float* __restrict__ rm, const float* __restrict__ rv,
                                         const float* __restrict__ gamma,
                                         const float* __restrict__ beta, int C, int c_real, float eps,
@@ -939,6 +966,17 @@ extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_
                      run_mean,
                      run_var, num_batches, momentum, eps, n_updates, mean, invstd, scale, shift);
   NSM_LAUNCH_CHECK("bn_finalize_train");
+  return 0;
+}
+
+extern "C" int nsm_bn_partials_merge(const float* partial, int nchunk, int rows_per_chunk, int M,
+                                     int C, int group, float* out, void* stream) {
+  NSM_CHECK_ARG(partial && out && nchunk >= 1 && group >= 1 && rows_per_chunk >= 1,
+                "bn_partials_merge: bad args");
+  dim3 grid(ceil_div(C, 256), ceil_div(nchunk, group));
+  hipLaunchKernelGGL(bn_partials_merge_kernel, grid, dim3(256), 0, as_stream(stream), partial,
+                     nchunk, rows_per_chunk, M, C, group, out);
+  NSM_LAUNCH_CHECK("bn_partials_merge");
   return 0;
 }
 

@@ -41,6 +41,7 @@ _SIGS = {
     "nsm_reduce_rows": (I, [I, I]),
     "nsm_bn_stats": (I, [P, I, I, I, P, I, I, P]),
     "nsm_bn_finalize_train": (I, [P, I, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P]),
+    "nsm_bn_partials_merge": (I, [P, I, I, I, I, I, P, P]),
     "nsm_bn_finalize_eval": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
     "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, I, P]),
     "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
@@ -69,6 +70,7 @@ _SIGS = {
     "nsm_pack_conv_weight_bf16": (I, [P, I, I, I, I, I, I, P, P]),
     "nsm_conv_fwd_bf16": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
     "nsm_conv_wgrad_bf16_ws": (Z, [I, I, I, I, I, I]),
+    "nsm_conv_stat_rows_bf16": (I, [I, I, I, I]),
     "nsm_conv_wgrad_bf16": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
     "nsm_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
 }

@@ -73,10 +73,11 @@ def _probe(tag):
 
 class Partials:
     """Per-channel BN partials {sum, M2} over row chunks: [nchunk][2][C]."""
-    __slots__ = ("buf", "nchunk", "rpc")
+    __slots__ = ("buf", "nchunk", "rpc", "_merged")
 
     def __init__(self, buf, nchunk, rpc):
         self.buf, self.nchunk, self.rpc = buf, nchunk, rpc
+        self._merged = None
 
 
 class stage:
@@ -120,7 +121,8 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
         sc, sh, mk = pro
     part = None
     if stats:
-        rpc = lib.nsm_conv_stat_rows(B, H, W, cout_p)
+        rows_fn = lib.nsm_conv_stat_rows_bf16 if x.dtype == BF16 else lib.nsm_conv_stat_rows
+        rpc = rows_fn(B, H, W, cout_p)
         nchunk = -(-M // rpc)
         part = Partials(empty(nchunk * 2 * cout_p, device=x.device), nchunk, rpc)
     ev = _probe(tag)
@@ -234,7 +236,25 @@ def bn_partials(y):
     return part
 
 
+MERGE_ABOVE = 256   # partial chunks beyond which a parallel first-level merge runs
+
+
+def merged(part, M, C):
+    """Partials with at most MERGE_ABOVE chunks (cached on the Partials)."""
+    if part.nchunk <= MERGE_ABOVE:
+        return part
+    if part._merged is None:
+        G = -(-part.nchunk // MERGE_ABOVE)
+        n2 = -(-part.nchunk // G)
+        buf = empty(n2 * 2 * C, device=part.buf.device)
+        call("nsm_bn_partials_merge", ptr(part.buf), part.nchunk, part.rpc, M, C, G, ptr(buf),
+             stream())
+        part._merged = Partials(buf, n2, part.rpc * G)
+    return part._merged
+
+
 def _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, gamma):
+    part = merged(part, M, C)
     beta = pad_vec(bn_mod.bias.detach(), C)
     track = bn_mod.track_running_stats
     call("nsm_bn_finalize_train", ptr(part.buf), part.nchunk, part.rpc, M, C, c_real, ptr(gamma),
