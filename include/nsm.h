@@ -204,6 +204,10 @@ int nsm_head_bwd(const float* gout, const float* out, const void* z, int ldz, in
 int nsm_loss_blocks(int64_t n);
 int nsm_l1_loss_fwd(const float* o, const float* t, int64_t n, float alpha, float* partial,
                     float* out, void* stream);
+/* mean(exp(alpha*|a-b|) - 1): one frame pair of measure_temporal_instability
+ * (pert_loss.py:170-199) */
+int nsm_expdiff_mean(const float* a, const float* b, int64_t n, float alpha, float* partial,
+                     float* out, void* stream);
 int nsm_l1_loss_bwd(const float* o, const float* t, int64_t n, float alpha, const float* gscale,
                     float* grad, int accumulate, void* stream);
 /* PerturbationLoss.perturb_input (pert_loss.py:26-59):
@@ -249,6 +253,28 @@ int nsm_conv_wgrad_bf16(const void* dy, int lddy, const void* x, int ldx, int B,
 int nsm_vgg_prep(const float* output, const float* target, int B, int H, int W, float mean,
                  float denom, float* out, void* stream);
 int nsm_maxpool2_fwd(const float* x, int B, int H, int W, int C, float* y, void* stream);
+
+/* ---- frame loader (setdata.MmapLiverDataset's files) -----
+ * nsm_npy_info: shape / dtype (0 f32, 1 f64) / data offset of an .npy file.
+ * nsm_loader_create: mmap {split}_inputs.npy (f32 [N,C,H,W]) and
+ *   {split}_labels.npy (f64|f32 [N,1,H,W]); this rank's contiguous shard
+ *   [rank*N/world, (rank+1)*N/world) in order (DataLoader shuffle=False,
+ *   main.py:850), batches of `batch` (last one short), cycling epochs; nthreads
+ *   host threads stage upcoming batches into nslots pinned slots.
+ * nsm_loader_next: async H2D of the next batch on `stream` into dev_x / dev_y
+ *   (raw f32; labels converted on the host); returns the frame count or -1.
+ * nsm_normalize_frames: x = (x - mean[c]) / (std[c] + eps) on the GPU
+ *   (setdata.py:316). */
+int nsm_npy_info(const char* path, int64_t* shape, int max_dims, int* ndim, int* dtype,
+                 int64_t* data_offset);
+void* nsm_loader_create(const char* inputs_path, const char* labels_path, int batch, int rank,
+                        int world, int nslots, int nthreads);
+int64_t nsm_loader_batches(void* loader);
+int nsm_loader_frame_dims(void* loader, int* C, int* H, int* W);
+int nsm_loader_next(void* loader, void* dev_x, void* dev_y, void* stream);
+void nsm_loader_destroy(void* loader);
+int nsm_normalize_frames(float* x, int B, int C, int64_t HW, const float* mean, const float* stdv,
+                         float eps, void* stream);
 
 #ifdef __cplusplus
 }

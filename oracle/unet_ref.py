@@ -165,3 +165,14 @@ def param_keys(in_ch=4):
 __all__ = ["forward", "conv5_recompute_bn_update", "l1_loss", "custom_loss",
            "perturbation_loss", "perturb_inputs", "torch_state", "param_keys",
            "block_channels", "block_dropout"]
+
+
+def temporal_instability(frames, alpha=5.0):
+    """pert_loss.py:166-199 (measure_temporal_instability, no motion vectors):
+    mean over consecutive pairs of mean(exp(alpha*|f_t - f_{t-1}|) - 1)."""
+    if len(frames) < 2:
+        return torch.tensor(0.0)
+    total = 0
+    for t in range(1, len(frames)):
+        total = total + torch.mean(torch.exp(alpha * torch.abs(frames[t] - frames[t - 1])) - 1)
+    return total / (len(frames) - 1)

@@ -796,6 +796,20 @@ __global__ void __launch_bounds__(256) l1_partial_kernel(const float* __restrict
   if (threadIdx.x == 0) partial[blockIdx.x] = r;
 }
 
+// sum of exp(alpha*|a-b|) - 1 (measure_temporal_instability, pert_loss.py:170-199)
+__global__ void __launch_bounds__(256) expdiff_partial_kernel(const float* __restrict__ a,
+                                                              const float* __restrict__ b,
+                                                              int64_t n, float alpha,
+                                                              float* __restrict__ partial) {
+  __shared__ float sh[4];
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    s += expf(alpha * fabsf(a[i] - b[i])) - 1.f;
+  float r = block_sum256(s, sh);
+  if (threadIdx.x == 0) partial[blockIdx.x] = r;
+}
+
 __global__ void finalize_mean_kernel(const float* __restrict__ partial, int nblk, double scale,
                                      float* out) {
   // one wave; fixed-order double accumulation
@@ -855,6 +869,18 @@ __global__ void __launch_bounds__(1024) channel_std_kernel(const float* __restri
     double t2 = 0.0;
     for (int k = 0; k < (int)(blockDim.x >> 6); ++k) t2 += sh[k];
     std_o[c] = (float)sqrt(t2 / (double)(n > 1 ? n - 1 : 1));
+  }
+}
+
+// setdata.py:316: x = (x - mean[c]) / (std[c] + eps), in place on [B][C][HW]
+__global__ void normalize_frames_kernel(float* __restrict__ x, int C, long long HW, long long total,
+                                        const float* __restrict__ mean,
+                                        const float* __restrict__ stdv, float eps) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)((i / HW) % C);
+    const float d = stdv[c] + eps;
+    x[i] = (x[i] - mean[c]) / d;
   }
 }
 
@@ -1259,6 +1285,18 @@ extern "C" int nsm_l1_loss_fwd(const float* o, const float* t, int64_t n, float 
   return 0;
 }
 
+extern "C" int nsm_expdiff_mean(const float* a, const float* b, int64_t n, float alpha,
+                                float* partial, float* out, void* stream) {
+  NSM_CHECK_ARG(a && b && partial && out && n > 0, "expdiff_mean: bad args");
+  int nb = nsm_loss_blocks(n);
+  hipStream_t s = as_stream(stream);
+  hipLaunchKernelGGL(expdiff_partial_kernel, dim3(nb), dim3(256), 0, s, a, b, n, alpha, partial);
+  hipLaunchKernelGGL(finalize_mean_kernel, dim3(1), dim3(64), 0, s, partial, nb, 1.0 / (double)n,
+                     out);
+  NSM_LAUNCH_CHECK("expdiff_mean");
+  return 0;
+}
+
 extern "C" int nsm_l1_loss_bwd(const float* o, const float* t, int64_t n, float alpha,
                                const float* gscale, float* grad, int accumulate, void* stream) {
   NSM_CHECK_ARG(o && t && grad && n > 0, "l1_loss_bwd: bad args");
@@ -1285,6 +1323,16 @@ extern "C" int nsm_perturb(const float* x, const float* noise, const float* stdv
   hipLaunchKernelGGL(perturb_kernel, dim3(grid_for(total)), dim3(256), 0, as_stream(stream), x,
                      noise, stdv, C, H * W, total, factor, out);
   NSM_LAUNCH_CHECK("perturb");
+  return 0;
+}
+
+extern "C" int nsm_normalize_frames(float* x, int B, int C, int64_t HW, const float* mean,
+                                    const float* stdv, float eps, void* stream) {
+  NSM_CHECK_ARG(x && mean && stdv && B > 0 && C > 0 && HW > 0, "normalize_frames: bad args");
+  long long total = (long long)B * C * HW;
+  hipLaunchKernelGGL(normalize_frames_kernel, dim3(grid_for(total)), dim3(256), 0,
+                     as_stream(stream), x, C, (long long)HW, total, mean, stdv, eps);
+  NSM_LAUNCH_CHECK("normalize_frames");
   return 0;
 }
 

@@ -6,7 +6,8 @@ Importing this package loads libnsm.so and fails loudly if it is missing.
 """
 from ._lib import LIB_PATH, NsmError, lib  # noqa: F401  (loads the HIP library)
 from .unet import DoubleConv, Unet  # noqa: F401
-from .losses import CustomLoss, L1Loss, PerturbationLoss, l1_loss  # noqa: F401
+from .losses import (CustomLoss, EnhancedCustomLoss, L1Loss, PerturbationLoss,  # noqa: F401
+                     l1_loss, measure_temporal_instability)
 from .optim import FlatAdamW, allreduce_grads, flat_grad  # noqa: F401
 from .infer import GraphedUnet  # noqa: F401
 from .vgg import MultiLayerVGGLoss  # noqa: F401

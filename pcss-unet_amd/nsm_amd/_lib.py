@@ -60,6 +60,7 @@ _SIGS = {
     "nsm_head_bwd": (I, [P, P, P, I, I, I, I, P, P, P, P, P, I, P]),
     "nsm_loss_blocks": (I, [L]),
     "nsm_l1_loss_fwd": (I, [P, P, L, F, P, P, P]),
+    "nsm_expdiff_mean": (I, [P, P, L, F, P, P, P]),
     "nsm_l1_loss_bwd": (I, [P, P, L, F, P, P, I, P]),
     "nsm_channel_std": (I, [P, I, I, I, I, P, P, P]),
     "nsm_perturb": (I, [P, P, P, I, I, I, I, F, P, P]),
@@ -67,6 +68,13 @@ _SIGS = {
     "nsm_clip_coef": (I, [P, F, F, P, P]),
     "nsm_adamw_step": (I, [P, P, P, P, L, F, F, F, F, F, I, P, P]),
     "nsm_vgg_prep": (I, [P, P, I, I, I, F, F, P, P]),
+    "nsm_npy_info": (I, [ctypes.c_char_p, P, I, P, P, P]),
+    "nsm_loader_create": (P, [ctypes.c_char_p, ctypes.c_char_p, I, I, I, I, I]),
+    "nsm_loader_batches": (L, [P]),
+    "nsm_loader_frame_dims": (I, [P, P, P, P]),
+    "nsm_loader_next": (I, [P, P, P, P]),
+    "nsm_loader_destroy": (None, [P]),
+    "nsm_normalize_frames": (I, [P, I, I, L, P, P, F, P]),
     "nsm_pack_conv_weight_bf16": (I, [P, I, I, I, I, I, I, P, P]),
     "nsm_conv_fwd_bf16": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
     "nsm_conv_wgrad_bf16_ws": (Z, [I, I, I, I, I, I]),

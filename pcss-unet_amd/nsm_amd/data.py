@@ -12,6 +12,10 @@ data-parallel sharding of it.
 * `shard_range` / `ShardedFrames`: plain data parallelism — rank r owns the
   contiguous frame slice [r*N/W, (r+1)*N/W) (the reference iterates in order,
   shuffle=False, main.py:850) and serves batches already resident on its GPU.
+* `FrameLoader`: the same frames through the native loader (libnsm
+  nsm_loader_*: mmap + host threads staging upcoming batches in pinned
+  memory + async H2D on the compute stream), normalised on the GPU
+  (nsm_normalize_frames) — the production input path.
 """
 import json
 import os
@@ -22,14 +26,14 @@ import torch
 
 def load_stats(stats_dir, channels=None):
     js = os.path.join(stats_dir, "train_stats.json")
-    npy = os.path.join(stats_dir, "train_stats.npy")
     st = None
     if os.path.exists(js):
         with open(js) as f:
             st = json.load(f)
-    elif os.path.exists(npy):
-        # the reference's own stats file is a pickled dict (calculate_dataset_stats.py:88-92)
-        st = np.load(npy, allow_pickle=True).item()
+    elif os.path.exists(os.path.join(stats_dir, "train_stats.npy")):
+        raise FileNotFoundError(
+            f"{js} not found: only the pickled train_stats.npy is present, and pickles are not "
+            "loaded; calculate_dataset_stats.py writes train_stats.json with the same content")
     if not st or "means" not in st or "stds" not in st:
         return None
     if channels is not None and len(st["means"]) != channels:
@@ -110,3 +114,65 @@ class ShardedFrames:
                 x = x.pin_memory().to(self.device, non_blocking=True)
                 y = y.pin_memory().to(self.device, non_blocking=True)
             yield x.requires_grad_(True), y
+
+
+class FrameLoader:
+    """Batches (x [b,C,H,W] normalised f32 requiring grad, y [b,1,H,W] f32) of
+    this rank's shard, resident on `device`, in the reference's order; loops
+    over epochs. len() = batches per epoch."""
+
+    def __init__(self, data_dir, split="train", batch=8, device="cuda", world=1, rank=0,
+                 stats_dir=None, apply_normalization=True, slots=3, threads=4):
+        from ._lib import NsmError, call, last_error, lib
+        self._lib, self._call = lib, call
+        self.device = torch.device(device)
+        xin = os.path.join(data_dir, f"{split}_inputs.npy")
+        yin = os.path.join(data_dir, f"{split}_labels.npy")
+        h = lib.nsm_loader_create(xin.encode(), yin.encode(), batch, rank, world, slots, threads)
+        if not h:
+            raise NsmError(f"nsm_loader_create failed: {last_error()}")
+        self._h = h
+        import ctypes
+        c, hh, ww = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        call("nsm_loader_frame_dims", h, ctypes.byref(c), ctypes.byref(hh), ctypes.byref(ww))
+        self.C, self.H, self.W = c.value, hh.value, ww.value
+        self.batch = batch
+        self.nbatches = int(lib.nsm_loader_batches(h))
+        self.norm = None
+        if apply_normalization:
+            st = load_stats(stats_dir or data_dir, self.C)
+            if st is not None:
+                self.norm = (st[0].to(self.device), st[1].to(self.device))
+
+    def __len__(self):
+        return self.nbatches
+
+    def next(self):
+        from ._lib import NsmError, last_error, ptr, stream
+        x = torch.empty(self.batch, self.C, self.H, self.W, dtype=torch.float32, device=self.device)
+        y = torch.empty(self.batch, 1, self.H, self.W, dtype=torch.float32, device=self.device)
+        n = self._lib.nsm_loader_next(self._h, ptr(x), ptr(y), stream())
+        if n < 0:
+            raise NsmError(f"nsm_loader_next failed: {last_error()}")
+        x, y = x[:n], y[:n]
+        if self.norm is not None:
+            self._call("nsm_normalize_frames", ptr(x), n, self.C, self.H * self.W, ptr(self.norm[0]),
+                       ptr(self.norm[1]), MmapLiverDataset.EPS, stream())
+        return x.requires_grad_(True), y
+
+    def __iter__(self):
+        for _ in range(self.nbatches):
+            yield self.next()
+
+    def close(self):
+        if getattr(self, "_h", None):
+            # the staged copies ran on the current stream: let them land first
+            torch.cuda.current_stream(self.device).synchronize()
+            self._lib.nsm_loader_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -13,6 +13,17 @@
 * `PerturbationLoss(perturbation_count=3)`: pert_loss.py:7-90 — three
   no-grad forwards of the model on inputs perturbed by per-channel
   std * 0.01 Gaussian noise, mean L1 to the original output.
+* `EnhancedCustomLoss(device, alpha=0.9, perturb_weight=0.5)`: the wired
+  perturbation-training loss of pert_loss.py:92-163 (§8f next-row #4). The
+  reference's class cannot be constructed (it imports a `VGGLoss` that
+  customLoss.py does not define); this one uses the `MultiLayerVGGLoss`
+  CustomLoss uses and otherwise follows the reference: returns
+  (total, {'l1_loss', 'vgg_loss', 'perturbation_loss', 'total_loss'}),
+  total = alpha*L1 + (1-alpha)*vgg [+ perturb_weight*perturbation while
+  training].
+* `measure_temporal_instability(frames, motion_vectors=None, alpha=5.0)`:
+  pert_loss.py:166-199, mean over consecutive frame pairs of
+  mean(exp(alpha*|f_t - f_{t-1}|) - 1) (`nsm_expdiff_mean`).
 """
 import torch
 import torch.nn as nn
@@ -124,3 +135,52 @@ class PerturbationLoss(nn.Module):
         for po in pouts:
             total = total + l1_loss(original_output, po)
         return total / len(pouts)
+
+
+class EnhancedCustomLoss(nn.Module):
+    def __init__(self, device=None, alpha=0.9, perturb_weight=0.5, vgg=None, vgg_weights=None):
+        super().__init__()
+        self.alpha = alpha
+        self.perturb_weight = perturb_weight
+        self.l1 = L1Loss()
+        self.base = CustomLoss(device, alpha, vgg=vgg, vgg_weights=vgg_weights)
+        self.vgg_loss = getattr(self.base, "vgg_loss", None) or vgg
+        self.perturbation_loss = PerturbationLoss()
+
+    def forward(self, model, output, target, inputs, noises=None):
+        l1 = l1_loss(output, target)
+        if self.vgg_loss is not None:
+            vgg = torch.as_tensor(self.vgg_loss(output, target), device=l1.device).detach()
+        else:
+            vgg = torch.zeros((), device=l1.device)
+        # d(alpha*l1)/do reaches the L1 backward as gscale = alpha: alpha*sign/N
+        basic = self.alpha * l1 + (1 - self.alpha) * vgg
+        losses = {"l1_loss": l1, "vgg_loss": vgg}
+        if self.training and self.perturb_weight > 0:
+            pert = self.perturbation_loss(model, inputs, output, noises=noises)
+            total = basic + self.perturb_weight * pert
+            losses["perturbation_loss"] = pert
+        else:
+            total = basic
+            losses["perturbation_loss"] = torch.zeros((), device=l1.device)
+        losses["total_loss"] = total
+        return total, losses
+
+
+def measure_temporal_instability(frames, motion_vectors=None, alpha=5.0):
+    """frames: sequence of same-shape tensors on the GPU (e.g. [B,1,H,W] outputs)."""
+    if len(frames) < 2:
+        return torch.tensor(0.0)
+    # motion_vectors: the reference accepts them but does not use them (pert_loss.py:184-187)
+    dev = frames[0].device
+    require_gpu(frames[0], "temporal-instability frames")
+    n = frames[0].numel()
+    partial = torch.empty(lib.nsm_loss_blocks(n), dtype=torch.float32, device=dev)
+    total = torch.zeros((), dtype=torch.float32, device=dev)
+    for t in range(1, len(frames)):
+        a = frames[t].detach().contiguous().to(torch.float32)
+        b = frames[t - 1].detach().contiguous().to(torch.float32)
+        out = torch.empty((), dtype=torch.float32, device=dev)
+        call("nsm_expdiff_mean", ptr(a), ptr(b), n, float(alpha), ptr(partial), ptr(out), stream())
+        total = total + out
+    return total / (len(frames) - 1)

@@ -262,6 +262,21 @@ def vgg_case(name, B, H, W, seed=11):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **rec)
 
 
+def temporal_case(name="temporal_b2_5f"):
+    """measure_temporal_instability (pert_loss.py:166-199) on 5 frames."""
+    import pert_loss
+    g = torch.Generator().manual_seed(21)
+    frames = [torch.sigmoid(torch.randn(2, 1, 48, 40, generator=g)) for _ in range(5)]
+    vals = {a: pert_loss.measure_temporal_instability(frames, alpha=a).item() for a in (5.0, 3.0)}
+    from oracle import unet_ref as O
+    for a, v in vals.items():
+        ov = O.temporal_instability(frames, a).item()
+        print(f"{name}: alpha {a} ref {v:.8e} oracle {ov:.8e}")
+        assert abs(ov - v) <= 1e-6 * abs(v)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), frames=torch.stack(frames).numpy(),
+                        value_a5=np.array(vals[5.0]), value_a3=np.array(vals[3.0]))
+
+
 def dataset_case(name="mmap_norm"):
     """MmapLiverDataset.__getitem__ normalisation (setdata.py:296-328)."""
     import tempfile
@@ -297,6 +312,9 @@ def dataset_case(name="mmap_norm"):
 if __name__ == "__main__":
     torch.set_num_threads(8)
     install_stubs()
+    if sys.argv[1:] == ["temporal"]:
+        temporal_case()
+        sys.exit(0)
     if sys.argv[1:] == ["vgg"]:
         vgg_case("vgg_b2_96x128", 2, 96, 128)
         vgg_case("vgg_b1_40x72", 1, 40, 72)
@@ -310,3 +328,4 @@ if __name__ == "__main__":
     dataset_case()
     vgg_case("vgg_b2_96x128", 2, 96, 128)
     vgg_case("vgg_b1_40x72", 1, 40, 72)
+    temporal_case()

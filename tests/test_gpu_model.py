@@ -255,3 +255,80 @@ def test_bf16_autocast_selects_bf16(device):
     assert m.activation_dtype() == torch.float32
     with torch.autocast("cuda", dtype=torch.bfloat16):
         assert m.activation_dtype() == torch.bfloat16
+
+
+def test_enhanced_custom_loss(device):
+    """EnhancedCustomLoss (pert_loss.py:92-163, made constructible) = its pinned
+    parts: 0.9*L1 + 0.1*VGG (stand-in weights, oracle/vgg_ref.py) + 0.5 *
+    the reference's PerturbationLoss value on the same noise; gradient
+    0.9*sign(o-y)/N + 0.5*(the reference's perturbation output grad);
+    running stats after the three train-mode perturbed forwards as in the reference."""
+    import nsm_amd
+    from oracle import vgg_ref as V
+    fx = load("perturb_c4_b1_64")
+    m = build(device, 4, 0.0, make_state(4, int(fx["meta/seed_w"])), running_from(fx, "run_before/")).train()
+    x = torch.from_numpy(fx["x"]).to(device)
+    out = torch.from_numpy(fx["out"]).to(device).requires_grad_(True)
+    y = torch.rand(out.shape, generator=torch.Generator().manual_seed(4)).to(device)
+    noises = [torch.from_numpy(n).to(device) for n in fx["noise"]]
+    crit = nsm_amd.EnhancedCustomLoss(device, alpha=0.9, perturb_weight=0.5,
+                                      vgg_weights=V.standin_state())
+    total, parts = crit(m, out, y, x, noises=noises)
+    total.backward()
+    l1 = (torch.from_numpy(fx["out"]) - y.cpu()).abs().mean().item()
+    vgg = V.vgg_loss(V.standin_state(), torch.from_numpy(fx["out"]), y.cpu()).item()
+    pert = float(fx["loss"])
+    assert abs(parts["l1_loss"].item() - l1) <= 1e-6 * l1
+    assert abs(parts["vgg_loss"].item() - vgg) <= 2e-5 * vgg
+    assert abs(parts["perturbation_loss"].item() - pert) <= 2e-5 + 1e-2 * pert
+    assert abs(total.item() - (0.9 * l1 + 0.1 * vgg + 0.5 * parts["perturbation_loss"].item())) <= 1e-5
+    ref_g = 0.9 * np.sign(fx["out"] - y.cpu().numpy()) / out.numel() + 0.5 * fx["out_grad"]
+    agree = np.mean(np.abs(out.grad.cpu().numpy() - ref_g) <= 1e-9 + 1e-5 * np.abs(ref_g))
+    assert agree >= 0.99
+    sd = m.state_dict()
+    for k, v in running_from(fx).items():
+        assert np.abs(sd[k].cpu().numpy() - v).max() <= RUN_TOL * (1 + np.abs(v).max()), k
+    crit.eval()   # no perturbation term outside training
+    total_e, parts_e = crit(m, out.detach(), y, x)
+    assert parts_e["perturbation_loss"].item() == 0.0
+
+
+def test_temporal_instability(device):
+    import nsm_amd
+    fx = load("temporal_b2_5f")
+    frames = [torch.from_numpy(f).to(device) for f in fx["frames"]]
+    for a, key in ((5.0, "value_a5"), (3.0, "value_a3")):
+        v = nsm_amd.measure_temporal_instability(frames, alpha=a).item()
+        assert abs(v - float(fx[key])) <= 1e-6 * float(fx[key])
+
+
+def test_frame_loader_matches_dataset(device, tmp_path):
+    """nsm_amd.data.FrameLoader (native mmap + pinned staging + GPU normalise)
+    yields exactly MmapLiverDataset's frames (the reference's
+    normalisation), per rank shard, batch by batch, across an epoch wrap."""
+    import json as _json
+    from nsm_amd.data import FrameLoader, MmapLiverDataset, shard_range
+    rng = np.random.default_rng(3)
+    N, C, H, W = 11, 7, 16, 24
+    inputs = (rng.standard_normal((N, C, H, W)) * 2 + 0.5).astype(np.float32)
+    labels = rng.integers(0, 256, (N, 1, H, W)) / 255.0            # f64, as prepare_dataset.py
+    np.save(tmp_path / "train_inputs.npy", inputs)
+    np.save(tmp_path / "train_labels.npy", labels)
+    st = {"means": inputs.transpose(1, 0, 2, 3).reshape(C, -1).mean(1).tolist(),
+          "stds": inputs.transpose(1, 0, 2, 3).reshape(C, -1).std(1).tolist()}
+    (tmp_path / "train_stats.json").write_text(_json.dumps(st))
+    ds = MmapLiverDataset(str(tmp_path), "train")
+    for world, rank, batch in ((1, 0, 4), (2, 1, 3)):
+        fl = FrameLoader(str(tmp_path), "train", batch, device, world=world, rank=rank)
+        lo, hi = shard_range(N, world, rank)
+        frames = list(range(lo, hi))
+        assert len(fl) == -(-len(frames) // batch)
+        got = [fl.next() for _ in range(len(fl) + 1)]       # one past the epoch: wraps
+        fl.close()
+        for bi, (x, y) in enumerate(got):
+            idx = frames[(bi % len(fl)) * batch:][:batch]
+            ref_x = torch.stack([ds[i][0].detach() for i in idx])
+            ref_y = torch.stack([ds[i][1] for i in idx])
+            assert x.requires_grad and x.shape[0] == len(idx)
+            assert torch.allclose(x.detach().cpu(), ref_x, rtol=1e-6, atol=1e-6)
+            assert torch.equal(y.cpu(), ref_y)

@@ -108,3 +108,10 @@ def test_oracle_vgg_matches_train_fixture_vgg_term():
     fx = load("train_c7_p0_b2_64")
     v = V.vgg_loss(V.standin_state(), torch.from_numpy(fx["out"]), torch.from_numpy(fx["y"])).item()
     assert abs(v - float(fx["vgg"])) <= 1e-6 * abs(v)
+
+
+def test_oracle_temporal_instability():
+    fx = load("temporal_b2_5f")
+    frames = [torch.from_numpy(f) for f in fx["frames"]]
+    assert O.temporal_instability(frames, 5.0).item() == float(fx["value_a5"])
+    assert O.temporal_instability(frames, 3.0).item() == float(fx["value_a3"])
