@@ -33,7 +33,10 @@ def bf_close(got, ref, ulps=2.0):
 @pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 9, 11, 32, 64, 3), (1, 16, 16, 64, 32, 3),
                                            (2, 8, 8, 128, 128, 3), (3, 7, 5, 32, 128, 1),
                                            (2, 32, 32, 64, 512, 1), (1, 5, 67, 96, 32, 3),
-                                           (4, 32, 32, 256, 256, 3)])
+                                           (4, 32, 32, 256, 256, 3),
+                                           # >= 1024 blocks of 256 rows: the LDS-DMA kernel
+                                           (4, 128, 128, 64, 512, 3), (3, 97, 93, 64, 1280, 3),
+                                           (1, 128, 256, 128, 1024, 3)])
 def test_conv_fwd_bf16(ops, device, B, H, W, ci, co, k):
     g = torch.Generator().manual_seed(B * 1000 + H * 10 + ci + co + k)
     x = r(torch.randn(B, ci, H, W, generator=g))
@@ -68,7 +71,8 @@ def test_conv1x1_prologue_bf16(ops, device, B, H, W, ci, co):
 
 
 @pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 9, 11, 32, 64, 3), (2, 8, 8, 64, 64, 3),
-                                           (2, 12, 12, 64, 128, 1)])
+                                           (2, 12, 12, 64, 128, 1),
+                                           (4, 128, 128, 512, 64, 3), (2, 150, 147, 768, 64, 3)])
 def test_conv_dgrad_bf16(ops, device, B, H, W, ci, co, k):
     g = torch.Generator().manual_seed(11)
     x = torch.randn(B, ci, H, W, generator=g, requires_grad=True)
@@ -85,7 +89,13 @@ def test_conv_dgrad_bf16(ops, device, B, H, W, ci, co, k):
                                                (1, 33, 35, 128, 128, 3, False),
                                                (2, 8, 8, 32, 64, 1, True),
                                                (2, 16, 16, 128, 512, 1, True),
-                                               (4, 64, 64, 32, 32, 3, False)])
+                                               (4, 64, 64, 32, 32, 3, False),
+                                               # LDS-DMA tiles 64x64 / 128x128 / 256x128,
+                                               # split-K with pixel tails
+                                               (4, 64, 64, 64, 64, 3, False),
+                                               (2, 12, 10, 128, 512, 3, False),
+                                               (2, 16, 16, 256, 256, 3, False),
+                                               (3, 45, 43, 128, 128, 3, False)])
 def test_conv_wgrad_bf16(ops, device, B, H, W, ci, co, k, pro):
     g = torch.Generator().manual_seed(13)
     x = r(torch.randn(B, ci, H, W, generator=g))
