@@ -143,11 +143,12 @@ int nsm_bn_partials_merge(const float* partial, int nchunk, int rows_per_chunk, 
 int nsm_bn_finalize_eval(const float* run_mean, const float* run_var, const float* gamma,
                          const float* beta, int C, int c_real, float eps, float* mean,
                          float* invstd, float* scale, float* shift, void* stream);
-/* out = lrelu(y*scale+shift, slope) (+ res): BN apply + LeakyReLU
- * (Unetmodel.py:27-28) fused with the additive skip (Unetmodel.py:125,131,137) */
+/* out = lrelu(y*scale+shift, slope) (* mask[row / HW][c]) (+ res): BN apply +
+ * LeakyReLU (Unetmodel.py:22-23,27-28), optionally Dropout2d (:24; mask NULL =
+ * none), fused with the additive skip (Unetmodel.py:125,131,137) */
 int nsm_bn_act(const void* y, int ldy, int M, int C, const float* scale, const float* shift,
-               float slope, const void* res, int ldres, void* out, int ldo, int dtype,
-               void* stream);
+               float slope, const float* mask, int HW, const void* res, int ldres, void* out,
+               int ldo, int dtype, void* stream);
 /* backward of  z = lrelu(mask * ... ) chains around a train-mode BN:
  *   dz = g * mask[b][c] * lrelu'(y*scale+shift); partial {sum dz, sum dz*xhat}. */
 int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy, int M, int C, int HW,

@@ -94,6 +94,36 @@ __device__ __forceinline__ void st4(float* p, f32x4 v) { *(f32x4*)p = v; }
 __device__ __forceinline__ void st4(bf16_t* p, f32x4 v) {
   *(u32x2*)p = u32x2{pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)};
 }
+// 8 consecutive elements per lane (16 B of bf16 / 32 B of fp32): the unit of
+// the streaming kernels, so a bf16 lane moves a full 16-B vector
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+struct F8 {
+  f32x4 a, b;
+};
+__device__ __forceinline__ F8 operator+(F8 x, F8 y) { return F8{x.a + y.a, x.b + y.b}; }
+__device__ __forceinline__ F8 operator-(F8 x, F8 y) { return F8{x.a - y.a, x.b - y.b}; }
+__device__ __forceinline__ F8 operator*(F8 x, F8 y) { return F8{x.a * y.a, x.b * y.b}; }
+__device__ __forceinline__ F8 operator*(float s, F8 x) { return F8{s * x.a, s * x.b}; }
+__device__ __forceinline__ F8& operator+=(F8& x, F8 y) {
+  x.a += y.a;
+  x.b += y.b;
+  return x;
+}
+__device__ __forceinline__ F8 f8zero() { return F8{f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}}; }
+__device__ __forceinline__ F8 ld8(const float* p) { return F8{*(const f32x4*)p, *(const f32x4*)(p + 4)}; }
+__device__ __forceinline__ F8 ld8(const bf16_t* p) {
+  const u32x4 w = *(const u32x4*)p;
+  return F8{f32x4{bf_lo(w.x), bf_hi(w.x), bf_lo(w.y), bf_hi(w.y)},
+            f32x4{bf_lo(w.z), bf_hi(w.z), bf_lo(w.w), bf_hi(w.w)}};
+}
+__device__ __forceinline__ void st8(float* p, F8 v) {
+  *(f32x4*)p = v.a;
+  *(f32x4*)(p + 4) = v.b;
+}
+__device__ __forceinline__ void st8(bf16_t* p, F8 v) {
+  *(u32x4*)p = u32x4{pack_bf2(v.a.x, v.a.y), pack_bf2(v.a.z, v.a.w), pack_bf2(v.b.x, v.b.y),
+                     pack_bf2(v.b.z, v.b.w)};
+}
 __device__ __forceinline__ float ld1(const float* p) { return *p; }
 __device__ __forceinline__ float ld1(const bf16_t* p) { return __uint_as_float((uint32_t)*p << 16); }
 __device__ __forceinline__ void st1(float* p, float v) { *p = v; }

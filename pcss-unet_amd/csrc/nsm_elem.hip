@@ -12,8 +12,12 @@
 namespace nsm {
 
 // ---------------------------------------------------------------------------
+// Streaming layout: every lane moves 8 consecutive channels (F8: one 16-B
+// vector of bf16, two of fp32) and all index math is 32-bit with
+// multiply-high division (no 64-bit divides in the loops).
+// ---------------------------------------------------------------------------
 // Column reductions over an [M][C] NHWC matrix: block = 256 threads laid out
-// as rl row-lanes x cl float4 channel-lanes; grid = (gx channel groups, nchunk).
+// as rl row-lanes x cl 8-channel lanes; grid = (gx channel groups, nchunk).
 // ---------------------------------------------------------------------------
 static inline int gcd_i(int a, int b) {
   while (b) {
@@ -28,9 +32,9 @@ struct ColRed {
 };
 static ColRed colred_plan(int M, int C) {
   ColRed r;
-  r.cl = gcd_i(C / 4, 64);
+  r.cl = gcd_i(C / 8, 64);
   r.rl = 256 / r.cl;
-  r.gx = (C / 4) / r.cl;
+  r.gx = (C / 8) / r.cl;
   long long want = (M + 63) / 64;
   long long cap = 1024 / r.gx;  // ~1024 blocks fill the 256 CUs; finalize stays short
   if (cap < 1) cap = 1;
@@ -40,8 +44,8 @@ static ColRed colred_plan(int M, int C) {
   return r;
 }
 
-// reduce red[rl][cl] (f32x4) over rl; result valid in red[0][tc] for all tc.
-__device__ __forceinline__ void col_tree_reduce(f32x4* red, int cl, int rl, int tid) {
+// reduce red[rl][cl] (F8) over rl; result valid in red[0][tc] for all tc.
+__device__ __forceinline__ void col_tree_reduce(F8* red, int cl, int rl, int tid) {
   for (int s = rl / 2; s > 0; s >>= 1) {
     __syncthreads();
     int tr = tid / cl;
@@ -50,33 +54,37 @@ __device__ __forceinline__ void col_tree_reduce(f32x4* red, int cl, int rl, int 
   __syncthreads();
 }
 
+__device__ __forceinline__ F8 ldf8(const float* p) { return ld8(p); }  // fp32 parameter vectors
+
 template <typename T>
 __global__ void __launch_bounds__(256) bn_stats_kernel(const T* __restrict__ y, int ld, int M,
                                                        int C, int cl, int rl, int rpc,
                                                        float* __restrict__ partial) {
-  __shared__ f32x4 red[256];
+  __shared__ F8 red[256];
   const int tid = threadIdx.x, tc = tid % cl, tr = tid / cl;
-  const int c = (blockIdx.x * cl + tc) * 4;
+  const int c = (blockIdx.x * cl + tc) * 8;
   const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
-  f32x4 s = {0.f, 0.f, 0.f, 0.f};
-  for (int r = r0 + tr; r < r1; r += rl) s += ld4(y + (size_t)r * ld + c);
+  F8 s = f8zero();
+#pragma unroll 4
+  for (int r = r0 + tr; r < r1; r += rl) s += ld8(y + (size_t)r * ld + c);
   red[tid] = s;
   col_tree_reduce(red, cl, rl, tid);
   const float n = (float)max(r1 - r0, 1);
-  const f32x4 sum = red[tc];
-  const f32x4 mean = sum / n;
+  const F8 sum = red[tc];
+  const F8 mean = (1.f / n) * sum;
   __syncthreads();
-  f32x4 s2 = {0.f, 0.f, 0.f, 0.f};
+  F8 s2 = f8zero();
+#pragma unroll 4
   for (int r = r0 + tr; r < r1; r += rl) {
-    f32x4 d = ld4(y + (size_t)r * ld + c) - mean;
+    F8 d = ld8(y + (size_t)r * ld + c) - mean;
     s2 += d * d;
   }
   red[tid] = s2;
   col_tree_reduce(red, cl, rl, tid);
   if (tr == 0) {
     float* pr = partial + (size_t)blockIdx.y * 2 * C;
-    *(f32x4*)(pr + c) = sum;
-    *(f32x4*)(pr + C + c) = red[tc];
+    st8(pr + c, sum);
+    st8(pr + C + c, red[tc]);
   }
 }
 
@@ -191,39 +199,51 @@ __global__ void bn_finalize_eval_kernel(const float* __restrict__ rm, const floa
   shift_o[c] = beta[c] - m * sc;
 }
 
+__device__ __forceinline__ f32x4 lrelu4(f32x4 v, float slope) {
+  return f32x4{lrelu(v.x, slope), lrelu(v.y, slope), lrelu(v.z, slope), lrelu(v.w, slope)};
+}
+__device__ __forceinline__ F8 lrelu8(F8 v, float slope) {
+  return F8{lrelu4(v.a, slope), lrelu4(v.b, slope)};
+}
+
+// Pixel-row streaming (bn_act, bn_bwd_apply): a block covers whole pixels
+// (blockDim = k*C8, pix_launch), so each lane keeps ONE 8-channel group for
+// the whole grid-stride loop and its per-channel vectors stay in registers.
+//
+// out = lrelu(y*scale+shift) (* mask[b][c]) (+ res)
 template <typename T>
-__global__ void bn_act_kernel(const T* __restrict__ y, int ldy, int M, int C4,
-                              const float* __restrict__ scale, const float* __restrict__ shift,
-                              float slope, const T* __restrict__ res, int ldres,
-                              T* __restrict__ out, int ldo) {
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long total = (long long)M * C4;
-  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int p = (int)(i / C4), c = (int)(i - (long long)p * C4) * 4;
-    f32x4 v = ld4(y + (size_t)p * ldy + c);
-    f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
-    f32x4 o;
-    o.x = lrelu(v.x * sc.x + sh.x, slope);
-    o.y = lrelu(v.y * sc.y + sh.y, slope);
-    o.z = lrelu(v.z * sc.z + sh.z, slope);
-    o.w = lrelu(v.w * sc.w + sh.w, slope);
-    if (res) o += ld4(res + (size_t)p * ldres + c);
-    st4(out + (size_t)p * ldo + c, o);
+__global__ void __launch_bounds__(256) bn_act_kernel(const T* __restrict__ y, int ldy, int M,
+                                                     int C8, FastDiv fdHW,
+                                                     const float* __restrict__ scale,
+                                                     const float* __restrict__ shift, float slope,
+                                                     const float* __restrict__ mask,
+                                                     const T* __restrict__ res, int ldres,
+                                                     T* __restrict__ out, int ldo) {
+  const int ppb = blockDim.x / C8, tp = threadIdx.x / C8;
+  const int c = (threadIdx.x - tp * C8) * 8;
+  const F8 sc = ldf8(scale + c), sh = ldf8(shift + c);
+  const int pstep = gridDim.x * ppb;
+  for (int p = blockIdx.x * ppb + tp; p < M; p += pstep) {
+    F8 o = lrelu8(ld8(y + (size_t)p * ldy + c) * sc + sh, slope);
+    // Dropout2d after the LeakyReLU (Unetmodel.py:23-24)
+    if (mask) o = o * ld8(mask + (size_t)fdiv((uint32_t)p, fdHW) * (C8 * 8) + c);
+    if (res) o += ld8(res + (size_t)p * ldres + c);
+    st8(out + (size_t)p * ldo + c, o);
   }
 }
 
 // dz = g * mask[b][c] * lrelu'(y*scale+shift)
-__device__ __forceinline__ f32x4 bn_dz(const f32x4 g, const f32x4 v, const f32x4 sc,
-                                       const f32x4 sh, float slope, const float* mask, int b,
-                                       int C, int c) {
-  f32x4 d;
-  d.x = g.x * lrelu_grad(v.x * sc.x + sh.x, slope);
-  d.y = g.y * lrelu_grad(v.y * sc.y + sh.y, slope);
-  d.z = g.z * lrelu_grad(v.z * sc.z + sh.z, slope);
-  d.w = g.w * lrelu_grad(v.w * sc.w + sh.w, slope);
+__device__ __forceinline__ f32x4 lrelu_grad4(f32x4 z, float slope) {
+  return f32x4{lrelu_grad(z.x, slope), lrelu_grad(z.y, slope), lrelu_grad(z.z, slope),
+               lrelu_grad(z.w, slope)};
+}
+__device__ __forceinline__ F8 bn_dz8(const F8 g, const F8 v, const F8 sc, const F8 sh,
+                                     float slope, const float* mask, int b, int C, int c) {
+  const F8 z = v * sc + sh;
+  F8 d{g.a * lrelu_grad4(z.a, slope), g.b * lrelu_grad4(z.b, slope)};
   // Dropout2d sits AFTER the LeakyReLU (Unetmodel.py:23-24): d(out)/d(z) =
   // mask * lrelu'(z); multiplication order does not matter for the value.
-  if (mask) d *= *(const f32x4*)(mask + (size_t)b * C + c);
+  if (mask) d = d * ld8(mask + (size_t)b * C + c);
   return d;
 }
 
@@ -233,31 +253,32 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     FastDiv fdHW, const float* __restrict__ scale, const float* __restrict__ shift, float slope,
     const float* __restrict__ mask, const float* __restrict__ mean,
     const float* __restrict__ invstd, int cl, int rl, int rpc, float* __restrict__ partial) {
-  __shared__ f32x4 red[256];
+  __shared__ F8 red[256];
   const int tid = threadIdx.x, tc = tid % cl, tr = tid / cl;
-  const int c = (blockIdx.x * cl + tc) * 4;
+  const int c = (blockIdx.x * cl + tc) * 8;
   const int r0 = blockIdx.y * rpc, r1 = min(M, r0 + rpc);
-  const f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
-  const f32x4 mu = *(const f32x4*)(mean + c), is = *(const f32x4*)(invstd + c);
-  f32x4 s1 = {0.f, 0.f, 0.f, 0.f}, s2 = {0.f, 0.f, 0.f, 0.f};
+  const F8 sc = ldf8(scale + c), sh = ldf8(shift + c);
+  const F8 mu = ldf8(mean + c), is = ldf8(invstd + c);
+  F8 s1 = f8zero(), s2 = f8zero();
+#pragma unroll 2
   for (int r = r0 + tr; r < r1; r += rl) {
-    f32x4 v = ld4(y + (size_t)r * ldy + c);
-    f32x4 gg = ld4(g + (size_t)r * ldg + c);
-    int b = mask ? (int)fdiv((uint32_t)r, fdHW) : 0;
-    f32x4 dz = bn_dz(gg, v, sc, sh, slope, mask, b, C, c);
+    const F8 v = ld8(y + (size_t)r * ldy + c);
+    const F8 gg = ld8(g + (size_t)r * ldg + c);
+    const int b = mask ? (int)fdiv((uint32_t)r, fdHW) : 0;
+    const F8 dz = bn_dz8(gg, v, sc, sh, slope, mask, b, C, c);
     s1 += dz;
     s2 += dz * ((v - mu) * is);
   }
   red[tid] = s1;
   col_tree_reduce(red, cl, rl, tid);
-  f32x4 t1 = red[tc];
+  const F8 t1 = red[tc];
   __syncthreads();
   red[tid] = s2;
   col_tree_reduce(red, cl, rl, tid);
   if (tr == 0) {
     float* pr = partial + (size_t)blockIdx.y * 2 * C;
-    *(f32x4*)(pr + c) = t1;
-    *(f32x4*)(pr + C + c) = red[tc];
+    st8(pr + c, t1);
+    st8(pr + C + c, red[tc]);
   }
 }
 
@@ -300,26 +321,22 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
 }
 
 template <typename T>
-__global__ void bn_bwd_apply_kernel(const T* __restrict__ g, int ldg,
-                                    const T* __restrict__ y, int ldy, int M, int C,
-                                    FastDiv fdHW, const float* __restrict__ scale,
-                                    const float* __restrict__ shift, float slope,
-                                    const float* __restrict__ mask, const float* __restrict__ mean,
-                                    const float* __restrict__ coef, T* __restrict__ dy,
-                                    int lddy) {
-  const int C4 = C / 4;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  long long total = (long long)M * C4;
-  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int p = (int)(i / C4), c = (int)(i - (long long)p * C4) * 4;
-    f32x4 v = ld4(y + (size_t)p * ldy + c);
-    f32x4 gg = ld4(g + (size_t)p * ldg + c);
-    f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
-    int b = mask ? (int)fdiv((uint32_t)p, fdHW) : 0;
-    f32x4 dz = bn_dz(gg, v, sc, sh, slope, mask, b, C, c);
-    f32x4 k1 = *(const f32x4*)(coef + c), k2 = *(const f32x4*)(coef + C + c),
-          k3 = *(const f32x4*)(coef + 2 * C + c), mu = *(const f32x4*)(mean + c);
-    st4(dy + (size_t)p * lddy + c, k1 * dz + k2 * (v - mu) + k3);
+__global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
+    const T* __restrict__ g, int ldg, const T* __restrict__ y, int ldy, int M, int C, int C8,
+    FastDiv fdHW, const float* __restrict__ scale, const float* __restrict__ shift, float slope,
+    const float* __restrict__ mask, const float* __restrict__ mean,
+    const float* __restrict__ coef, T* __restrict__ dy, int lddy) {
+  const int ppb = blockDim.x / C8, tp = threadIdx.x / C8;
+  const int c = (threadIdx.x - tp * C8) * 8;
+  const F8 sc = ldf8(scale + c), sh = ldf8(shift + c), mu = ldf8(mean + c);
+  const F8 k1 = ldf8(coef + c), k2 = ldf8(coef + C + c), k3 = ldf8(coef + 2 * C + c);
+  const int pstep = gridDim.x * ppb;
+  for (int p = blockIdx.x * ppb + tp; p < M; p += pstep) {
+    const F8 v = ld8(y + (size_t)p * ldy + c);
+    const F8 gg = ld8(g + (size_t)p * ldg + c);
+    const int b = mask ? (int)fdiv((uint32_t)p, fdHW) : 0;
+    const F8 dz = bn_dz8(gg, v, sc, sh, slope, mask, b, C, c);
+    st8(dy + (size_t)p * lddy + c, k1 * dz + k2 * (v - mu) + k3);
   }
 }
 
@@ -327,45 +344,48 @@ __global__ void bn_bwd_apply_kernel(const T* __restrict__ g, int ldg,
 // AvgPool2d(2), floor mode
 // ---------------------------------------------------------------------------
 template <typename T>
-__global__ void avgpool2_fwd_kernel(const T* __restrict__ x, int B, int H, int W, int C4,
-                                    T* __restrict__ y) {
-  const int Ho = H / 2, Wo = W / 2;
-  long long total = (long long)B * Ho * Wo * C4;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int c = (int)(i % C4);
-    long long t = i / C4;
-    int ox = (int)(t % Wo);
-    t /= Wo;
-    int oy = (int)(t % Ho);
-    int b = (int)(t / Ho);
-    const T* base = x + (((size_t)b * H + 2 * oy) * W + 2 * ox) * (C4 * 4) + c * 4;
-    size_t rs = (size_t)W * C4 * 4, cs = (size_t)C4 * 4;
-    f32x4 s = ld4(base);
-    s += ld4(base + cs);
-    s += ld4(base + rs);
-    s += ld4(base + rs + cs);
-    st4(y + (size_t)i * 4, s * 0.25f);
+__global__ void __launch_bounds__(256) avgpool2_fwd_kernel(const T* __restrict__ x, int B, int H,
+                                                           int W, int C8, FastDiv fdC8,
+                                                           FastDiv fdWo, FastDiv fdHo,
+                                                           T* __restrict__ y) {
+  const int Ho = H / 2, Wo = W / 2, C = C8 * 8;
+  const uint32_t total = (uint32_t)B * Ho * Wo * C8;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t p = fdiv(i, fdC8);
+    const int c = (int)(i - p * (uint32_t)C8) * 8;
+    const uint32_t t = fdiv(p, fdWo);
+    const int ox = (int)(p - t * Wo);
+    const uint32_t b = fdiv(t, fdHo);
+    const int oy = (int)(t - b * Ho);
+    const T* base = x + (((size_t)b * H + 2 * oy) * W + 2 * ox) * C + c;
+    const size_t rs = (size_t)W * C;
+    F8 s = ld8(base);
+    s += ld8(base + C);
+    s += ld8(base + rs);
+    s += ld8(base + rs + C);
+    st8(y + (size_t)p * C + c, 0.25f * s);
   }
 }
 
 template <typename T>
-__global__ void avgpool2_bwd_add_kernel(const T* __restrict__ dy, int B, int H, int W, int C4,
-                                        const T* __restrict__ skip, T* __restrict__ dx) {
-  const int Ho = H / 2, Wo = W / 2;
-  long long total = (long long)B * H * W * C4;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int c = (int)(i % C4);
-    long long t = i / C4;
-    int xx = (int)(t % W);
-    t /= W;
-    int yy = (int)(t % H);
-    int b = (int)(t / H);
-    f32x4 v = skip ? ld4(skip + (size_t)i * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-    int oy = yy >> 1, ox = xx >> 1;
-    if (oy < Ho && ox < Wo) v += ld4(dy + ((((size_t)b * Ho + oy) * Wo + ox) * C4 + c) * 4) * 0.25f;
-    st4(dx + (size_t)i * 4, v);
+__global__ void __launch_bounds__(256) avgpool2_bwd_add_kernel(const T* __restrict__ dy, int B,
+                                                               int H, int W, int C8, FastDiv fdC8,
+                                                               FastDiv fdW, FastDiv fdH,
+                                                               const T* __restrict__ skip,
+                                                               T* __restrict__ dx) {
+  const int Ho = H / 2, Wo = W / 2, C = C8 * 8;
+  const uint32_t total = (uint32_t)B * H * W * C8;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t p = fdiv(i, fdC8);
+    const int c = (int)(i - p * (uint32_t)C8) * 8;
+    const uint32_t t = fdiv(p, fdW);
+    const int xx = (int)(p - t * W);
+    const uint32_t b = fdiv(t, fdH);
+    const int yy = (int)(t - b * H);
+    F8 v = skip ? ld8(skip + (size_t)p * C + c) : f8zero();
+    const int oy = yy >> 1, ox = xx >> 1;
+    if (oy < Ho && ox < Wo) v += 0.25f * ld8(dy + (((size_t)b * Ho + oy) * Wo + ox) * C + c);
+    st8(dx + (size_t)p * C + c, v);
   }
 }
 
@@ -386,19 +406,61 @@ __device__ __forceinline__ void lin_idx(float scale, int dst, int in, int& i0, i
   i1 = i0 + (i0 < in - 1 ? 1 : 0);
 }
 
-static inline float ac_scale(int in, int out) {
+static inline float ac_scale(int in, int out) {  // align_corners source step
   return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
 }
 
-template <bool VEC, typename T>
-__global__ void resize_fwd_kernel(const T* __restrict__ x, int B, int Hi, int Wi, int C,
-                                  T* __restrict__ y, int Ho, int Wo, float sh, float sw) {
-  const int CV = VEC ? C / 4 : C;
-  long long total = (long long)B * Ho * Wo * CV;
+// (pixel, 8-channel group) of a flat index over [B][H][W][C8] (32-bit fast division)
+struct Pix8 {
+  int b, y, x, c;
+};
+__device__ __forceinline__ Pix8 pix8(uint32_t i, int C8, int H, int W, const FastDiv& fdC8,
+                                     const FastDiv& fdW, const FastDiv& fdH, uint32_t& p) {
+  Pix8 r;
+  p = fdiv(i, fdC8);
+  r.c = (int)(i - p * (uint32_t)C8) * 8;
+  const uint32_t t = fdiv(p, fdW);
+  r.x = (int)(p - t * (uint32_t)W);
+  const uint32_t b = fdiv(t, fdH);
+  r.y = (int)(t - b * (uint32_t)H);
+  r.b = (int)b;
+  return r;
+}
+
+// 8 channels (one 16-B bf16 vector / two fp32 vectors) per lane: the model's
+// activations (C % 8 == 0)
+template <typename T>
+__global__ void __launch_bounds__(256) resize_fwd8_kernel(const T* __restrict__ x, int Hi, int Wi,
+                                                          int C8, uint32_t total, FastDiv fdC8,
+                                                          FastDiv fdWo, FastDiv fdHo,
+                                                          T* __restrict__ y, int Ho, int Wo,
+                                                          float sh, float sw) {
+  const int C = C8 * 8;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    uint32_t p;
+    const Pix8 q = pix8(i, C8, Ho, Wo, fdC8, fdWo, fdHo, p);
+    int y0, y1, x0, x1;
+    float ly0, ly1, lx0, lx1;
+    lin_idx(sh, q.y, Hi, y0, y1, ly0, ly1);
+    lin_idx(sw, q.x, Wi, x0, x1, lx0, lx1);
+    const size_t rb = (size_t)q.b * Hi;
+    const T* r0 = x + (rb + y0) * Wi * C + q.c;
+    const T* r1 = x + (rb + y1) * Wi * C + q.c;
+    const F8 v = ly0 * (lx0 * ld8(r0 + x0 * C) + lx1 * ld8(r0 + x1 * C)) +
+                 ly1 * (lx0 * ld8(r1 + x0 * C) + lx1 * ld8(r1 + x1 * C));
+    st8(y + (size_t)p * C + q.c, v);
+  }
+}
+
+// any C: the odd-size input guard (Unetmodel.py:94-97) runs on [B*C][H][W][1]
+template <typename T>
+__global__ void resize_fwd1_kernel(const T* __restrict__ x, int B, int Hi, int Wi, int C,
+                                   T* __restrict__ y, int Ho, int Wo, float sh, float sw) {
+  long long total = (long long)B * Ho * Wo * C;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int c = (int)(i % CV);
-    long long t = i / CV;
+    int c = (int)(i % C);
+    long long t = i / C;
     int ox = (int)(t % Wo);
     t /= Wo;
     int oy = (int)(t % Ho);
@@ -408,20 +470,11 @@ __global__ void resize_fwd_kernel(const T* __restrict__ x, int B, int Hi, int Wi
     lin_idx(sh, oy, Hi, y0, y1, ly0, ly1);
     lin_idx(sw, ox, Wi, x0, x1, lx0, lx1);
     const size_t rb = (size_t)b * Hi;
-    if constexpr (VEC) {
-      const T* p00 = x + ((rb + y0) * Wi + x0) * C + c * 4;
-      const T* p01 = x + ((rb + y0) * Wi + x1) * C + c * 4;
-      const T* p10 = x + ((rb + y1) * Wi + x0) * C + c * 4;
-      const T* p11 = x + ((rb + y1) * Wi + x1) * C + c * 4;
-      f32x4 v = ly0 * (lx0 * ld4(p00) + lx1 * ld4(p01)) + ly1 * (lx0 * ld4(p10) + lx1 * ld4(p11));
-      st4(y + (size_t)i * 4, v);
-    } else {
-      float v = ly0 * (lx0 * ld1(x + ((rb + y0) * Wi + x0) * C + c) +
-                       lx1 * ld1(x + ((rb + y0) * Wi + x1) * C + c)) +
-                ly1 * (lx0 * ld1(x + ((rb + y1) * Wi + x0) * C + c) +
-                       lx1 * ld1(x + ((rb + y1) * Wi + x1) * C + c));
-      st1(y + i, v);
-    }
+    float v = ly0 * (lx0 * ld1(x + ((rb + y0) * Wi + x0) * C + c) +
+                     lx1 * ld1(x + ((rb + y0) * Wi + x1) * C + c)) +
+              ly1 * (lx0 * ld1(x + ((rb + y1) * Wi + x0) * C + c) +
+                     lx1 * ld1(x + ((rb + y1) * Wi + x1) * C + c));
+    st1(y + i, v);
   }
 }
 
@@ -443,15 +496,61 @@ __device__ __forceinline__ void cand_range(float scale, int i, int out, int& lo,
   hi = min(out - 1, (int)ceilf((float)(i + 1) / scale) + 1);
 }
 
-template <bool VEC, typename T>
-__global__ void resize_bwd_kernel(const T* __restrict__ dy, int B, int Hi, int Wi, int C,
-                                  T* __restrict__ dx, int Ho, int Wo, float sh, float sw) {
-  const int CV = VEC ? C / 4 : C;
-  long long total = (long long)B * Hi * Wi * CV;
+// The backward gathers keep the x-axis candidate weights of a lane in a fully
+// unrolled register array (a runtime-indexed one would live in scratch); a
+// wider window (extreme downsizing) takes the on-the-fly loop.
+constexpr int RS_MAXC = 16;
+
+template <typename T>
+__global__ void __launch_bounds__(256) resize_bwd8_kernel(const T* __restrict__ dy, int Hi, int Wi,
+                                                          int C8, uint32_t total, FastDiv fdC8,
+                                                          FastDiv fdWi, FastDiv fdHi,
+                                                          T* __restrict__ dx, int Ho, int Wo,
+                                                          float sh, float sw) {
+  const int C = C8 * 8;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    uint32_t p;
+    const Pix8 q = pix8(i, C8, Hi, Wi, fdC8, fdWi, fdHi, p);
+    int ylo, yhi, xlo, xhi;
+    cand_range(sh, q.y, Ho, ylo, yhi);
+    cand_range(sw, q.x, Wo, xlo, xhi);
+    const T* base = dy + (size_t)q.b * Ho * Wo * C + q.c;
+    F8 acc = f8zero();
+    if (xhi - xlo < RS_MAXC) {
+      float wx[RS_MAXC];
+#pragma unroll
+      for (int k = 0; k < RS_MAXC; ++k) wx[k] = xlo + k <= xhi ? lin_w(sw, xlo + k, Wi, q.x) : 0.f;
+      for (int oy = ylo; oy <= yhi; ++oy) {
+        const float wy = lin_w(sh, oy, Hi, q.y);
+        if (wy == 0.f) continue;
+        const T* row = base + (size_t)oy * Wo * C;
+#pragma unroll
+        for (int k = 0; k < RS_MAXC; ++k)
+          if (wx[k] != 0.f) acc += (wy * wx[k]) * ld8(row + (size_t)(xlo + k) * C);
+      }
+    } else {
+      for (int oy = ylo; oy <= yhi; ++oy) {
+        const float wy = lin_w(sh, oy, Hi, q.y);
+        if (wy == 0.f) continue;
+        const T* row = base + (size_t)oy * Wo * C;
+        for (int ox = xlo; ox <= xhi; ++ox) {
+          const float w = lin_w(sw, ox, Wi, q.x);
+          if (w != 0.f) acc += (wy * w) * ld8(row + (size_t)ox * C);
+        }
+      }
+    }
+    st8(dx + (size_t)p * C + q.c, acc);
+  }
+}
+
+template <typename T>
+__global__ void resize_bwd1_kernel(const T* __restrict__ dy, int B, int Hi, int Wi, int C,
+                                   T* __restrict__ dx, int Ho, int Wo, float sh, float sw) {
+  long long total = (long long)B * Hi * Wi * C;
   long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   for (; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int c = (int)(i % CV);
-    long long t = i / CV;
+    int c = (int)(i % C);
+    long long t = i / C;
     int ix = (int)(t % Wi);
     t /= Wi;
     int iy = (int)(t % Hi);
@@ -459,28 +558,17 @@ __global__ void resize_bwd_kernel(const T* __restrict__ dy, int B, int Hi, int W
     int ylo, yhi, xlo, xhi;
     cand_range(sh, iy, Ho, ylo, yhi);
     cand_range(sw, ix, Wo, xlo, xhi);
-    float wxs[16];
-    int nx = 0, xs0 = xlo;
-    for (int ox = xlo; ox <= xhi && nx < 16; ++ox) wxs[nx++] = lin_w(sw, ox, Wi, ix);
-    f32x4 acc4 = {0.f, 0.f, 0.f, 0.f};
     float acc = 0.f;
     for (int oy = ylo; oy <= yhi; ++oy) {
-      float wy = lin_w(sh, oy, Hi, iy);
+      const float wy = lin_w(sh, oy, Hi, iy);
       if (wy == 0.f) continue;
       const T* row = dy + ((size_t)b * Ho + oy) * Wo * C;
-      for (int k = 0; k < nx; ++k) {
-        float w = wxs[k];
-        if (w == 0.f) continue;
-        if constexpr (VEC)
-          acc4 += (wy * w) * ld4(row + (size_t)(xs0 + k) * C + c * 4);
-        else
-          acc += (wy * w) * ld1(row + (size_t)(xs0 + k) * C + c);
+      for (int ox = xlo; ox <= xhi; ++ox) {
+        const float w = lin_w(sw, ox, Wi, ix);
+        if (w != 0.f) acc += (wy * w) * ld1(row + (size_t)ox * C + c);
       }
     }
-    if constexpr (VEC)
-      st4(dx + (size_t)i * 4, acc4);
-    else
-      st1(dx + i, acc);
+    st1(dx + i, acc);
   }
 }
 
@@ -492,43 +580,39 @@ __global__ void resize_bwd_kernel(const T* __restrict__ dy, int B, int Hi, int W
 // separable combined weights W[o->i] = sum_m w2(o->m) w1(m->i).
 // ---------------------------------------------------------------------------
 template <typename T>
-__device__ __forceinline__ f32x4 up_sample4(const T* __restrict__ x, size_t rb, int h, int w,
-                                            int C, int c4, float s1h, float s1w, int my, int mx) {
+__device__ __forceinline__ F8 up_sample8(const T* __restrict__ x, size_t rb, int h, int w, int C,
+                                         int c, float s1h, float s1w, int my, int mx) {
   int y0, y1, x0, x1;
   float a0, a1, b0, b1;
   lin_idx(s1h, my, h, y0, y1, a0, a1);
   lin_idx(s1w, mx, w, x0, x1, b0, b1);
-  const f32x4 v00 = ld4(x + ((rb + y0) * w + x0) * C + c4 * 4);
-  const f32x4 v01 = ld4(x + ((rb + y0) * w + x1) * C + c4 * 4);
-  const f32x4 v10 = ld4(x + ((rb + y1) * w + x0) * C + c4 * 4);
-  const f32x4 v11 = ld4(x + ((rb + y1) * w + x1) * C + c4 * 4);
-  return a0 * (b0 * v00 + b1 * v01) + a1 * (b0 * v10 + b1 * v11);
+  const T* r0 = x + (rb + y0) * w * C + c;
+  const T* r1 = x + (rb + y1) * w * C + c;
+  return a0 * (b0 * ld8(r0 + x0 * C) + b1 * ld8(r0 + x1 * C)) +
+         a1 * (b0 * ld8(r1 + x0 * C) + b1 * ld8(r1 + x1 * C));
 }
 
 template <typename T>
-__global__ void up2_resize_fwd_kernel(const T* __restrict__ x, int B, int h, int w, int C,
-                                      T* __restrict__ y, int th, int tw, float s1h, float s1w,
-                                      float s2h, float s2w) {
-  const int C4 = C / 4, h2 = 2 * h, w2 = 2 * w;
-  long long total = (long long)B * th * tw * C4;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    int c = (int)(i % C4);
-    long long t = i / C4;
-    int ox = (int)(t % tw);
-    t /= tw;
-    int oy = (int)(t % th);
-    int b = (int)(t / th);
+__global__ void __launch_bounds__(256) up2_resize_fwd8_kernel(const T* __restrict__ x, int h, int w,
+                                                              int C8, uint32_t total,
+                                                              FastDiv fdC8, FastDiv fdtw,
+                                                              FastDiv fdth, T* __restrict__ y,
+                                                              int th, int tw, float s1h, float s1w,
+                                                              float s2h, float s2w) {
+  const int C = C8 * 8, h2 = 2 * h, w2 = 2 * w;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    uint32_t p;
+    const Pix8 q = pix8(i, C8, th, tw, fdC8, fdtw, fdth, p);
     int m0, m1, n0, n1;
     float l0, l1, k0, k1;
-    lin_idx(s2h, oy, h2, m0, m1, l0, l1);
-    lin_idx(s2w, ox, w2, n0, n1, k0, k1);
-    const size_t rb = (size_t)b * h;
-    f32x4 u00 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m0, n0);
-    f32x4 u01 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m0, n1);
-    f32x4 u10 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m1, n0);
-    f32x4 u11 = up_sample4(x, rb, h, w, C, c, s1h, s1w, m1, n1);
-    st4(y + (size_t)i * 4, l0 * (k0 * u00 + k1 * u01) + l1 * (k0 * u10 + k1 * u11));
+    lin_idx(s2h, q.y, h2, m0, m1, l0, l1);
+    lin_idx(s2w, q.x, w2, n0, n1, k0, k1);
+    const size_t rb = (size_t)q.b * h;
+    const F8 u00 = up_sample8(x, rb, h, w, C, q.c, s1h, s1w, m0, n0);
+    const F8 u01 = up_sample8(x, rb, h, w, C, q.c, s1h, s1w, m0, n1);
+    const F8 u10 = up_sample8(x, rb, h, w, C, q.c, s1h, s1w, m1, n0);
+    const F8 u11 = up_sample8(x, rb, h, w, C, q.c, s1h, s1w, m1, n1);
+    st8(y + (size_t)p * C + q.c, l0 * (k0 * u00 + k1 * u01) + l1 * (k0 * u10 + k1 * u11));
   }
 }
 
@@ -544,46 +628,56 @@ __device__ __forceinline__ float comb_w(float s2, int o, int n2, float s1, int n
 }
 
 template <typename T>
-__global__ void up2_resize_bwd_kernel(const T* __restrict__ dy, int B, int h, int w, int C,
-                                      T* __restrict__ dx, int th, int tw, float s1h, float s1w,
-                                      float s2h, float s2w) {
-  const int C4 = C / 4, h2 = 2 * h, w2 = 2 * w;
-  long long total = (long long)B * h * w * C4;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    int c = (int)(i % C4);
-    long long t = i / C4;
-    int ix = (int)(t % w);
-    t /= w;
-    int iy = (int)(t % h);
-    int b = (int)(t / h);
+__global__ void __launch_bounds__(256) up2_resize_bwd8_kernel(const T* __restrict__ dy, int h,
+                                                              int w, int C8, uint32_t total,
+                                                              FastDiv fdC8, FastDiv fdw,
+                                                              FastDiv fdh, T* __restrict__ dx,
+                                                              int th, int tw, float s1h, float s1w,
+                                                              float s2h, float s2w) {
+  const int C = C8 * 8, h2 = 2 * h, w2 = 2 * w;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    uint32_t p;
+    const Pix8 q = pix8(i, C8, h, w, fdC8, fdw, fdh, p);
     // intermediate rows touching iy, then final rows touching those
     int mlo, mhi, olo, ohi, olo2, ohi2;
-    cand_range(s1h, iy, h2, mlo, mhi);
+    cand_range(s1h, q.y, h2, mlo, mhi);
     cand_range(s2h, mlo, th, olo, ohi2);
     cand_range(s2h, mhi, th, olo2, ohi);
     olo = min(olo, olo2);
     ohi = max(ohi, ohi2);
     int nlo, nhi, plo, phi, plo2, phi2;
-    cand_range(s1w, ix, w2, nlo, nhi);
+    cand_range(s1w, q.x, w2, nlo, nhi);
     cand_range(s2w, nlo, tw, plo, phi2);
     cand_range(s2w, nhi, tw, plo2, phi);
     plo = min(plo, plo2);
     phi = max(phi, phi2);
-    float wx[24];
-    int nx = 0;
-    for (int ox = plo; ox <= phi && nx < 24; ++ox) wx[nx++] = comb_w(s2w, ox, w2, s1w, w, ix);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int oy = olo; oy <= ohi; ++oy) {
-      float wy = comb_w(s2h, oy, h2, s1h, h, iy);
-      if (wy == 0.f) continue;
-      const T* row = dy + ((size_t)b * th + oy) * tw * C + c * 4;
-      for (int k = 0; k < nx; ++k) {
-        if (wx[k] == 0.f) continue;
-        acc += (wy * wx[k]) * ld4(row + (size_t)(plo + k) * C);
+    const T* base = dy + (size_t)q.b * th * tw * C + q.c;
+    F8 acc = f8zero();
+    if (phi - plo < RS_MAXC) {
+      float wx[RS_MAXC];
+#pragma unroll
+      for (int k = 0; k < RS_MAXC; ++k)
+        wx[k] = plo + k <= phi ? comb_w(s2w, plo + k, w2, s1w, w, q.x) : 0.f;
+      for (int oy = olo; oy <= ohi; ++oy) {
+        const float wy = comb_w(s2h, oy, h2, s1h, h, q.y);
+        if (wy == 0.f) continue;
+        const T* row = base + (size_t)oy * tw * C;
+#pragma unroll
+        for (int k = 0; k < RS_MAXC; ++k)
+          if (wx[k] != 0.f) acc += (wy * wx[k]) * ld8(row + (size_t)(plo + k) * C);
+      }
+    } else {
+      for (int oy = olo; oy <= ohi; ++oy) {
+        const float wy = comb_w(s2h, oy, h2, s1h, h, q.y);
+        if (wy == 0.f) continue;
+        const T* row = base + (size_t)oy * tw * C;
+        for (int ox = plo; ox <= phi; ++ox) {
+          const float wxk = comb_w(s2w, ox, w2, s1w, w, q.x);
+          if (wxk != 0.f) acc += (wy * wxk) * ld8(row + (size_t)ox * C);
+        }
       }
     }
-    st4(dx + (size_t)i * 4, acc);
+    st8(dx + (size_t)p * C + q.c, acc);
   }
 }
 
@@ -950,7 +1044,7 @@ using namespace nsm;
 
 // ============================== C ABI ======================================
 extern "C" int nsm_reduce_chunks(int M, int C) {
-  if (M <= 0 || C <= 0 || C % 4) return 0;
+  if (M <= 0 || C <= 0 || C % 8) return 0;
   return colred_plan(M, C).nchunk;
 }
 
@@ -959,7 +1053,7 @@ extern "C" int nsm_reduce_chunks(int M, int C) {
 
 extern "C" int nsm_bn_stats(const void* y, int ld, int M, int C, float* partial, int nchunk,
                             int dtype, void* stream) {
-  NSM_CHECK_ARG(y && partial && M > 0 && C % 4 == 0 && ld % 4 == 0, "bn_stats: bad args");
+  NSM_CHECK_ARG(y && partial && M > 0 && C % 8 == 0 && ld % 8 == 0, "bn_stats: bad args");
   ColRed r = colred_plan(M, C);
   NSM_CHECK_ARG(nchunk == r.nchunk, "bn_stats: nchunk %d != %d", nchunk, r.nchunk);
   dim3 g(r.gx, r.nchunk);
@@ -974,7 +1068,7 @@ extern "C" int nsm_bn_stats(const void* y, int ld, int M, int C, float* partial,
 }
 
 extern "C" int nsm_reduce_rows(int M, int C) {
-  if (M <= 0 || C <= 0 || C % 4) return 0;
+  if (M <= 0 || C <= 0 || C % 8) return 0;
   return colred_plan(M, C).rpc;
 }
 
@@ -1018,19 +1112,36 @@ extern "C" int nsm_bn_finalize_eval(const float* run_mean, const float* run_var,
   return 0;
 }
 
+// streaming launch over [M pixels][C8 channel groups]: blockDim = the largest
+// multiple of C8 <= 256 (each lane keeps one channel group), <= 2048 blocks
+static void pix_launch(long long M, int C8, dim3& grid, dim3& block) {
+  const int tpb = (256 / C8) * C8;
+  const long long ppb = tpb / C8;
+  long long g = (M + ppb - 1) / ppb;
+  g = g < 1 ? 1 : (g > 2048 ? 2048 : g);
+  grid = dim3((unsigned)g);
+  block = dim3((unsigned)tpb);
+}
+
 extern "C" int nsm_bn_act(const void* y, int ldy, int M, int C, const float* scale,
-                          const float* shift, float slope, const void* res, int ldres, void* out,
-                          int ldo, int dtype, void* stream) {
-  NSM_CHECK_ARG(y && scale && shift && out && C % 4 == 0, "bn_act: bad args");
-  long long work = (long long)M * (C / 4);
-  dim3 g(grid_for(work));
+                          const float* shift, float slope, const float* mask, int HW,
+                          const void* res, int ldres, void* out, int ldo, int dtype,
+                          void* stream) {
+  NSM_CHECK_ARG(y && scale && shift && out && C % 8 == 0 && C <= 2048 && ldy % 8 == 0 &&
+                    ldo % 8 == 0 && (!res || ldres % 8 == 0) && (!mask || HW > 0),
+                "bn_act: bad args");
+  NSM_CHECK_ARG(M >= 0 && M < (1 << 30), "bn_act: too large");
+  if (M == 0) return 0;
+  dim3 g, b;
+  pix_launch(M, C / 8, g, b);
+  const FastDiv fh = make_fastdiv(mask ? HW : 1);
   if (dtype == NSM_BF16)
-    hipLaunchKernelGGL(bn_act_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(bf16_t, y), ldy, M, C / 4, scale, shift, slope, NSM_CT(bf16_t, res),
-                       ldres, NSM_T(bf16_t, out), ldo);
+    hipLaunchKernelGGL(bn_act_kernel<bf16_t>, g, b, 0, as_stream(stream), NSM_CT(bf16_t, y), ldy,
+                       M, C / 8, fh, scale, shift, slope, mask, NSM_CT(bf16_t, res), ldres,
+                       NSM_T(bf16_t, out), ldo);
   else
-    hipLaunchKernelGGL(bn_act_kernel<float>, g, dim3(256), 0, as_stream(stream), NSM_CT(float, y),
-                       ldy, M, C / 4, scale, shift, slope, NSM_CT(float, res), ldres,
+    hipLaunchKernelGGL(bn_act_kernel<float>, g, b, 0, as_stream(stream), NSM_CT(float, y), ldy, M,
+                       C / 8, fh, scale, shift, slope, mask, NSM_CT(float, res), ldres,
                        NSM_T(float, out), ldo);
   NSM_LAUNCH_CHECK("bn_act");
   return 0;
@@ -1040,8 +1151,8 @@ extern "C" int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy,
                                  int HW, const float* scale, const float* shift, float slope,
                                  const float* mask, const float* mean, const float* invstd,
                                  float* partial, int nchunk, int dtype, void* stream) {
-  NSM_CHECK_ARG(g && y && scale && shift && mean && invstd && partial && C % 4 == 0,
-                "bn_bwd_reduce: bad args");
+  NSM_CHECK_ARG(g && y && scale && shift && mean && invstd && partial && C % 8 == 0 &&
+                    ldg % 8 == 0 && ldy % 8 == 0, "bn_bwd_reduce: bad args");
   ColRed r = colred_plan(M, C);
   NSM_CHECK_ARG(nchunk == r.nchunk, "bn_bwd_reduce: nchunk mismatch");
   dim3 gr(r.gx, r.nchunk);
@@ -1072,17 +1183,21 @@ extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, 
                                 int HW, const float* scale, const float* shift, float slope,
                                 const float* mask, const float* mean, const float* coef, void* dy,
                                 int lddy, int dtype, void* stream) {
-  NSM_CHECK_ARG(g && y && scale && shift && mean && coef && dy && C % 4 == 0,
+  NSM_CHECK_ARG(g && y && scale && shift && mean && coef && dy && C % 8 == 0 && C <= 2048 &&
+                    ldg % 8 == 0 && ldy % 8 == 0 && lddy % 8 == 0 && (!mask || HW > 0),
                 "bn_bwd_apply: bad args");
-  long long work = (long long)M * (C / 4);
-  dim3 gr(grid_for(work));
+  NSM_CHECK_ARG(M >= 0 && M < (1 << 30), "bn_bwd_apply: too large");
+  if (M == 0) return 0;
+  dim3 gr, b;
+  pix_launch(M, C / 8, gr, b);
+  const FastDiv fh = make_fastdiv(mask ? HW : 1);
   if (dtype == NSM_BF16)
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, gr, dim3(256), 0, as_stream(stream),
-                       NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, make_fastdiv(HW),
-                       scale, shift, slope, mask, mean, coef, NSM_T(bf16_t, dy), lddy);
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, gr, b, 0, as_stream(stream),
+                       NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, C / 8, fh, scale,
+                       shift, slope, mask, mean, coef, NSM_T(bf16_t, dy), lddy);
   else
-    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, gr, dim3(256), 0, as_stream(stream),
-                       NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, make_fastdiv(HW), scale,
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, gr, b, 0, as_stream(stream),
+                       NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, C / 8, fh, scale,
                        shift, slope, mask, mean, coef, NSM_T(float, dy), lddy);
   NSM_LAUNCH_CHECK("bn_bwd_apply");
   return 0;
@@ -1090,52 +1205,68 @@ extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, 
 
 extern "C" int nsm_avgpool2_fwd(const void* x, int B, int H, int W, int C, void* y, int dtype,
                                 void* stream) {
-  NSM_CHECK_ARG(x && y && C % 4 == 0 && H >= 2 && W >= 2, "avgpool2_fwd: bad args");
-  long long work = (long long)B * (H / 2) * (W / 2) * (C / 4);
+  NSM_CHECK_ARG(x && y && C % 8 == 0 && H >= 2 && W >= 2, "avgpool2_fwd: bad args");
+  long long work = (long long)B * (H / 2) * (W / 2) * (C / 8);
+  NSM_CHECK_ARG(work < (1ll << 31), "avgpool2_fwd: too large");
   dim3 g(grid_for(work));
+  const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(W / 2), fh = make_fastdiv(H / 2);
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(avgpool2_fwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(bf16_t, x), B, H, W, C / 4, NSM_T(bf16_t, y));
+                       NSM_CT(bf16_t, x), B, H, W, C / 8, f8, fw, fh, NSM_T(bf16_t, y));
   else
     hipLaunchKernelGGL(avgpool2_fwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(float, x), B, H, W, C / 4, NSM_T(float, y));
+                       NSM_CT(float, x), B, H, W, C / 8, f8, fw, fh, NSM_T(float, y));
   NSM_LAUNCH_CHECK("avgpool2_fwd");
   return 0;
 }
 
 extern "C" int nsm_avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, const void* skip,
                                     void* dx, int dtype, void* stream) {
-  NSM_CHECK_ARG(dy && dx && C % 4 == 0, "avgpool2_bwd: bad args");
-  long long work = (long long)B * H * W * (C / 4);
+  NSM_CHECK_ARG(dy && dx && C % 8 == 0, "avgpool2_bwd: bad args");
+  long long work = (long long)B * H * W * (C / 8);
+  NSM_CHECK_ARG(work < (1ll << 31), "avgpool2_bwd: too large");
   dim3 g(grid_for(work));
+  const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(W), fh = make_fastdiv(H);
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(avgpool2_bwd_add_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(bf16_t, dy), B, H, W, C / 4, NSM_CT(bf16_t, skip), NSM_T(bf16_t, dx));
+                       NSM_CT(bf16_t, dy), B, H, W, C / 8, f8, fw, fh, NSM_CT(bf16_t, skip),
+                       NSM_T(bf16_t, dx));
   else
     hipLaunchKernelGGL(avgpool2_bwd_add_kernel<float>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(float, dy), B, H, W, C / 4, NSM_CT(float, skip), NSM_T(float, dx));
+                       NSM_CT(float, dy), B, H, W, C / 8, f8, fw, fh, NSM_CT(float, skip),
+                       NSM_T(float, dx));
   NSM_LAUNCH_CHECK("avgpool2_bwd");
   return 0;
 }
+
+// 8-channel path when C % 8 == 0 (all model activations), scalar otherwise
+#define NSM_DT(KER, ...)                                                        \
+  do {                                                                          \
+    if (dtype == NSM_BF16)                                                      \
+      hipLaunchKernelGGL(KER<bf16_t>, g, dim3(256), 0, s, __VA_ARGS__(bf16_t)); \
+    else                                                                        \
+      hipLaunchKernelGGL(KER<float>, g, dim3(256), 0, s, __VA_ARGS__(float));   \
+  } while (0)
 
 extern "C" int nsm_resize_fwd(const void* x, int B, int Hi, int Wi, int C, void* y, int Ho, int Wo,
                               int dtype, void* stream) {
   NSM_CHECK_ARG(x && y && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0,
                 "resize_fwd: bad args");
-  float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
-  bool vec = C % 4 == 0;
-  long long work = (long long)B * Ho * Wo * (vec ? C / 4 : C);
-  dim3 g(grid_for(work));
+  const float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
   hipStream_t s = as_stream(stream);
-#define NSM_RF(V, T)                                                                          \
-  hipLaunchKernelGGL((resize_fwd_kernel<V, T>), g, dim3(256), 0, s, NSM_CT(T, x), B, Hi, Wi, C, \
-                     NSM_T(T, y), Ho, Wo, sh, sw)
-  if (dtype == NSM_BF16) {
-    if (vec) NSM_RF(true, bf16_t); else NSM_RF(false, bf16_t);
+  const long long tot8 = (long long)B * Ho * Wo * (C / 8);
+  if (C % 8 == 0 && tot8 < (1ll << 31)) {
+    dim3 g(grid_for(tot8, 256, 2048));
+    const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(Wo), fh = make_fastdiv(Ho);
+#define A_(T) NSM_CT(T, x), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, y), Ho, Wo, sh, sw
+    NSM_DT(resize_fwd8_kernel, A_);
+#undef A_
   } else {
-    if (vec) NSM_RF(true, float); else NSM_RF(false, float);
+    dim3 g(grid_for((long long)B * Ho * Wo * C));
+#define A_(T) NSM_CT(T, x), B, Hi, Wi, C, NSM_T(T, y), Ho, Wo, sh, sw
+    NSM_DT(resize_fwd1_kernel, A_);
+#undef A_
   }
-#undef NSM_RF
   NSM_LAUNCH_CHECK("resize_fwd");
   return 0;
 }
@@ -1144,63 +1275,61 @@ extern "C" int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void
                               int dtype, void* stream) {
   NSM_CHECK_ARG(dy && dx && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0,
                 "resize_bwd: bad args");
-  float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
-  // the gather visits at most 16 candidate columns per input column
-  NSM_CHECK_ARG(sw == 0.f || (2.f / sw + 4.f) < 16.f, "resize_bwd: scale too small");
-  bool vec = C % 4 == 0;
-  long long work = (long long)B * Hi * Wi * (vec ? C / 4 : C);
-  dim3 g(grid_for(work));
+  const float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
   hipStream_t s = as_stream(stream);
-#define NSM_RB(V, T)                                                                           \
-  hipLaunchKernelGGL((resize_bwd_kernel<V, T>), g, dim3(256), 0, s, NSM_CT(T, dy), B, Hi, Wi, C, \
-                     NSM_T(T, dx), Ho, Wo, sh, sw)
-  if (dtype == NSM_BF16) {
-    if (vec) NSM_RB(true, bf16_t); else NSM_RB(false, bf16_t);
+  const long long tot8 = (long long)B * Hi * Wi * (C / 8);
+  if (C % 8 == 0 && tot8 < (1ll << 31)) {
+    dim3 g(grid_for(tot8, 256, 2048));
+    const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(Wi), fh = make_fastdiv(Hi);
+#define A_(T) NSM_CT(T, dy), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), Ho, Wo, sh, sw
+    NSM_DT(resize_bwd8_kernel, A_);
+#undef A_
   } else {
-    if (vec) NSM_RB(true, float); else NSM_RB(false, float);
+    dim3 g(grid_for((long long)B * Hi * Wi * C));
+#define A_(T) NSM_CT(T, dy), B, Hi, Wi, C, NSM_T(T, dx), Ho, Wo, sh, sw
+    NSM_DT(resize_bwd1_kernel, A_);
+#undef A_
   }
-#undef NSM_RB
   NSM_LAUNCH_CHECK("resize_bwd");
   return 0;
 }
 
 extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, void* y, int th,
                                   int tw, int dtype, void* stream) {
-  NSM_CHECK_ARG(x && y && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 4 == 0,
+  NSM_CHECK_ARG(x && y && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 8 == 0,
                 "up2_resize_fwd: bad args");
-  long long work = (long long)B * th * tw * (C / 4);
-  dim3 g(grid_for(work));
+  const long long tot8 = (long long)B * th * tw * (C / 8);
+  NSM_CHECK_ARG(tot8 < (1ll << 31), "up2_resize_fwd: too large");
+  hipStream_t s = as_stream(stream);
+  dim3 g(grid_for(tot8, 256, 2048));
   const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
               d = ac_scale(2 * w, tw);
-  if (dtype == NSM_BF16)
-    hipLaunchKernelGGL(up2_resize_fwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(bf16_t, x), B, h, w, C, NSM_T(bf16_t, y), th, tw, a, b, c, d);
-  else
-    hipLaunchKernelGGL(up2_resize_fwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(float, x), B, h, w, C, NSM_T(float, y), th, tw, a, b, c, d);
+  const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(tw), fh = make_fastdiv(th);
+#define A_(T) NSM_CT(T, x), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, y), th, tw, a, b, c, d
+  NSM_DT(up2_resize_fwd8_kernel, A_);
+#undef A_
   NSM_LAUNCH_CHECK("up2_resize_fwd");
   return 0;
 }
 
 extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th,
                                   int tw, int dtype, void* stream) {
-  NSM_CHECK_ARG(dy && dx && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 4 == 0,
+  NSM_CHECK_ARG(dy && dx && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 8 == 0,
                 "up2_resize_bwd: bad args");
-  // the combined-weight gather assumes a downsizing second step of at most ~2x
-  NSM_CHECK_ARG(th * 3 >= 2 * h && tw * 3 >= 2 * w, "up2_resize_bwd: target too small");
-  long long work = (long long)B * h * w * (C / 4);
-  dim3 g(grid_for(work));
+  const long long tot8 = (long long)B * h * w * (C / 8);
+  NSM_CHECK_ARG(tot8 < (1ll << 31), "up2_resize_bwd: too large");
+  hipStream_t s = as_stream(stream);
+  dim3 g(grid_for(tot8, 256, 2048));
   const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
               d = ac_scale(2 * w, tw);
-  if (dtype == NSM_BF16)
-    hipLaunchKernelGGL(up2_resize_bwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(bf16_t, dy), B, h, w, C, NSM_T(bf16_t, dx), th, tw, a, b, c, d);
-  else
-    hipLaunchKernelGGL(up2_resize_bwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(float, dy), B, h, w, C, NSM_T(float, dx), th, tw, a, b, c, d);
+  const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(w), fh = make_fastdiv(h);
+#define A_(T) NSM_CT(T, dy), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), th, tw, a, b, c, d
+  NSM_DT(up2_resize_bwd8_kernel, A_);
+#undef A_
   NSM_LAUNCH_CHECK("up2_resize_bwd");
   return 0;
 }
+#undef NSM_DT
 
 extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, void* out, int cp,
                               int dtype, void* stream) {

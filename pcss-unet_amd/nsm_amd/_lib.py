@@ -43,7 +43,7 @@ _SIGS = {
     "nsm_bn_finalize_train": (I, [P, I, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P]),
     "nsm_bn_partials_merge": (I, [P, I, I, I, I, I, P, P]),
     "nsm_bn_finalize_eval": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
-    "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, I, P]),
+    "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, P, I, I, P]),
     "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
     "nsm_bn_bwd_finalize": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
     "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),

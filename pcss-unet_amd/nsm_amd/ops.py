@@ -295,12 +295,15 @@ def bn_eval(bn_mod, C, c_real, eps, device):
     return st
 
 
-def bn_act(y, st, slope=0.2, res=None, out=None):
+def bn_act(y, st, slope=0.2, res=None, out=None, mask=None, HW=0):
+    """lrelu(y*scale+shift) (* mask[b, c] with b = row // HW) (+ res)."""
     M, C = y.shape
     o = out if out is not None else like(M, C, y)
     assert res is None or res.dtype == y.dtype
-    call("nsm_bn_act", ptr(y), y.stride(0), M, C, ptr(st.scale), ptr(st.shift), slope, ptr(res),
-         res.stride(0) if res is not None else 0, ptr(o), o.stride(0), dt(y), stream())
+    assert mask is None or HW > 0
+    call("nsm_bn_act", ptr(y), y.stride(0), M, C, ptr(st.scale), ptr(st.shift), slope, ptr(mask),
+         HW, ptr(res), res.stride(0) if res is not None else 0, ptr(o), o.stride(0), dt(y),
+         stream())
     return o
 
 
