@@ -34,6 +34,11 @@ SLOPE = 0.2
 WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "128"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
 WINO_TILE = int(os.environ.get("NSM_WINO_TILE", "4"))
+# bf16: materialise the activated 3x3 output A1 = lrelu(BN(Y1))*mask once (one
+# streaming pass) so the 1x1 conv and its weight gradient run prologue-free on
+# the LDS-DMA GEMMs, instead of re-applying BN+LReLU+mask in both operand
+# loaders; NSM_BF16_ACT=0 keeps the fused-prologue path.
+BF16_MATERIALIZE_ACT = os.environ.get("NSM_BF16_ACT", "1") != "0"
 ENCODER = (2, 3, 4, 5)
 DECODER = (6, 7, 8, 9)
 SKIP_OF = {6: 4, 7: 3, 8: 2}          # merge_k = conv_k(...) + c_skip  (Unetmodel.py:125,131,137)
@@ -161,7 +166,7 @@ def _masks_for(mod, B, device, training):
 
 
 class _BlockSaved:
-    __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop", "V")
+    __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop", "V", "A1")
 
 
 def _block_fwd(blk, X, B, H, W, training, mask, name=""):
@@ -188,8 +193,15 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
         bn1 = ops.bn_eval(bn1m, cip, ci, eps1, X.device)
     w2 = ops.pack_conv_weight(c4.weight.detach(), cop, cip, ops.PACK_FWD, dtype)
     b2 = ops.pad_vec(c4.bias.detach(), cop)
-    Y2, part2 = ops.conv_fwd_bn(Y1, B, H, W, w2, b2, cop, 1, pro=(bn1.scale, bn1.shift, mask),
-                             tag=name + ".conv.4.fwd", stats=training)
+    A1 = None
+    if dtype == torch.bfloat16 and BF16_MATERIALIZE_ACT:
+        # the same fp32 arithmetic and bf16 rounding as the fused operand prologue
+        A1 = ops.bn_act(Y1, bn1, SLOPE, mask=mask, HW=H * W)
+        Y2, part2 = ops.conv_fwd_bn(A1, B, H, W, w2, b2, cop, 1, tag=name + ".conv.4.fwd",
+                                    stats=training)
+    else:
+        Y2, part2 = ops.conv_fwd_bn(Y1, B, H, W, w2, b2, cop, 1, pro=(bn1.scale, bn1.shift, mask),
+                                    tag=name + ".conv.4.fwd", stats=training)
     if training:
         bn2 = ops.bn_train(Y2, bn2m, co, bn2m.momentum, eps2, part=part2)
     else:
@@ -198,6 +210,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     s.X, s.Y1, s.Y2, s.bn1, s.bn2, s.mask = X, Y1, Y2, bn1, bn2, mask
     s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
     s.V = V if training else None  # Winograd-domain input, reused by the weight gradient
+    s.A1 = A1 if training else None  # activated 1x1 operand, reused by its weight gradient
     return s
 
 
@@ -212,8 +225,12 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
     dtype = G.dtype
     w2d = ops.pack_conv_weight(c4.weight.detach(), s.cop, s.cip, ops.PACK_DGRAD, dtype)
     dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
-    ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
-                   pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
+    if s.A1 is not None:
+        ops.conv_wgrad(dY2, s.A1, B, H, W, 1, ci, co, g[c4.weight], tag=name + ".conv.4.wgrad")
+        s.A1 = None
+    else:
+        ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
+                       pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
     dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias], g[c0.bias])
     if s.V is not None:
         ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=WINO_TILE,
