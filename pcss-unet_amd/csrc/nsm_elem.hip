@@ -427,6 +427,15 @@ __device__ __forceinline__ Pix8 pix8(uint32_t i, int C8, int H, int W, const Fas
   return r;
 }
 
+// XCD-local block order for the resampling gathers: consecutive blocks are
+// dispatched round-robin over the 8 XCDs (separate L2s); renumber so each XCD
+// sweeps a contiguous slice of every grid-stride window and the rows its
+// neighbours share stay in its own L2 (grid % 8 == 0, see xcd_grid)
+__device__ __forceinline__ uint32_t xcd_block() {
+  const uint32_t per = gridDim.x >> 3;
+  return (blockIdx.x & 7u) * per + (blockIdx.x >> 3);
+}
+
 // 8 channels (one 16-B bf16 vector / two fp32 vectors) per lane: the model's
 // activations (C % 8 == 0)
 template <typename T>
@@ -436,7 +445,7 @@ __global__ void __launch_bounds__(256) resize_fwd8_kernel(const T* __restrict__ 
                                                           T* __restrict__ y, int Ho, int Wo,
                                                           float sh, float sw) {
   const int C = C8 * 8;
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+  for (uint32_t i = xcd_block() * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     uint32_t p;
     const Pix8 q = pix8(i, C8, Ho, Wo, fdC8, fdWo, fdHo, p);
     int y0, y1, x0, x1;
@@ -508,7 +517,7 @@ __global__ void __launch_bounds__(256) resize_bwd8_kernel(const T* __restrict__ 
                                                           T* __restrict__ dx, int Ho, int Wo,
                                                           float sh, float sw) {
   const int C = C8 * 8;
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+  for (uint32_t i = xcd_block() * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     uint32_t p;
     const Pix8 q = pix8(i, C8, Hi, Wi, fdC8, fdWi, fdHi, p);
     int ylo, yhi, xlo, xhi;
@@ -600,7 +609,7 @@ __global__ void __launch_bounds__(256) up2_resize_fwd8_kernel(const T* __restric
                                                               int th, int tw, float s1h, float s1w,
                                                               float s2h, float s2w) {
   const int C = C8 * 8, h2 = 2 * h, w2 = 2 * w;
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+  for (uint32_t i = xcd_block() * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     uint32_t p;
     const Pix8 q = pix8(i, C8, th, tw, fdC8, fdtw, fdth, p);
     int m0, m1, n0, n1;
@@ -635,7 +644,7 @@ __global__ void __launch_bounds__(256) up2_resize_bwd8_kernel(const T* __restric
                                                               int th, int tw, float s1h, float s1w,
                                                               float s2h, float s2w) {
   const int C = C8 * 8, h2 = 2 * h, w2 = 2 * w;
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+  for (uint32_t i = xcd_block() * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     uint32_t p;
     const Pix8 q = pix8(i, C8, h, w, fdC8, fdw, fdh, p);
     // intermediate rows touching iy, then final rows touching those
@@ -1031,6 +1040,13 @@ __global__ void adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
   }
 }
 
+// grid for the xcd_block() kernels: a multiple of 8 blocks, <= 2048
+static inline int xcd_grid(long long work) {
+  long long g = (work + 255) / 256;
+  g = g > 2048 ? 2048 : g;
+  return (int)((g + 7) / 8 * 8);
+}
+
 static inline int grid_for(long long work, int per_block = 256, int cap = 8192) {
   long long g = (work + per_block - 1) / per_block;
   if (g < 1) g = 1;
@@ -1256,7 +1272,7 @@ extern "C" int nsm_resize_fwd(const void* x, int B, int Hi, int Wi, int C, void*
   hipStream_t s = as_stream(stream);
   const long long tot8 = (long long)B * Ho * Wo * (C / 8);
   if (C % 8 == 0 && tot8 < (1ll << 31)) {
-    dim3 g(grid_for(tot8, 256, 2048));
+    dim3 g(xcd_grid(tot8));
     const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(Wo), fh = make_fastdiv(Ho);
 #define A_(T) NSM_CT(T, x), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, y), Ho, Wo, sh, sw
     NSM_DT(resize_fwd8_kernel, A_);
@@ -1279,7 +1295,7 @@ extern "C" int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void
   hipStream_t s = as_stream(stream);
   const long long tot8 = (long long)B * Hi * Wi * (C / 8);
   if (C % 8 == 0 && tot8 < (1ll << 31)) {
-    dim3 g(grid_for(tot8, 256, 2048));
+    dim3 g(xcd_grid(tot8));
     const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(Wi), fh = make_fastdiv(Hi);
 #define A_(T) NSM_CT(T, dy), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), Ho, Wo, sh, sw
     NSM_DT(resize_bwd8_kernel, A_);
@@ -1301,7 +1317,7 @@ extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, voi
   const long long tot8 = (long long)B * th * tw * (C / 8);
   NSM_CHECK_ARG(tot8 < (1ll << 31), "up2_resize_fwd: too large");
   hipStream_t s = as_stream(stream);
-  dim3 g(grid_for(tot8, 256, 2048));
+  dim3 g(xcd_grid(tot8));
   const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
               d = ac_scale(2 * w, tw);
   const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(tw), fh = make_fastdiv(th);
@@ -1319,7 +1335,7 @@ extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, vo
   const long long tot8 = (long long)B * h * w * (C / 8);
   NSM_CHECK_ARG(tot8 < (1ll << 31), "up2_resize_bwd: too large");
   hipStream_t s = as_stream(stream);
-  dim3 g(grid_for(tot8, 256, 2048));
+  dim3 g(xcd_grid(tot8));
   const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
               d = ac_scale(2 * w, tw);
   const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(w), fh = make_fastdiv(h);
