@@ -34,11 +34,13 @@ SLOPE = 0.2
 WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "128"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
 WINO_TILE = int(os.environ.get("NSM_WINO_TILE", "4"))
-# bf16: materialise the activated 3x3 output A1 = lrelu(BN(Y1))*mask once (one
+# Materialise the activated 3x3 output A1 = lrelu(BN(Y1))*mask once (one
 # streaming pass) so the 1x1 conv and its weight gradient run prologue-free on
 # the LDS-DMA GEMMs, instead of re-applying BN+LReLU+mask in both operand
-# loaders; NSM_BF16_ACT=0 keeps the fused-prologue path.
+# loaders (bf16 +1.3 %, fp32 +1.2 % measured); NSM_BF16_ACT=0 / NSM_F32_ACT=0 keep
+# the fused-prologue path.
 BF16_MATERIALIZE_ACT = os.environ.get("NSM_BF16_ACT", "1") != "0"
+F32_MATERIALIZE_ACT = os.environ.get("NSM_F32_ACT", "1") != "0"
 ENCODER = (2, 3, 4, 5)
 DECODER = (6, 7, 8, 9)
 SKIP_OF = {6: 4, 7: 3, 8: 2}          # merge_k = conv_k(...) + c_skip  (Unetmodel.py:125,131,137)
@@ -194,7 +196,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     w2 = ops.pack_conv_weight(c4.weight.detach(), cop, cip, ops.PACK_FWD, dtype)
     b2 = ops.pad_vec(c4.bias.detach(), cop)
     A1 = None
-    if dtype == torch.bfloat16 and BF16_MATERIALIZE_ACT:
+    if BF16_MATERIALIZE_ACT if dtype == torch.bfloat16 else F32_MATERIALIZE_ACT:
         # the same fp32 arithmetic and bf16 rounding as the fused operand prologue
         A1 = ops.bn_act(Y1, bn1, SLOPE, mask=mask, HW=H * W)
         Y2, part2 = ops.conv_fwd_bn(A1, B, H, W, w2, b2, cop, 1, tag=name + ".conv.4.fwd",
