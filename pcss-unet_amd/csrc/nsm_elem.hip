@@ -505,10 +505,35 @@ __device__ __forceinline__ void cand_range(float scale, int i, int out, int& lo,
   hi = min(out - 1, (int)ceilf((float)(i + 1) / scale) + 1);
 }
 
-// The backward gathers keep the x-axis candidate weights of a lane in a fully
-// unrolled register array (a runtime-indexed one would live in scratch); a
-// wider window (extreme downsizing) takes the on-the-fly loop.
-constexpr int RS_MAXC = 16;
+// The backward gathers: per axis, the candidate window is trimmed to the
+// outputs with a non-zero weight (4-5 for a x2 upsample); the x weights and
+// clamped column indices of a lane sit in fully unrolled register arrays, and
+// each output row's loads are issued together, unconditionally, so a row costs
+// one memory latency (a load under a per-lane branch would wait alone). Zero
+// weights are skipped by select, exactly as a skipped term. Wider windows
+// (strong downsizing) take the plain loop.
+constexpr int RS_W = 6;
+
+template <typename WF>
+__device__ __forceinline__ void trim_range(int& lo, int& hi, WF w) {
+  while (lo < hi && w(lo) == 0.f) ++lo;
+  while (hi > lo && w(hi) == 0.f) --hi;
+}
+
+template <typename T>
+__device__ __forceinline__ void gather_row(F8& acc, const T* __restrict__ row, int C, float wy,
+                                           const float (&wx)[RS_W], const int (&xo)[RS_W]) {
+  F8 v[RS_W];
+#pragma unroll
+  for (int k = 0; k < RS_W; ++k) v[k] = ld8(row + (size_t)xo[k] * C);
+#pragma unroll
+  for (int k = 0; k < RS_W; ++k) {
+    const float w = wy * wx[k];
+    const F8 t = acc + w * v[k];
+    acc.a = wx[k] != 0.f ? t.a : acc.a;
+    acc.b = wx[k] != 0.f ? t.b : acc.b;
+  }
+}
 
 template <typename T>
 __global__ void __launch_bounds__(256) resize_bwd8_kernel(const T* __restrict__ dy, int Hi, int Wi,
@@ -523,19 +548,21 @@ __global__ void __launch_bounds__(256) resize_bwd8_kernel(const T* __restrict__ 
     int ylo, yhi, xlo, xhi;
     cand_range(sh, q.y, Ho, ylo, yhi);
     cand_range(sw, q.x, Wo, xlo, xhi);
+    trim_range(ylo, yhi, [&](int o) { return lin_w(sh, o, Hi, q.y); });
+    trim_range(xlo, xhi, [&](int o) { return lin_w(sw, o, Wi, q.x); });
     const T* base = dy + (size_t)q.b * Ho * Wo * C + q.c;
     F8 acc = f8zero();
-    if (xhi - xlo < RS_MAXC) {
-      float wx[RS_MAXC];
+    if (xhi - xlo < RS_W) {
+      float wx[RS_W];
+      int xo[RS_W];
 #pragma unroll
-      for (int k = 0; k < RS_MAXC; ++k) wx[k] = xlo + k <= xhi ? lin_w(sw, xlo + k, Wi, q.x) : 0.f;
+      for (int k = 0; k < RS_W; ++k) {
+        xo[k] = min(xlo + k, xhi);
+        wx[k] = xlo + k <= xhi ? lin_w(sw, xlo + k, Wi, q.x) : 0.f;
+      }
       for (int oy = ylo; oy <= yhi; ++oy) {
         const float wy = lin_w(sh, oy, Hi, q.y);
-        if (wy == 0.f) continue;
-        const T* row = base + (size_t)oy * Wo * C;
-#pragma unroll
-        for (int k = 0; k < RS_MAXC; ++k)
-          if (wx[k] != 0.f) acc += (wy * wx[k]) * ld8(row + (size_t)(xlo + k) * C);
+        if (wy != 0.f) gather_row(acc, base + (size_t)oy * Wo * C, C, wy, wx, xo);
       }
     } else {
       for (int oy = ylo; oy <= yhi; ++oy) {
@@ -660,20 +687,21 @@ __global__ void __launch_bounds__(256) up2_resize_bwd8_kernel(const T* __restric
     cand_range(s2w, nhi, tw, plo2, phi);
     plo = min(plo, plo2);
     phi = max(phi, phi2);
+    trim_range(olo, ohi, [&](int o) { return comb_w(s2h, o, h2, s1h, h, q.y); });
+    trim_range(plo, phi, [&](int o) { return comb_w(s2w, o, w2, s1w, w, q.x); });
     const T* base = dy + (size_t)q.b * th * tw * C + q.c;
     F8 acc = f8zero();
-    if (phi - plo < RS_MAXC) {
-      float wx[RS_MAXC];
+    if (phi - plo < RS_W) {
+      float wx[RS_W];
+      int xo[RS_W];
 #pragma unroll
-      for (int k = 0; k < RS_MAXC; ++k)
+      for (int k = 0; k < RS_W; ++k) {
+        xo[k] = min(plo + k, phi);
         wx[k] = plo + k <= phi ? comb_w(s2w, plo + k, w2, s1w, w, q.x) : 0.f;
+      }
       for (int oy = olo; oy <= ohi; ++oy) {
         const float wy = comb_w(s2h, oy, h2, s1h, h, q.y);
-        if (wy == 0.f) continue;
-        const T* row = base + (size_t)oy * tw * C;
-#pragma unroll
-        for (int k = 0; k < RS_MAXC; ++k)
-          if (wx[k] != 0.f) acc += (wy * wx[k]) * ld8(row + (size_t)(plo + k) * C);
+        if (wy != 0.f) gather_row(acc, base + (size_t)oy * tw * C, C, wy, wx, xo);
       }
     } else {
       for (int oy = olo; oy <= ohi; ++oy) {
