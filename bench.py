@@ -129,11 +129,11 @@ def mean_ms(evs):
     return float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else float("nan")
 
 
-def load_traffic():
+def load_traffic(name="traffic_wino_gemm_conv6.json"):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
     PMC summary (FETCH_SIZE x2 per the gfx950 calibration + WRITE_SIZE)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic_wino_gemm_conv6.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)))
     if not files:
         return None, None
     with open(files[-1]) as f:
@@ -297,7 +297,9 @@ def run_train(args):
     if bf16:
         work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30)
         roof = direct_roofline(B, H, W, kern_ms, len(evs))
-        roof.update({"traffic": None, "traffic_source": None})
+        traffic, traffic_src = (load_traffic("traffic_conv6_fwd_bf16.json") if B == 64
+                                else (None, None))
+        roof.update({"traffic": traffic, "traffic_source": traffic_src})
     else:
         work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE)
         traffic, traffic_src = load_traffic()
