@@ -299,6 +299,7 @@ struct EpiCtx {
   int wm, wn, lane;
   float* lds;  // the GEMM's LDS array (free after the main loop)
   int mblk;    // M-block index (BN-partial row)
+  int zslab;   // split-K / batch slab of EpiSlab (blockIdx.z unless remapped)
 };
 
 struct EpiStoreP {
@@ -422,7 +423,7 @@ struct EpiSlab {
                                int split) {
     const int col = cx.lane & 31, h = cx.lane >> 5;
     const int mb = cx.mb, nb = cx.nb;
-    float* out = e.ws + (size_t)blockIdx.z * M * N;  // slab per (batch, split)
+    float* out = e.ws + (size_t)cx.zslab * M * N;  // slab per (batch, split)
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
       int n = nb + tn * 32 + col;
@@ -549,7 +550,7 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
     __builtin_amdgcn_sched_group_barrier(0x200, 16, 0);
     __syncthreads();
   }
-  EpiCtx cx{m0, n0, m0 + arb, n0 + brb, wm, wn, lane, lds, (int)blockIdx.x};
+  EpiCtx cx{m0, n0, m0 + arb, n0 + brb, wm, wn, lane, lds, (int)blockIdx.x, (int)blockIdx.z};
   EP::template apply<TM, TN, WM, WN>(ep, acc, cx, M, N, split);
 }
 
