@@ -236,7 +236,7 @@ def bn_partials(y):
     return part
 
 
-MERGE_ABOVE = 256   # partial chunks beyond which a parallel first-level merge runs
+MERGE_ABOVE = 1024  # partial chunks beyond which a parallel first-level merge runs
 
 
 def merged(part, M, C):
