@@ -652,6 +652,66 @@ __global__ void __launch_bounds__(256) up2_resize_fwd8_kernel(const T* __restric
   }
 }
 
+// Row-blocked forward of the composite: one block per output row (b, oy). Per
+// axis the two bilinear steps collapse to at most 3 consecutive input taps
+// (m1 = m0 + 1 and each step spreads by < 1 input), so an output is a 3x3
+// stencil: 9 loads instead of the 16 of evaluating the 4 intermediate samples.
+// The taps and combined weights of every column live in LDS, the row's in
+// registers (fp32 combination: within an ulp of the two-step rounding).
+__device__ __forceinline__ int comb3(float s2, int o, int n2, float s1, int n1, float* wk) {
+  int m0, m1, i00, i01, i10, i11;
+  float l0, l1, a00, a01, a10, a11;
+  lin_idx(s2, o, n2, m0, m1, l0, l1);
+  lin_idx(s1, m0, n1, i00, i01, a00, a01);
+  lin_idx(s1, m1, n1, i10, i11, a10, a11);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    const int i = i00 + k;
+    wk[k] = l0 * ((i00 == i ? a00 : 0.f) + (i01 == i ? a01 : 0.f)) +
+            l1 * ((i10 == i ? a10 : 0.f) + (i11 == i ? a11 : 0.f));
+  }
+  return i00;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) up2_resize_fwd_rows_kernel(
+    const T* __restrict__ x, int h, int w, int C8, FastDiv fdC8, T* __restrict__ y, int th, int tw,
+    float s1h, float s1w, float s2h, float s2w) {
+  extern __shared__ float u2f_tables[];  // [tw][3] weights, [tw] first tap
+  float* xw = u2f_tables;
+  int* xb = (int*)(u2f_tables + (size_t)tw * 3);
+  const int C = C8 * 8;
+  const int b = blockIdx.x / th, oy = blockIdx.x - b * th;
+  for (int ox = threadIdx.x; ox < tw; ox += blockDim.x) xb[ox] = comb3(s2w, ox, 2 * w, s1w, w, xw + ox * 3);
+  float wy[3];
+  const int yb = comb3(s2h, oy, 2 * h, s1h, h, wy);
+  __syncthreads();
+  const T* rows[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) rows[a] = x + ((size_t)b * h + min(yb + a, h - 1)) * w * C;
+  T* orow = y + ((size_t)b * th + oy) * tw * C;
+  const uint32_t items = (uint32_t)tw * (uint32_t)C8;
+  for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+    const int ox = (int)fdiv(it, fdC8);
+    const int c = (int)(it - (uint32_t)ox * (uint32_t)C8) * 8;
+    const int x0 = xb[ox];
+    const float wx0 = xw[ox * 3], wx1 = xw[ox * 3 + 1], wx2 = xw[ox * 3 + 2];
+    const int c0 = x0 * C + c, c1 = min(x0 + 1, w - 1) * C + c, c2 = min(x0 + 2, w - 1) * C + c;
+    F8 v[9];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      v[3 * a] = ld8(rows[a] + c0);
+      v[3 * a + 1] = ld8(rows[a] + c1);
+      v[3 * a + 2] = ld8(rows[a] + c2);
+    }
+    F8 acc = f8zero();
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+      acc += wy[a] * (wx0 * v[3 * a] + wx1 * v[3 * a + 1] + wx2 * v[3 * a + 2]);
+    st8(orow + (size_t)ox * C + c, acc);
+  }
+}
+
 // combined 1-D weight of final output index o on input index i
 __device__ __forceinline__ float comb_w(float s2, int o, int n2, float s1, int n1, int i) {
   int m0, m1;
@@ -715,6 +775,88 @@ __global__ void __launch_bounds__(256) up2_resize_bwd8_kernel(const T* __restric
       }
     }
     st8(dx + (size_t)p * C + q.c, acc);
+  }
+}
+
+// Row-blocked form of the composite backward: one block per input row (b, iy).
+// The x-axis windows and combined weights of every column are built once per
+// block into LDS (the per-element form recomputes ~25 composite weights per
+// lane: ALU-bound), the row's y window once; the lanes then only gather.
+constexpr int U2_MAXW = 2048;  // widest row the LDS tables hold
+
+template <typename T>
+__global__ void __launch_bounds__(256) up2_resize_bwd_rows_kernel(
+    const T* __restrict__ dy, int h, int w, int C8, FastDiv fdC8, T* __restrict__ dx, int th,
+    int tw, float s1h, float s1w, float s2h, float s2w) {
+  extern __shared__ float u2_tables[];  // [w][RS_W] weights, [w] window starts, [w] widths
+  float* xw = u2_tables;
+  int* xlo = (int*)(u2_tables + (size_t)w * RS_W);
+  int* xn = xlo + w;
+  __shared__ float yw[RS_W];
+  __shared__ int ywin[2];
+  const int C = C8 * 8, h2 = 2 * h, w2 = 2 * w;
+  const int b = blockIdx.x / h, iy = blockIdx.x - b * h;
+  for (int ix = threadIdx.x; ix < w; ix += blockDim.x) {
+    int nlo, nhi, plo, phi, plo2, phi2;
+    cand_range(s1w, ix, w2, nlo, nhi);
+    cand_range(s2w, nlo, tw, plo, phi2);
+    cand_range(s2w, nhi, tw, plo2, phi);
+    plo = min(plo, plo2);
+    phi = max(phi, phi2);
+    trim_range(plo, phi, [&](int o) { return comb_w(s2w, o, w2, s1w, w, ix); });
+    xlo[ix] = plo;
+    xn[ix] = phi - plo + 1;
+#pragma unroll
+    for (int k = 0; k < RS_W; ++k)
+      xw[ix * RS_W + k] = plo + k <= phi ? comb_w(s2w, plo + k, w2, s1w, w, ix) : 0.f;
+  }
+  if (threadIdx.x == 0) {
+    int mlo, mhi, olo, ohi, olo2, ohi2;
+    cand_range(s1h, iy, h2, mlo, mhi);
+    cand_range(s2h, mlo, th, olo, ohi2);
+    cand_range(s2h, mhi, th, olo2, ohi);
+    olo = min(olo, olo2);
+    ohi = max(ohi, ohi2);
+    trim_range(olo, ohi, [&](int o) { return comb_w(s2h, o, h2, s1h, h, iy); });
+    ywin[0] = olo;
+    ywin[1] = ohi;
+#pragma unroll
+    for (int k = 0; k < RS_W; ++k) yw[k] = olo + k <= ohi ? comb_w(s2h, olo + k, h2, s1h, h, iy) : 0.f;
+  }
+  __syncthreads();
+  const int olo = ywin[0], ohi = ywin[1];
+  const T* base = dy + (size_t)b * th * tw * C;
+  T* orow = dx + ((size_t)b * h + iy) * w * C;
+  const uint32_t items = (uint32_t)w * (uint32_t)C8;
+  for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+    const int ix = (int)fdiv(it, fdC8);
+    const int c = (int)(it - (uint32_t)ix * (uint32_t)C8) * 8;
+    const int plo = xlo[ix], n = xn[ix];
+    F8 acc = f8zero();
+    if (n <= RS_W && ohi - olo < RS_W) {
+      float wx[RS_W];
+      int xo[RS_W];
+#pragma unroll
+      for (int k = 0; k < RS_W; ++k) {
+        wx[k] = xw[ix * RS_W + k];
+        xo[k] = plo + min(k, n - 1);
+      }
+      for (int oy = olo; oy <= ohi; ++oy) {
+        const float wy = yw[oy - olo];
+        if (wy != 0.f) gather_row(acc, base + (size_t)oy * tw * C + c, C, wy, wx, xo);
+      }
+    } else {  // wide windows: weights on the fly, as the per-element kernel
+      for (int oy = olo; oy <= ohi; ++oy) {
+        const float wy = comb_w(s2h, oy, h2, s1h, h, iy);
+        if (wy == 0.f) continue;
+        const T* row = base + (size_t)oy * tw * C + c;
+        for (int ox = plo; ox < plo + n; ++ox) {
+          const float wxk = comb_w(s2w, ox, w2, s1w, w, ix);
+          if (wxk != 0.f) acc += (wy * wxk) * ld8(row + (size_t)ox * C);
+        }
+      }
+    }
+    st8(orow + (size_t)ix * C + c, acc);
   }
 }
 
@@ -1349,9 +1491,22 @@ extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, voi
   const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
               d = ac_scale(2 * w, tw);
   const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(tw), fh = make_fastdiv(th);
-#define A_(T) NSM_CT(T, x), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, y), th, tw, a, b, c, d
-  NSM_DT(up2_resize_fwd8_kernel, A_);
+  if (tw <= U2_MAXW && (long long)B * th < (1ll << 31) && th * 2 >= 2 * h - 1 && tw * 2 >= 2 * w - 1) {
+    // second step downsizes (or keeps) the x2 grid: the 3-tap collapse holds
+    const size_t lds = (size_t)tw * 4 * 4;
+#define A_(T) NSM_CT(T, x), h, w, C / 8, f8, NSM_T(T, y), th, tw, a, b, c, d
+    if (dtype == NSM_BF16)
+      hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<bf16_t>, dim3((unsigned)(B * th)), dim3(256),
+                         lds, s, A_(bf16_t));
+    else
+      hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<float>, dim3((unsigned)(B * th)), dim3(256),
+                         lds, s, A_(float));
 #undef A_
+  } else {
+#define A_(T) NSM_CT(T, x), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, y), th, tw, a, b, c, d
+    NSM_DT(up2_resize_fwd8_kernel, A_);
+#undef A_
+  }
   NSM_LAUNCH_CHECK("up2_resize_fwd");
   return 0;
 }
@@ -1367,9 +1522,21 @@ extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, vo
   const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
               d = ac_scale(2 * w, tw);
   const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(w), fh = make_fastdiv(h);
-#define A_(T) NSM_CT(T, dy), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), th, tw, a, b, c, d
-  NSM_DT(up2_resize_bwd8_kernel, A_);
+  if (w <= U2_MAXW && (long long)B * h < (1ll << 31)) {
+    const size_t lds = (size_t)w * (RS_W + 2) * 4;
+#define A_(T) NSM_CT(T, dy), h, w, C / 8, f8, NSM_T(T, dx), th, tw, a, b, c, d
+    if (dtype == NSM_BF16)
+      hipLaunchKernelGGL(up2_resize_bwd_rows_kernel<bf16_t>, dim3((unsigned)(B * h)), dim3(256),
+                         lds, s, A_(bf16_t));
+    else
+      hipLaunchKernelGGL(up2_resize_bwd_rows_kernel<float>, dim3((unsigned)(B * h)), dim3(256),
+                         lds, s, A_(float));
 #undef A_
+  } else {
+#define A_(T) NSM_CT(T, dy), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), th, tw, a, b, c, d
+    NSM_DT(up2_resize_bwd8_kernel, A_);
+#undef A_
+  }
   NSM_LAUNCH_CHECK("up2_resize_bwd");
   return 0;
 }
