@@ -611,9 +611,11 @@ __global__ void resize_bwd1_kernel(const T* __restrict__ dy, int B, int Hi, int 
 // ---------------------------------------------------------------------------
 // Composite: nn.Upsample(x2) to (2h,2w) followed by _upsample_and_match to
 // (th,tw) (Unetmodel.py:140-141, the up9 "blur"), without materialising the
-// 4x intermediate. Forward evaluates the up-sampled values exactly as the
-// two-step path rounds them (fp32 per intermediate sample); backward uses the
-// separable combined weights W[o->i] = sum_m w2(o->m) w1(m->i).
+// 4x intermediate. The row-blocked forward (used for rows up to U2_MAXW)
+// applies the separable combined weights as a 3x3 stencil; the per-element
+// fallback evaluates the intermediate samples as the two-step path rounds
+// them (fp32 per sample). Backward uses the combined weights
+// W[o->i] = sum_m w2(o->m) w1(m->i).
 // ---------------------------------------------------------------------------
 template <typename T>
 __device__ __forceinline__ F8 up_sample8(const T* __restrict__ x, size_t rb, int h, int w, int C,
