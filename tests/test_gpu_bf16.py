@@ -36,7 +36,9 @@ def bf_close(got, ref, ulps=2.0):
                                            (4, 32, 32, 256, 256, 3),
                                            # >= 1024 blocks of 256 rows: the LDS-DMA kernel
                                            (4, 128, 128, 64, 512, 3), (3, 97, 93, 64, 1280, 3),
-                                           (1, 128, 256, 128, 1024, 3)])
+                                           (1, 128, 256, 128, 1024, 3),
+                                           # 256x64 LDS-DMA tiles (64-channel layers), 3x3 and 1x1
+                                           (4, 256, 256, 64, 64, 3), (4, 256, 255, 128, 64, 1)])
 def test_conv_fwd_bf16(ops, device, B, H, W, ci, co, k):
     g = torch.Generator().manual_seed(B * 1000 + H * 10 + ci + co + k)
     x = r(torch.randn(B, ci, H, W, generator=g))
@@ -95,7 +97,12 @@ def test_conv_dgrad_bf16(ops, device, B, H, W, ci, co, k):
                                                (4, 64, 64, 64, 64, 3, False),
                                                (2, 12, 10, 128, 512, 3, False),
                                                (2, 16, 16, 256, 256, 3, False),
-                                               (3, 45, 43, 128, 128, 3, False)])
+                                               (3, 45, 43, 128, 128, 3, False),
+                                               # multi-tap N tiles (Cin 64: 4 taps, 128: 3 taps)
+                                               (2, 37, 41, 64, 64, 3, False),
+                                               # prologue-free 1x1 on the DMA tiles
+                                               (2, 16, 16, 128, 256, 1, False),
+                                               (2, 20, 20, 512, 1024, 1, False)])
 def test_conv_wgrad_bf16(ops, device, B, H, W, ci, co, k, pro):
     g = torch.Generator().manual_seed(13)
     x = r(torch.randn(B, ci, H, W, generator=g))
