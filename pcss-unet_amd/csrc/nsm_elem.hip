@@ -866,25 +866,31 @@ __global__ void __launch_bounds__(256) up2_resize_bwd_rows_kernel(
 // Model boundary: pixel_unshuffle(2) + NCHW->NHWC (+ zero channel pad), and its
 // inverse for the input gradient.
 // ---------------------------------------------------------------------------
+// thread per output pixel: each group of 8 output channels = 2 input planes x
+// 2 rows x 2 columns (channel 4c + 2i + j, F.pixel_unshuffle), read as float2
+// pairs coalesced along x and written as one 16-B (bf16) / 32-B (fp32) vector
 template <typename T>
-__global__ void input_prep_kernel(const float* __restrict__ x, int B, int C, int H, int W,
-                                  T* __restrict__ out, int cp) {
+__global__ void __launch_bounds__(256) input_prep_kernel(const float* __restrict__ x, int B, int C,
+                                                         int H, int W, T* __restrict__ out, int cp,
+                                                         uint32_t npix, FastDiv fdRw, FastDiv fdRh) {
   const int Rh = H / 2, Rw = W / 2;
-  long long total = (long long)B * Rh * Rw * cp;
-  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  for (; i < total; i += (long long)gridDim.x * blockDim.x) {
-    int ch = (int)(i % cp);
-    long long t = i / cp;
-    int rx = (int)(t % Rw);
-    t /= Rw;
-    int ry = (int)(t % Rh);
-    int b = (int)(t / Rh);
-    float v = 0.f;
-    if (ch < 4 * C) {
-      int c = ch >> 2, di = (ch >> 1) & 1, dj = ch & 1;
-      v = x[(((size_t)b * C + c) * H + 2 * ry + di) * W + 2 * rx + dj];
+  const size_t plane = (size_t)H * W;
+  for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < npix; p += gridDim.x * 256u) {
+    const uint32_t t = fdiv(p, fdRw);
+    const int rx = (int)(p - t * (uint32_t)Rw);
+    const uint32_t b = fdiv(t, fdRh);
+    const int ry = (int)(t - b * (uint32_t)Rh);
+    const float* src = x + (size_t)b * C * plane + (size_t)(2 * ry) * W + 2 * rx;
+    for (int g = 0; g < cp / 8; ++g) {
+      f32x2 r[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {  // plane 2g + (q >> 1), row 2ry + (q & 1)
+        const int c = 2 * g + (q >> 1);
+        r[q] = c < C ? *(const f32x2*)(src + (size_t)c * plane + (q & 1) * W) : f32x2{0.f, 0.f};
+      }
+      st8(out + (size_t)p * cp + 8 * g,
+          F8{f32x4{r[0].x, r[0].y, r[1].x, r[1].y}, f32x4{r[2].x, r[2].y, r[3].x, r[3].y}});
     }
-    st1(out + i, v);
   }
 }
 
@@ -1546,15 +1552,19 @@ extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, vo
 
 extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, void* out, int cp,
                               int dtype, void* stream) {
-  NSM_CHECK_ARG(x && out && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C, "input_prep: bad args");
-  long long work = (long long)B * (H / 2) * (W / 2) * cp;
-  dim3 g(grid_for(work));
+  NSM_CHECK_ARG(x && out && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C && cp % 8 == 0,
+                "input_prep: bad args");
+  NSM_CHECK_ARG(((uintptr_t)x % 8) == 0, "input_prep: x must be 8-byte aligned");
+  const long long npix = (long long)B * (H / 2) * (W / 2);
+  NSM_CHECK_ARG(npix < (1ll << 31), "input_prep: too large");
+  dim3 g(grid_for(npix, 256, 2048));
+  const FastDiv fw = make_fastdiv(W / 2), fh = make_fastdiv(H / 2);
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(input_prep_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
-                       NSM_T(bf16_t, out), cp);
+                       NSM_T(bf16_t, out), cp, (uint32_t)npix, fw, fh);
   else
     hipLaunchKernelGGL(input_prep_kernel<float>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
-                       NSM_T(float, out), cp);
+                       NSM_T(float, out), cp, (uint32_t)npix, fw, fh);
   NSM_LAUNCH_CHECK("input_prep");
   return 0;
 }
