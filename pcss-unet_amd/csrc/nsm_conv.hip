@@ -209,13 +209,15 @@ struct PixRowsLoader {  // KM / KN image
     int c4 = tid % C4;
     c4o = c4 * 4;
     krow0 = tid / C4;
-    int tap = 0, c = off;
+    // this thread's column (fixed over K) and, for the shifted operand, its
+    // own tap: an N tile may span several taps when BN > Cin
+    int tap = 0, c = off + c4 * 4;
     if (p.cin > 0) {
-      tap = off / p.cin;
-      c = off - tap * p.cin;
+      tap = c / p.cin;
+      c -= tap * p.cin;
     }
-    col = c + c4 * 4;
-    colok = col < p.ncols && (p.cin == 0 || c + c4 * 4 < p.cin);
+    col = c;
+    colok = col < p.ncols && (p.cin == 0 || tap < p.ksize * p.ksize);
     dy = dx = 0;
     if (SHIFT && p.ksize == 3) {
       dy = tap / 3 - 1;
@@ -637,12 +639,24 @@ struct WgradPlan {
   size_t ws_floats;
 };
 
+// NSM_WGRAD_MULTITAP=0: one tap per weight-gradient N tile (register kernels)
+static bool wgrad_multitap_f32() {
+  static bool v = [] {
+    const char* e = getenv("NSM_WGRAD_MULTITAP");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksize) {
   WgradPlan pl;
   const int M = cout_p, N = ksize * ksize * cin_p;
   const long long K = (long long)B * H * W;
   pl.BM = cout_p >= 128 ? 128 : (cout_p >= 64 ? 64 : 32);
-  pl.BN = cin_p >= 128 ? 128 : (cin_p >= 64 ? 64 : 32);
+  // 3x3 with Cin < 128: N tiles of 128 columns spanning 2 (Cin 64) or 4
+  // (Cin 32) taps: wider waves, the dy operand shared by more columns
+  pl.BN = cin_p >= 128 || (ksize == 3 && wgrad_multitap_f32()) ? 128
+                                                                : (cin_p >= 64 ? 64 : 32);
   long long tiles = (long long)ceil_div(M, pl.BM) * ceil_div(N, pl.BN);
   // ~4096 blocks (8 waves of 2 blocks/CU) keeps the tail under ~6 %; each
   // split keeps >= 8 K-slabs, and the fp32 partial slabs stay <= 512 MB.
@@ -1159,7 +1173,7 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
   NSM_CHECK_ARG(!pro_scale || (pro_shift && ksize == 1), "conv_wgrad: prologue needs 1x1");
   NSM_CHECK_ARG(cin <= cin_p && cout <= cout_p, "conv_wgrad: real dims exceed padded");
   WgradPlan pl = plan_wgrad(B, H, W, cin_p, cout_p, ksize);
-  NSM_CHECK_ARG(cin_p % pl.BN == 0, "conv_wgrad: N tile straddles taps");
+  NSM_CHECK_ARG(cin_p % pl.BN == 0 || pl.BN % cin_p == 0, "conv_wgrad: N tile straddles taps");
   if (ws_floats < pl.ws_floats)
     return fail(NSM_E_WS, "conv_wgrad: workspace %zu < %zu floats", ws_floats, pl.ws_floats);
   const int M = cout_p, N = ksize * ksize * cin_p;
