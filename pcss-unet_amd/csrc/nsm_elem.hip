@@ -862,6 +862,75 @@ __global__ void __launch_bounds__(256) up2_resize_bwd_rows_kernel(
   }
 }
 
+// Row-blocked single-step resize backward (same scheme as the composite's).
+template <typename T>
+__global__ void __launch_bounds__(256) resize_bwd_rows_kernel(
+    const T* __restrict__ dy, int h, int w, int C8, FastDiv fdC8, T* __restrict__ dx, int th,
+    int tw, float sh, float sw) {
+  extern __shared__ float rs_tables[];  // [w][RS_W] weights, [w] window starts, [w] widths
+  float* xw = rs_tables;
+  int* xlo = (int*)(rs_tables + (size_t)w * RS_W);
+  int* xn = xlo + w;
+  __shared__ float yw[RS_W];
+  __shared__ int ywin[2];
+  const int C = C8 * 8;
+  const int b = blockIdx.x / h, iy = blockIdx.x - b * h;
+  for (int ix = threadIdx.x; ix < w; ix += blockDim.x) {
+    int plo, phi;
+    cand_range(sw, ix, tw, plo, phi);
+    trim_range(plo, phi, [&](int o) { return lin_w(sw, o, w, ix); });
+    xlo[ix] = plo;
+    xn[ix] = phi - plo + 1;
+#pragma unroll
+    for (int k = 0; k < RS_W; ++k)
+      xw[ix * RS_W + k] = plo + k <= phi ? lin_w(sw, plo + k, w, ix) : 0.f;
+  }
+  if (threadIdx.x == 0) {
+    int olo, ohi;
+    cand_range(sh, iy, th, olo, ohi);
+    trim_range(olo, ohi, [&](int o) { return lin_w(sh, o, h, iy); });
+    ywin[0] = olo;
+    ywin[1] = ohi;
+#pragma unroll
+    for (int k = 0; k < RS_W; ++k) yw[k] = olo + k <= ohi ? lin_w(sh, olo + k, h, iy) : 0.f;
+  }
+  __syncthreads();
+  const int olo = ywin[0], ohi = ywin[1];
+  const T* base = dy + (size_t)b * th * tw * C;
+  T* orow = dx + ((size_t)b * h + iy) * w * C;
+  const uint32_t items = (uint32_t)w * (uint32_t)C8;
+  for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+    const int ix = (int)fdiv(it, fdC8);
+    const int c = (int)(it - (uint32_t)ix * (uint32_t)C8) * 8;
+    const int plo = xlo[ix], n = xn[ix];
+    F8 acc = f8zero();
+    if (n <= RS_W && ohi - olo < RS_W) {
+      float wx[RS_W];
+      int xo[RS_W];
+#pragma unroll
+      for (int k = 0; k < RS_W; ++k) {
+        wx[k] = xw[ix * RS_W + k];
+        xo[k] = plo + min(k, n - 1);
+      }
+      for (int oy = olo; oy <= ohi; ++oy) {
+        const float wy = yw[oy - olo];
+        if (wy != 0.f) gather_row(acc, base + (size_t)oy * tw * C + c, C, wy, wx, xo);
+      }
+    } else {  // wide windows: weights on the fly, as the per-element kernel
+      for (int oy = olo; oy <= ohi; ++oy) {
+        const float wy = lin_w(sh, oy, h, iy);
+        if (wy == 0.f) continue;
+        const T* row = base + (size_t)oy * tw * C + c;
+        for (int ox = plo; ox < plo + n; ++ox) {
+          const float wxk = lin_w(sw, ox, w, ix);
+          if (wxk != 0.f) acc += (wy * wxk) * ld8(row + (size_t)ox * C);
+        }
+      }
+    }
+    st8(orow + (size_t)ix * C + c, acc);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Model boundary: pixel_unshuffle(2) + NCHW->NHWC (+ zero channel pad), and its
 // inverse for the input gradient.
@@ -1433,6 +1502,15 @@ extern "C" int nsm_avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, 
   return 0;
 }
 
+// NSM_RESIZE_ROWS=0: per-element resize backward instead of the row-blocked one
+static bool rows_resize() {
+  static bool v = [] {
+    const char* e = getenv("NSM_RESIZE_ROWS");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 // 8-channel path when C % 8 == 0 (all model activations), scalar otherwise
 #define NSM_DT(KER, ...)                                                        \
   do {                                                                          \
@@ -1475,9 +1553,21 @@ extern "C" int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void
   if (C % 8 == 0 && tot8 < (1ll << 31)) {
     dim3 g(xcd_grid(tot8));
     const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(Wi), fh = make_fastdiv(Hi);
-#define A_(T) NSM_CT(T, dy), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), Ho, Wo, sh, sw
-    NSM_DT(resize_bwd8_kernel, A_);
+    if (Wi <= U2_MAXW && (long long)B * Hi < (1ll << 31) && rows_resize()) {
+      const size_t lds = (size_t)Wi * (RS_W + 2) * 4;
+#define A_(T) NSM_CT(T, dy), Hi, Wi, C / 8, f8, NSM_T(T, dx), Ho, Wo, sh, sw
+      if (dtype == NSM_BF16)
+        hipLaunchKernelGGL(resize_bwd_rows_kernel<bf16_t>, dim3((unsigned)(B * Hi)), dim3(256), lds,
+                           s, A_(bf16_t));
+      else
+        hipLaunchKernelGGL(resize_bwd_rows_kernel<float>, dim3((unsigned)(B * Hi)), dim3(256), lds,
+                           s, A_(float));
 #undef A_
+    } else {
+#define A_(T) NSM_CT(T, dy), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), Ho, Wo, sh, sw
+      NSM_DT(resize_bwd8_kernel, A_);
+#undef A_
+    }
   } else {
     dim3 g(grid_for((long long)B * Hi * Wi * C));
 #define A_(T) NSM_CT(T, dy), B, Hi, Wi, C, NSM_T(T, dx), Ho, Wo, sh, sw
