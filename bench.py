@@ -273,6 +273,9 @@ def run_train(args):
             nsm_amd.allreduce_grads(model.parameters())
         opt.step()
         opt.zero_grad()
+        # the reference's batch is a fresh tensor every step (setdata.py:325-326),
+        # so its input gradient is written once, never accumulated into an old one
+        x.grad = None
         return loss
 
     for _ in range(args.warmup):
