@@ -346,13 +346,18 @@ struct EpiStore {
   }
   // fused BatchNorm batch statistics of this block's rows (two-pass); also
   // used by the bf16 store epilogue on its rounded values
-  template <int TM, int TN, int WM, int WN>
+  // RPP: rows per partial; a block of WM*TM*32 rows writes (WM*TM*32)/RPP
+  // partial rows, each over its own group of M-waves
+  template <int TM, int TN, int WM, int WN, int RPP = WM * TM * 32>
   __device__ static void stats_only(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M,
                                     int N) {
     const int col = cx.lane & 31, h = cx.lane >> 5;
     constexpr int BN = WN * TN * 32;
+    constexpr int G = (WM * TM * 32) / RPP, WG = WM / G;
+    static_assert(G >= 1 && G * RPP == WM * TM * 32 && WG * G == WM, "partial groups");
     float* red = cx.lds;  // [WM][BN]
-    const int cnt = min(M - cx.m0, WM * TM * 32);
+    const int g = cx.wm / WG, w0 = g * WG;
+    const int cnt = min(M - (cx.m0 + g * RPP), RPP);
     float s[TN];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
@@ -376,7 +381,7 @@ struct EpiStore {
     for (int tn = 0; tn < TN; ++tn) {
       float t = 0.f;
 #pragma unroll
-      for (int w = 0; w < WM; ++w) t += red[w * BN + cx.wn * TN * 32 + tn * 32 + col];
+      for (int w = 0; w < WG; ++w) t += red[(w0 + w) * BN + cx.wn * TN * 32 + tn * 32 + col];
       tot[tn] = t;
       mean[tn] = t / (float)cnt;
     }
@@ -399,15 +404,15 @@ struct EpiStore {
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) red[cx.wm * BN + cx.wn * TN * 32 + tn * 32 + col] = s[tn];
     __syncthreads();
-    if (cx.wm == 0 && h == 0) {
-      float* pr = e.stats + (size_t)cx.mblk * 2 * N;
+    if (cx.wm == w0 && h == 0 && cnt > 0) {
+      float* pr = e.stats + ((size_t)cx.mblk * G + g) * 2 * N;
 #pragma unroll
       for (int tn = 0; tn < TN; ++tn) {
         int n = cx.nb + tn * 32 + col;
         if (n >= N) continue;
         float q = 0.f;
 #pragma unroll
-        for (int w = 0; w < WM; ++w) q += red[w * BN + cx.wn * TN * 32 + tn * 32 + col];
+        for (int w = 0; w < WG; ++w) q += red[(w0 + w) * BN + cx.wn * TN * 32 + tn * 32 + col];
         pr[n] = tot[tn];
         pr[N + n] = q;
       }

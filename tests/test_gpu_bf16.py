@@ -38,7 +38,11 @@ def bf_close(got, ref, ulps=2.0):
                                            (4, 128, 128, 64, 512, 3), (3, 97, 93, 64, 1280, 3),
                                            (1, 128, 256, 128, 1024, 3),
                                            # 256x64 LDS-DMA tiles (64-channel layers), 3x3 and 1x1
-                                           (4, 256, 256, 64, 64, 3), (4, 256, 255, 128, 64, 1)])
+                                           (4, 256, 256, 64, 64, 3), (4, 256, 255, 128, 64, 1),
+                                           # N = 128: 512x128 LDS-DMA tiles, two 256-row
+                                           # BN partials per block (last block ragged)
+                                           (4, 256, 256, 64, 128, 3), (4, 257, 255, 128, 128, 3),
+                                           (4, 256, 256, 512, 128, 1)])
 def test_conv_fwd_bf16(ops, device, B, H, W, ci, co, k):
     g = torch.Generator().manual_seed(B * 1000 + H * 10 + ci + co + k)
     x = r(torch.randn(B, ci, H, W, generator=g))
@@ -52,8 +56,19 @@ def test_conv_fwd_bf16(ops, device, B, H, W, ci, co, k):
     # fused BN partials are taken on the rounded outputs
     yr = y.float().cpu()
     rpc, n = part.rpc, part.nchunk
-    sums = part.buf.view(n, 2, co)[:, 0].cpu().double().sum(0)
-    torch.testing.assert_close(sums, yr.double().sum(0), rtol=1e-4, atol=1e-3)
+    pb = part.buf.view(n, 2, co).cpu().double()
+    torch.testing.assert_close(pb[:, 0].sum(0), yr.double().sum(0), rtol=1e-4, atol=1e-3)
+    # every partial row: sum and centred sum of squares of its own rpc rows
+    M = yr.shape[0]
+    assert n == (M + rpc - 1) // rpc
+    yd = torch.nn.functional.pad(yr.double(), (0, 0, 0, n * rpc - M)).view(n, rpc, co)
+    cnt = torch.clamp(M - torch.arange(n) * rpc, max=rpc).double()[:, None]
+    s1 = yd.sum(1)
+    mu = s1 / cnt
+    valid = (torch.arange(rpc)[None, :] < cnt)[:, :, None]
+    m2 = (((yd - mu[:, None, :]) ** 2) * valid).sum(1)
+    torch.testing.assert_close(pb[:, 0], s1, rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(pb[:, 1], m2, rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.parametrize("B,H,W,ci,co", [(2, 6, 7, 32, 64), (2, 16, 16, 128, 64)])
@@ -74,7 +89,9 @@ def test_conv1x1_prologue_bf16(ops, device, B, H, W, ci, co):
 
 @pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 9, 11, 32, 64, 3), (2, 8, 8, 64, 64, 3),
                                            (2, 12, 12, 64, 128, 1),
-                                           (4, 128, 128, 512, 64, 3), (2, 150, 147, 768, 64, 3)])
+                                           (4, 128, 128, 512, 64, 3), (2, 150, 147, 768, 64, 3),
+                                           # 512x128 tiles (dx has 128 channels)
+                                           (4, 256, 256, 128, 64, 3)])
 def test_conv_dgrad_bf16(ops, device, B, H, W, ci, co, k):
     g = torch.Generator().manual_seed(11)
     x = torch.randn(B, ci, H, W, generator=g, requires_grad=True)
