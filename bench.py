@@ -3,9 +3,11 @@
 step (forward + CustomLoss + backward + grad all-reduce + clip + AdamW) on
 MI355X, data-parallel over N GPUs (one process per GPU, RCCL over xGMI).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    torchrun --nproc-per-node N bench.py --gpus N ...
-    python bench.py --workload infer1080     # configs[4]: 1080p eval fwd, hipGraph
+    python bench.py [--gpus N] [--steps K] [--warmup W]   # N > 1: spawns N ranks itself
+    torchrun --nproc-per-node N bench.py --gpus N ...       # or one rank per GPU via torchrun
+    python bench.py --dtype bf16 --batch 64                 # configs[2]
+    python bench.py --workload infer1080 [--dtype bf16]     # configs[4]: 1080p eval fwd, hipGraph
+    python bench.py --dry-run --gpus 2                      # CPU/gloo launcher check only
 
 Workload (BASELINE.json configs[1]): batch 8 per GPU, 7x512x512 fp32
 synthetic G-buffers (x ~ N(0,1), labels integers(0,256)/255), random-init
@@ -13,10 +15,15 @@ weights of the reference architecture, dropout 0.2 (train mode), inputs
 resident in HBM and requiring grad like the reference's batches
 (setdata.py:325-326). Weak scaling: per-GPU batch fixed as N grows.
 
+Step = forward + 0.9*L1 + backward + RCCL grad all-reduce (N > 1, overlapped
+with the backward) + the reference's whole step tail on the device
+(main.py:287-423: sanitise, per-parameter clips, clip_grad_norm_, AdamW).
+
 Rank 0 prints ONE JSON line with the metric, a roofline object for the
-dominant kernel (the Winograd F(4x4,3x3) batched MFMA GEMM of conv6.conv.0
-forward: 36 x [T=B*16*16, 1024] x [1024, 1024], the largest launch of the
-step) timed with HIP events on its launch stream during the timed steps, a
+dominant convolution (conv6.conv.0 forward, 3x3 1024->1024: Winograd input
+transform + batched MFMA GEMM + output transform, timed as a whole with HIP
+events on its launch stream during the timed steps, priced on SURVEY.md
+§8(d)'s algorithmic FLOPs, with the executed-MFMA fraction beside it), a
 per-stage table, and a CPU baseline (the oracle restatement on the host cores).
 """
 import argparse
@@ -173,27 +180,44 @@ def cpu_baseline(in_ch, H, W, frames=4, reps=5, train=True):
     t = float(np.median(ts))
     what = "train step (fwd+L1+bwd)" if train else "eval forward (no_grad)"
     return {"value": frames / t, "unit": "frames/s", "cores": torch.get_num_threads(),
-            "kind": "port",
+            "affinity_cores": cores, "kind": "port",
             "sample": f"{frames} frame(s) {in_ch}x{H}x{W} fp32 {what}, "
                       f"oracle/unet_ref.py on PyTorch CPU, median of {reps} after 1 warmup, "
                       f"{ts and round(sum(ts), 2)} s timed"}
 
 
-def dominant_roofline(B, H, W, kern_ms, launches, wino_tile):
-    """Roofline object of the Winograd batched GEMM of conv6.conv.0 forward."""
+def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
+    """Roofline object of conv6.conv.0's forward, the largest convolution of the
+    step, timed as a whole (Winograd input transform + batched MFMA GEMM +
+    output transform, HIP events on the launch stream). `achieved`/`frac` are
+    on SURVEY.md §8(d)'s algorithmic basis (direct-convolution FLOPs
+    2*B*h*w*Cin*Cout*9): F(4x4,3x3) issues 4x fewer MFMA products, so frac can
+    exceed 1. `executed_frac` prices the MFMA work actually issued (36 GEMMs of
+    T x 1024 x 1024) against the fp32 MFMA peak; `gemm` is the GEMM launch alone."""
     Rh, Rw = H // 2, W // 2
     m, nb = wino_tile, (wino_tile + 2) ** 2
     h6, w6 = Rh // 4, Rw // 4                     # conv6 runs at (H/8, W/8)
     T6 = B * ((h6 + m - 1) // m) * ((w6 + m - 1) // m)
-    k_flops = nb * 2.0 * T6 * 1024 * 1024
-    k_bytes = nb * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
-    achieved = k_flops / (kern_ms * 1e-3) / 1e12
-    return {"kernel": f"conv6.conv.0.fwd Winograd F({m}x{m},3x3) batched MFMA GEMM "
-                      f"(nsm_wino_gemm: {nb} x M={T6} N=1024 K=1024)",
+    alg_flops = conv_flops(B, h6, w6, 1024, 1024, 3)
+    alg_bytes = (2 * B * h6 * w6 * 1024 + 9 * 1024 * 1024 + 1024) * 4
+    ex_flops = nb * 2.0 * T6 * 1024 * 1024
+    gemm_bytes = nb * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
+    achieved = alg_flops / (conv_ms * 1e-3) / 1e12
+    ex = ex_flops / (conv_ms * 1e-3) / 1e12
+    gx = ex_flops / (gemm_ms * 1e-3) / 1e12
+    return {"kernel": f"conv6.conv.0.fwd 3x3 1024->1024 at {h6}x{w6}, B={B}: Winograd F({m}x{m},3x3) "
+                      f"= nsm_wino_input + nsm_wino_gemm ({nb} x M={T6} N=1024 K=1024) + "
+                      "nsm_wino_output",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-            "avg_launch_ms": round(kern_ms, 4), "launches": launches,
-            "algorithmic_flops_per_launch": k_flops, "algorithmic_bytes_per_launch": k_bytes}
+            "basis": "SURVEY.md §8(d) algorithmic (direct-conv) FLOPs per launch / whole-conv time",
+            "executed_tflops": round(ex, 2), "executed_frac": round(ex / FP32_PEAK_TFLOPS, 4),
+            "avg_launch_ms": round(conv_ms, 4), "launches": launches,
+            "algorithmic_flops_per_launch": alg_flops, "algorithmic_bytes_per_launch": alg_bytes,
+            "executed_flops_per_launch": ex_flops,
+            "gemm": {"avg_launch_ms": round(gemm_ms, 4), "executed_tflops": round(gx, 2),
+                     "executed_frac": round(gx / FP32_PEAK_TFLOPS, 4),
+                     "bytes_per_launch": gemm_bytes}}
 
 
 def direct_roofline(B, H, W, kern_ms, launches):
@@ -211,38 +235,78 @@ def direct_roofline(B, H, W, kern_ms, launches):
             "algorithmic_flops_per_launch": k_flops, "algorithmic_bytes_per_launch": k_bytes}
 
 
-def init_dist():
+def init_dist(args):
+    """One process per GPU: torchrun's env (WORLD_SIZE/RANK/LOCAL_RANK), or the
+    workers bench.py spawned itself for --gpus N. RCCL (`nccl`) on the GPUs;
+    gloo for --dry-run (CPU launcher check)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        if world > 1:
+            dist.init_process_group("gloo")
+        return world, rank, torch.device("cpu")
     if world > 1:
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        assert dist.get_world_size() == args.gpus
     return world, rank, torch.device("cuda", local)
 
 
-def timed(fn, steps, world):
+def _sync(dev):
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+
+
+def timed(fn, steps, world, dev):
     """Barrier + synchronize on both sides, max over ranks."""
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     for _ in range(steps):
         fn()
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], device=torch.device("cuda", torch.cuda.current_device()),
-                         dtype=torch.float64)
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
 
 
+def run_dry(args):
+    """--dry-run: the launcher / rendezvous / timing / JSON plumbing of the
+    train bench on CPU processes over gloo, with a stand-in step (a 1 MiB
+    all-reduce). No GPU is touched; the line says dry_run so it can never pass
+    for a measurement."""
+    world, rank, dev = init_dist(args)
+    buf = torch.ones(1 << 18)
+
+    def step():
+        if world > 1:
+            dist.all_reduce(buf)
+
+    for _ in range(args.warmup):
+        step()
+    elapsed = timed(step, args.steps, world, dev)
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run (launcher check, not a measurement)", "value": 0.0,
+                          "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+                          "dry_run": True, "world_size": world,
+                          "backend": dist.get_backend() if world > 1 else None}), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def run_train(args):
-    world, rank, dev = init_dist()
+    world, rank, dev = init_dist(args)
     import nsm_amd
     from nsm_amd import ops as nops
     from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
@@ -257,10 +321,15 @@ def run_train(args):
         with torch.no_grad():
             for p in model.parameters():
                 dist.broadcast(p, 0)
-        model.overlap_grad_allreduce()   # decoder bucket reduces under the encoder backward
+        # decoder bucket reduces under the encoder backward; rank 0's BN buffers
+        # are broadcast at each forward (DDP semantics)
+        model.data_parallel()
+    # the reference's whole step tail (main.py:287-423) on the device: sanitise,
+    # per-parameter clips, clip_grad_norm_(1.0) (epoch 0 of 200), AdamW
     opt = nsm_amd.FlatAdamW(model.parameters(), lr=7e-4, weight_decay=1e-3, max_grad_norm=1.0,
-                            world_size=world)
-    crit = nsm_amd.CustomLoss(dev, alpha=0.9, vgg_weights="random" if args.vgg else None)
+                            world_size=world, sanitize=True)
+    opt.set_epoch(0, 200)
+    crit = nsm_amd.CustomLoss(dev, alpha=0.9, vgg_weights="random" if args.vgg else False)
     g = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(B, C, H, W, device=dev, generator=g).requires_grad_(True)
     y = (torch.randint(0, 256, (B, 1, H, W), device=dev, generator=g).float() / 255.0)
@@ -284,13 +353,15 @@ def run_train(args):
 
     probe_tag = "conv6.conv.0.fwd"
     nops.PROBES[probe_tag] = []
+    nops.PROBES[probe_tag + ".gemm"] = []
     for st in STAGES:
         nops.PROBES[st + ".fwd"] = []
         nops.PROBES[st + ".bwd"] = []
     nops.PROBES["vgg.fwd"] = []
-    elapsed = timed(step, args.steps, world)
+    elapsed = timed(step, args.steps, world, dev)
     evs = nops.PROBES.pop(probe_tag)
     kern_ms = mean_ms(evs)
+    gemm_ms = mean_ms(nops.PROBES.pop(probe_tag + ".gemm"))
     vgg_evs = nops.PROBES.pop("vgg.fwd")
     times = {}
     for st in STAGES:
@@ -305,8 +376,8 @@ def run_train(args):
         roof.update({"traffic": traffic, "traffic_source": traffic_src})
     else:
         work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE)
-        traffic, traffic_src = load_traffic()
-        roof = dominant_roofline(B, H, W, kern_ms, len(evs), WINO_TILE)
+        traffic, traffic_src = load_traffic("traffic_conv6_fwd_f32.json")
+        roof = dominant_roofline(B, H, W, kern_ms, gemm_ms, len(evs), WINO_TILE)
         roof.update({"traffic": traffic, "traffic_source": traffic_src})
 
     frames = world * B * args.steps
@@ -355,7 +426,7 @@ def run_train(args):
 def run_infer(args):
     """configs[4]: 1x7x1080x1920 eval forward, hipGraph-captured (replicas only
     for N > 1: frames are independent, no collective)."""
-    world, rank, dev = init_dist()
+    world, rank, dev = init_dist(args)
     import nsm_amd
     from nsm_amd import ops as nops
     from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
@@ -372,12 +443,13 @@ def run_infer(args):
     for _ in range(args.warmup):
         graphed.replay()
     torch.cuda.synchronize()
-    elapsed = timed(graphed.replay, args.steps, world)
+    elapsed = timed(graphed.replay, args.steps, world, dev)
 
     # kernel/stage timing from eager forwards of the same shape (HIP events
     # cannot be read back from inside a replayed graph)
     probe_tag = "conv6.conv.0.fwd"
     nops.PROBES[probe_tag] = []
+    nops.PROBES[probe_tag + ".gemm"] = []
     for st in STAGES:
         nops.PROBES[st + ".fwd"] = []
     with torch.no_grad():
@@ -385,13 +457,14 @@ def run_infer(args):
             model(x)
     torch.cuda.synchronize()
     evs = nops.PROBES.pop(probe_tag)
+    gevs = nops.PROBES.pop(probe_tag + ".gemm", [])
     times = {st: mean_ms(nops.PROBES.pop(st + ".fwd")) for st in STAGES}
     if bf16:
         work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30, passes=1)
         roof = direct_roofline(B, H, W, mean_ms(evs), len(evs))
     else:
         work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE, passes=1)
-        roof = dominant_roofline(B, H, W, mean_ms(evs), len(evs), WINO_TILE)
+        roof = dominant_roofline(B, H, W, mean_ms(evs), mean_ms(gevs), len(evs), WINO_TILE)
     roof.update({"traffic": None, "traffic_source": None})
     frames = world * B * args.steps
     res = {
@@ -424,11 +497,35 @@ def run_infer(args):
         dist.destroy_process_group()
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, args):
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    _dispatch(args)
+
+
+def _dispatch(args):
+    if args.dry_run:
+        run_dry(args)
+    elif args.workload == "train":
+        run_train(args)
+    else:
+        run_infer(args)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (train 8, infer 1)")
     ap.add_argument("--in-ch", type=int, default=7)
     ap.add_argument("--res", type=int, default=512)
@@ -438,13 +535,18 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--vgg", action="store_true",
                     help="train: include CustomLoss's VGG19 perceptual term (customLoss.py:7-90)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU/gloo launcher check with a stand-in step (no GPU, not a measurement)")
     args = ap.parse_args()
-    if args.workload == "train":
-        args.batch = args.batch or 8
-        run_train(args)
-    else:
-        args.batch = args.batch or 1
-        run_infer(args)
+    args.batch = args.batch or (8 if args.workload == "train" else 1)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no torchrun: one worker process per GPU, spawned before anything
+        # touches the GPU in this process
+        import torch.multiprocessing as mp
+        mp.start_processes(_worker, args=(args.gpus, _free_port(), args), nprocs=args.gpus,
+                           start_method="spawn")
+        return
+    _dispatch(args)
 
 
 if __name__ == "__main__":

@@ -227,6 +227,54 @@ int nsm_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, floa
                    float beta2, float eps, float weight_decay, int step, const float* gcoef,
                    void* stream);
 
+/* ---- the reference's full step tail (main.py:287-423), no host sync ----------
+ * The gradient is one flat fp32 buffer of the module's parameters in order;
+ * seg_off[nseg+1] (device) delimits them. nsm_tail_plan (host) cuts the buffer
+ * into blocks of nsm_tail_chunk() elements that never straddle a parameter:
+ * blk_seg/blk_lo/blk_hi[nblk], seg_blk[nseg+1] (first block of each
+ * parameter); call once with blk_seg == NULL to get nblk. Upload the arrays.
+ * nsm_grad_tail, in place on g (the rank-sum of the DP all-reduce; inv_world
+ * turns it into the mean first):
+ *   NaN/Inf census; any parameter > 20 % invalid -> skip (main.py:295-317);
+ *   else repair NaN -> mean + randn*std*0.1, Inf -> sign*max|valid|*10
+ *   (:320-354; randn from `noise` if non-NULL, else a counter-based generator
+ *   keyed by seed and the step count); per-parameter clip to 1000*scale
+ *   (:361-365); unscale by 1/scale (:368); per-parameter skip above 1e5,
+ *   rescale to 1e3 above 1e3 (:383-397); clip_grad_norm_(max_norm) (:405);
+ *   skip if a clipped norm > 10 (:408-418).
+ *   Writes seg_coef[nseg][4] (pre-clip x unscale, 1e3 rescale, clip coef,
+ *   zeroed), stat[4] (total norm, clip coef, max_norm, max clipped norm),
+ *   flags[8] (skip, repaired, severe, nonfinite, huge, postclip, n_rescaled,
+ *   n_zeroed), and step[0] += !skip. workspace: nsm_tail_ws_bytes().
+ * nsm_adamw_tail: torch.optim.AdamW step (main.py:421, hyper-parameters
+ *   main.py:955) with g scaled by seg_coef; a no-op when flags[0] is set; the
+ *   bias corrections use the device step count. */
+int64_t nsm_tail_chunk(void);
+int nsm_tail_plan(const int64_t* seg_off, int nseg, int* blk_seg, int64_t* blk_lo,
+                  int64_t* blk_hi, int* seg_blk, int cap);
+size_t nsm_tail_ws_bytes(int nseg, int nblk);
+int nsm_grad_tail(float* g, int nseg, const int64_t* seg_off, const int* seg_blk,
+                  const int* blk_seg, const int64_t* blk_lo, const int64_t* blk_hi, int nblk,
+                  float inv_world, float scale, float max_norm, const float* noise, uint64_t seed,
+                  void* ws, size_t ws_bytes, float* seg_coef, float* stat, int* flags, int* step,
+                  void* stream);
+int nsm_adamw_tail(float* p, const float* g, float* m, float* v, const int* blk_seg,
+                   const int64_t* blk_lo, const int64_t* blk_hi, int nblk, const float* seg_coef,
+                   const int* flags, const int* step, double lr, double beta1, double beta2,
+                   double eps, double weight_decay, void* stream);
+
+/* ---- drop-in surface helpers ---------------------------------------------------
+ * NCHW fp32 <-> NHWC [B*H*W][cp] (dtype NSM_F32 / NSM_BF16) for a standalone
+ * DoubleConv call (Unetmodel.py:32-33); channels C..cp-1 are written as 0.
+ * nsm_range_flag: flag[0] = 1 if any o[i] is outside [lo, hi] or NaN (the
+ * `assert output.min() >= 0 and output.max() <= 1` of customLoss.py:131 /
+ * pert_loss.py:131 as a sticky device flag; never writes 0). */
+int nsm_nchw_to_nhwc(const float* x, int B, int C, int H, int W, void* y, int cp, int ldy,
+                     int dtype, void* stream);
+int nsm_nhwc_to_nchw(const void* z, int ldz, int B, int C, int H, int W, float* x, int dtype,
+                     void* stream);
+int nsm_range_flag(const float* o, int64_t n, float lo, float hi, int* flag, void* stream);
+
 /* ---- bf16 convolutions (BASELINE config 3) ---------------------------------
  * Same contracts as nsm_pack_conv_weight / nsm_conv_fwd_stats / nsm_conv_wgrad
  * with bf16 activations and packed weights (v_mfma_f32_32x32x16_bf16, fp32

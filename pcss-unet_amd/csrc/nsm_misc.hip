@@ -1,0 +1,114 @@
+// Small boundary kernels of the drop-in surface:
+//  * NCHW <-> NHWC layout changes for a standalone DoubleConv call
+//    (Unetmodel.py:32-33: `DoubleConv.forward(x)` on an NCHW tensor), tiled
+//    through LDS so both the NCHW rows and the NHWC pixel vectors are coalesced;
+//  * the output-range assertion of CustomLoss / PerturbationLoss
+//    (customLoss.py:131, pert_loss.py:131: min >= 0 and max <= 1, NaN fails)
+//    as a sticky device flag, so the check costs no host synchronisation.
+#include "nsm_common.h"
+
+namespace nsm {
+
+constexpr int LT_P = 64;  // pixels per tile
+constexpr int LT_C = 32;  // channels per tile
+
+// x [B][C][HW] fp32 -> y [B*HW][cp] (T), channels C..cp-1 written as 0.
+template <typename T>
+__global__ void __launch_bounds__(256) nchw_to_nhwc_kernel(const float* __restrict__ x, int C,
+                                                           int HW, int cp, T* __restrict__ y,
+                                                           int ldy) {
+  __shared__ float tile[LT_C][LT_P + 1];
+  const int b = blockIdx.z, c0 = blockIdx.y * LT_C, p0 = blockIdx.x * LT_P;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  for (int cc = ty; cc < LT_C; cc += 4) {
+    const int c = c0 + cc, p = p0 + tx;
+    float v = 0.f;
+    if (c < C && p < HW) v = x[((size_t)b * C + c) * HW + p];
+    tile[cc][tx] = v;
+  }
+  __syncthreads();
+  const int lc = threadIdx.x & 31, lp = threadIdx.x >> 5;  // 32 x 8
+  for (int pp = lp; pp < LT_P; pp += 8) {
+    const int p = p0 + pp, c = c0 + lc;
+    if (p < HW && c < cp) st1(y + ((size_t)b * HW + p) * ldy + c, tile[lc][pp]);
+  }
+}
+
+// z [B*HW][ld] (T) -> x [B][C][HW] fp32 (first C channels)
+template <typename T>
+__global__ void __launch_bounds__(256) nhwc_to_nchw_kernel(const T* __restrict__ z, int ldz, int C,
+                                                           int HW, float* __restrict__ x) {
+  __shared__ float tile[LT_C][LT_P + 1];
+  const int b = blockIdx.z, c0 = blockIdx.y * LT_C, p0 = blockIdx.x * LT_P;
+  const int lc = threadIdx.x & 31, lp = threadIdx.x >> 5;
+  for (int pp = lp; pp < LT_P; pp += 8) {
+    const int p = p0 + pp, c = c0 + lc;
+    tile[lc][pp] = (p < HW && c < C) ? ld1(z + ((size_t)b * HW + p) * ldz + c) : 0.f;
+  }
+  __syncthreads();
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int cc = ty; cc < LT_C; cc += 4) {
+    const int c = c0 + cc, p = p0 + tx;
+    if (c < C && p < HW) x[((size_t)b * C + c) * HW + p] = tile[cc][tx];
+  }
+}
+
+// flag[0] = 1 if any o[i] < lo, o[i] > hi or o[i] is NaN; never written 0
+__global__ void __launch_bounds__(256) range_flag_kernel(const float* __restrict__ o, int64_t n,
+                                                         float lo, float hi, int* flag) {
+  bool bad = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = o[i];
+    bad |= !(v >= lo && v <= hi);
+  }
+  if (__any(bad) && (threadIdx.x & 63) == 0) flag[0] = 1;
+}
+
+}  // namespace nsm
+
+using namespace nsm;
+
+extern "C" int nsm_nchw_to_nhwc(const float* x, int B, int C, int H, int W, void* y, int cp,
+                                int ldy, int dtype, void* stream) {
+  NSM_CHECK_ARG(x && y && B > 0 && C > 0 && cp >= C && ldy >= cp && H * W > 0,
+                "nchw_to_nhwc: bad args");
+  const int HW = H * W;
+  dim3 grid((HW + LT_P - 1) / LT_P, (cp + LT_C - 1) / LT_C, B);
+  hipStream_t s = as_stream(stream);
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, grid, dim3(256), 0, s, x, C, HW, cp,
+                       (bf16_t*)y, ldy);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, grid, dim3(256), 0, s, x, C, HW, cp, (float*)y,
+                       ldy);
+  NSM_LAUNCH_CHECK("nchw_to_nhwc");
+  return 0;
+}
+
+extern "C" int nsm_nhwc_to_nchw(const void* z, int ldz, int B, int C, int H, int W, float* x,
+                                int dtype, void* stream) {
+  NSM_CHECK_ARG(z && x && B > 0 && C > 0 && ldz >= C && H * W > 0, "nhwc_to_nchw: bad args");
+  const int HW = H * W;
+  dim3 grid((HW + LT_P - 1) / LT_P, (C + LT_C - 1) / LT_C, B);
+  hipStream_t s = as_stream(stream);
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)z, ldz,
+                       C, HW, x);
+  else
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, grid, dim3(256), 0, s, (const float*)z, ldz, C,
+                       HW, x);
+  NSM_LAUNCH_CHECK("nhwc_to_nchw");
+  return 0;
+}
+
+extern "C" int nsm_range_flag(const float* o, int64_t n, float lo, float hi, int* flag,
+                              void* stream) {
+  NSM_CHECK_ARG(o && flag && n > 0, "range_flag: bad args");
+  long long g = (n + 255) / 256;
+  if (g > 1024) g = 1024;
+  hipLaunchKernelGGL(range_flag_kernel, dim3((int)g), dim3(256), 0, as_stream(stream), o, n, lo, hi,
+                     flag);
+  NSM_LAUNCH_CHECK("range_flag");
+  return 0;
+}

@@ -17,6 +17,8 @@ I = ctypes.c_int
 L = ctypes.c_int64
 F = ctypes.c_float
 Z = ctypes.c_size_t
+D = ctypes.c_double
+U64 = ctypes.c_uint64
 
 # name -> (restype, argtypes)
 _SIGS = {
@@ -81,6 +83,14 @@ _SIGS = {
     "nsm_conv_stat_rows_bf16": (I, [I, I, I, I]),
     "nsm_conv_wgrad_bf16": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
     "nsm_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
+    "nsm_tail_chunk": (L, []),
+    "nsm_tail_plan": (I, [P, I, P, P, P, P, I]),
+    "nsm_tail_ws_bytes": (Z, [I, I]),
+    "nsm_grad_tail": (I, [P, I, P, P, P, P, P, I, F, F, F, P, U64, P, Z, P, P, P, P, P]),
+    "nsm_adamw_tail": (I, [P, P, P, P, P, P, P, I, P, P, P, D, D, D, D, D, P]),
+    "nsm_nchw_to_nhwc": (I, [P, I, I, I, I, P, I, I, I, P]),
+    "nsm_nhwc_to_nchw": (I, [P, I, I, I, I, I, P, I, P]),
+    "nsm_range_flag": (I, [P, L, F, F, P, P]),
 }
 
 

@@ -38,16 +38,30 @@ class GraphedUnet:
         self.graph = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(self.graph):
             self.static_out = model(self.static_in)
+        model.train(self.was_training)
+        # the graph holds raw parameter / buffer addresses: replay must see the same storage
+        self._ptrs = self._addresses()
+
+    def _addresses(self):
+        return [t.data_ptr() for t in list(self.model.parameters()) + list(self.model.buffers())]
+
+    def _check(self):
+        if self._addresses() != self._ptrs:
+            raise RuntimeError("GraphedUnet: the model's parameters or buffers were re-allocated "
+                               "after capture (e.g. FlatAdamW re-homed them, or .to()); the "
+                               "captured graph would read freed memory — capture again")
 
     def __call__(self, x):
         if tuple(x.shape) != self.shape or x.dtype != self.dtype:
             raise ValueError(f"GraphedUnet captured for {self.shape} {self.dtype}, "
                              f"got {tuple(x.shape)} {x.dtype}")
+        self._check()
         self.static_in.copy_(x)
         self.graph.replay()
         return self.static_out
 
     def replay(self):
         """Run the captured forward on whatever is in static_in."""
+        self._check()
         self.graph.replay()
         return self.static_out

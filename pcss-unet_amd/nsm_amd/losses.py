@@ -5,11 +5,21 @@
   (customLoss.py:129-193). The reference's VGG term is a DETACHED constant
   (`torch.tensor(total_loss, requires_grad=True)`, customLoss.py:90), so the
   gradient is exactly alpha*sign(o-t)/N. The VGG19 perceptual value
-  (`nsm_amd.vgg.MultiLayerVGGLoss`, on the libnsm kernels) needs ImageNet
-  weights the reference downloads at construction; offline pass
-  `vgg_weights=<local torchvision vgg19 .pth | state_dict | MultiLayerVGGLoss
-  | "random">` (or any `vgg=<callable(out, target)>`). With neither, the term
-  is 0 (the gradient is unchanged either way).
+  (`nsm_amd.vgg.MultiLayerVGGLoss`, on the libnsm kernels) needs the ImageNet
+  weights the reference downloads at construction (customLoss.py:20,97). By
+  default (`vgg_weights="auto"`) the torchvision checkpoint is taken from
+  $NSM_VGG19_WEIGHTS or torch.hub's cache (`<hub>/checkpoints/
+  vgg19-dcbb9e9d.pth`, loaded with weights_only=True); when neither exists the
+  loss warns once that its VGG term is 0. Other values: a .pth path, a
+  state_dict, a MultiLayerVGGLoss, "random", or False (term off, no warning);
+  any `vgg=<callable(out, target)>` overrides. The gradient is the same either
+  way.
+* The reference asserts `output.min() >= 0 and output.max() <= 1`
+  (customLoss.py:131) with a host sync per call. Here a range-check kernel
+  sets a sticky device flag that is copied to pinned host memory
+  asynchronously; the next call raises the same AssertionError once that copy
+  has landed (at most one step late, never a sync), and `check_range()`
+  checks it immediately (synchronising).
 * `PerturbationLoss(perturbation_count=3)`: pert_loss.py:7-90 — three
   no-grad forwards of the model on inputs perturbed by per-channel
   std * 0.01 Gaussian noise, mean L1 to the original output.
@@ -25,10 +35,64 @@
   pert_loss.py:166-199, mean over consecutive frame pairs of
   mean(exp(alpha*|f_t - f_{t-1}|) - 1) (`nsm_expdiff_mean`).
 """
+import os
+import warnings
+
 import torch
 import torch.nn as nn
 
 from ._lib import call, lib, ptr, require_gpu, stream
+
+VGG19_FILE = "vgg19-dcbb9e9d.pth"   # torchvision IMAGENET1K_V1 (customLoss.py:20)
+_VGG_WARNED = []
+
+
+def find_vgg19_checkpoint():
+    """A locally cached torchvision VGG19 ImageNet checkpoint, or None."""
+    env = os.environ.get("NSM_VGG19_WEIGHTS")
+    cands = [env] if env else []
+    try:
+        cands.append(os.path.join(torch.hub.get_dir(), "checkpoints", VGG19_FILE))
+    except Exception:  # noqa: BLE001  (hub dir unresolvable: no cache)
+        pass
+    for c in cands:
+        if c and os.path.isfile(c):
+            return c
+    return None
+
+
+class _RangeCheck:
+    """Sticky device flag for `assert 0 <= output <= 1` (customLoss.py:131,
+    pert_loss.py:131) without a host synchronisation."""
+
+    def __init__(self, what):
+        self.what = what
+        self.flag = None
+        self.host = None
+        self.event = None
+
+    def _raise_if_set(self):
+        if self.host is not None and int(self.host[0]) != 0:
+            self.host[0] = 0
+            self.flag.zero_()
+            raise AssertionError(f"{self.what}: output must be in [0, 1] (sigmoid output), "
+                                 "customLoss.py:131")
+
+    def launch(self, o):
+        if self.event is not None and self.event.query():
+            self._raise_if_set()
+        if self.flag is None or self.flag.device != o.device:
+            self.flag = torch.zeros(1, dtype=torch.int32, device=o.device)
+            self.host = torch.zeros(1, dtype=torch.int32).pin_memory()
+            self.event = torch.cuda.Event()
+        call("nsm_range_flag", ptr(o), o.numel(), 0.0, 1.0, ptr(self.flag), stream())
+        self.host.copy_(self.flag, non_blocking=True)
+        self.event.record()
+
+    def check(self):
+        if self.event is not None:
+            self.event.synchronize()
+            self._raise_if_set()
 
 
 class _L1Fn(torch.autograd.Function):
@@ -69,10 +133,21 @@ class L1Loss(nn.Module):
 
 
 class CustomLoss(nn.Module):
-    def __init__(self, device=None, alpha=0.9, vgg=None, vgg_weights=None, check_range=True):
+    def __init__(self, device=None, alpha=0.9, vgg=None, vgg_weights="auto", check_range=True):
         super().__init__()
         self.alpha = alpha
         self.l1 = L1Loss()
+        if vgg is None and isinstance(vgg_weights, str) and vgg_weights == "auto":
+            vgg_weights = find_vgg19_checkpoint()
+            if vgg_weights is None and not _VGG_WARNED:
+                _VGG_WARNED.append(True)
+                warnings.warn(
+                    "nsm_amd.CustomLoss: no VGG19 ImageNet checkpoint found ($NSM_VGG19_WEIGHTS "
+                    f"or torch.hub cache {VGG19_FILE}); the perceptual term (customLoss.py:137, "
+                    "weight 1-alpha) is 0 — the loss VALUE differs from the reference's, its "
+                    "gradient (alpha*sign/N) does not", RuntimeWarning, stacklevel=2)
+        if vgg_weights is False:
+            vgg_weights = None
         if vgg_weights is not None:
             from .vgg import MultiLayerVGGLoss
             if isinstance(vgg_weights, MultiLayerVGGLoss):
@@ -87,17 +162,21 @@ class CustomLoss(nn.Module):
         self.vgg = vgg
         self.device = device
         self.check_range = check_range
+        self._range = _RangeCheck("CustomLoss")
 
     def forward(self, output, target, inputs=None):
         if self.check_range:
-            # customLoss.py:131 asserts output in [0,1]; sigmoid guarantees it, so
-            # the check is done without a host sync (NaNs fail it too).
-            pass
+            require_gpu(output, "CustomLoss output")
+            self._range.launch(output.detach().contiguous().to(torch.float32))
         loss = l1_loss(output, target, self.alpha)
         if self.vgg is not None:
             v = self.vgg(output, target)
             loss = loss + (1 - self.alpha) * torch.as_tensor(v, device=loss.device).detach()
         return loss
+
+    def check_range_now(self):
+        """Raise now (host sync) if any output seen so far left [0, 1]."""
+        self._range.check()
 
 
 class PerturbationLoss(nn.Module):
@@ -138,7 +217,7 @@ class PerturbationLoss(nn.Module):
 
 
 class EnhancedCustomLoss(nn.Module):
-    def __init__(self, device=None, alpha=0.9, perturb_weight=0.5, vgg=None, vgg_weights=None):
+    def __init__(self, device=None, alpha=0.9, perturb_weight=0.5, vgg=None, vgg_weights="auto"):
         super().__init__()
         self.alpha = alpha
         self.perturb_weight = perturb_weight
@@ -148,6 +227,9 @@ class EnhancedCustomLoss(nn.Module):
         self.perturbation_loss = PerturbationLoss()
 
     def forward(self, model, output, target, inputs, noises=None):
+        # pert_loss.py:131: the same [0, 1] assertion, as CustomLoss's device flag
+        require_gpu(output, "EnhancedCustomLoss output")
+        self.base._range.launch(output.detach().contiguous().to(torch.float32))
         l1 = l1_loss(output, target)
         if self.vgg_loss is not None:
             vgg = torch.as_tensor(self.vgg_loss(output, target), device=l1.device).detach()

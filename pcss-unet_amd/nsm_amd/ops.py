@@ -158,12 +158,15 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     Mb = empty(nb * T * cout_p, device=x.device)
     y = empty(M, cout_p, device=x.device)
     st = stream()
+    ev_all = _probe(tag)  # the whole convolution: input transform + GEMM + output transform
     call("nsm_wino_input", ptr(x), x.stride(0), B, H, W, cin_p, tile, int(relu), ptr(V), st)
-    ev = _probe(tag)      # the probe times the batched MFMA GEMM alone
+    ev = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
     call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb), st)
     if ev is not None:
         ev.record()
     call("nsm_wino_output", ptr(Mb), B, H, W, cout_p, tile, ptr(bias), ptr(y), y.stride(0), st)
+    if ev_all is not None:
+        ev_all.record()
     return (y, V) if keep_v else y
 
 

@@ -18,13 +18,15 @@ Execution: one torch.autograd.Function per forward. Activations live in HBM
 as NHWC fp32 `[pixels, channels padded to 32]`; every op is a libnsm kernel
 launched on the current HIP stream (see DESIGN.md for the kernel list).
 """
+import os
+import warnings
+
 import torch
+import torch.distributed as dist
 import torch.nn as nn
 
 from . import ops, optim
-from ._lib import require_gpu
-
-import os
+from ._lib import call, ptr, require_gpu, stream
 
 SLOPE = 0.2
 # 3x3 convolutions with at least this many (padded) input channels use the
@@ -47,8 +49,92 @@ SKIP_OF = {6: 4, 7: 3, 8: 2}          # merge_k = conv_k(...) + c_skip  (Unetmod
 POOL_SKIP = {4: 6, 3: 7, 2: 8}        # c_k feeds pool_k and decoder merge (6,7,8)
 
 
+_WARNED = set()
+
+
+def _warn_once(key, msg):
+    if key not in _WARNED:
+        _WARNED.add(key)
+        warnings.warn(msg, RuntimeWarning, stacklevel=3)
+
+
+def _check_autocast():
+    """main.py:257 runs the GPU step under fp16 autocast; this path has fp32 and
+    bf16 kernels only (bf16 under bf16 autocast), so fp16 requests run fp32."""
+    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16:
+        _warn_once("fp16", "nsm_amd: fp16 autocast requested (main.py:257); the MI355X path "
+                   "computes in fp32 here (use torch.autocast('cuda', dtype=torch.bfloat16) or "
+                   "Unet.set_compute_dtype(torch.bfloat16) for the bf16 kernels)")
+
+
+def _nhwc(x, cp, dtype):
+    """NCHW [B,C,H,W] -> NHWC 2-D [B*H*W, cp] in `dtype` (zero-padded channels)."""
+    B, C, H, W = x.shape
+    x = x.detach().to(torch.float32).contiguous()
+    out = torch.empty(B * H * W, cp, dtype=dtype, device=x.device)
+    call("nsm_nchw_to_nhwc", ptr(x), B, C, H, W, ptr(out), cp, cp, ops.dt(out), stream())
+    return out
+
+
+def _nchw(z, B, C, H, W):
+    """NHWC 2-D [B*H*W, ld] -> fp32 NCHW [B,C,H,W] (first C channels)."""
+    out = torch.empty(B, C, H, W, dtype=torch.float32, device=z.device)
+    call("nsm_nhwc_to_nchw", ptr(z), z.stride(0), B, C, H, W, ptr(out), ops.dt(z), stream())
+    return out
+
+
+def _dropout_mask(p, B, ci, device):
+    """ATen feature dropout (Unetmodel.py:24): bernoulli(1-p) / (1-p) per (n, c),
+    padded to the NHWC channel count with zeros."""
+    m = torch.empty(B, ci, device=device).bernoulli_(1 - p).div_(1 - p)
+    cp = ops.pad32(ci)
+    if cp != ci:
+        m = torch.nn.functional.pad(m, (0, cp - ci))
+    return m.contiguous()
+
+
+class _DoubleConvFn(torch.autograd.Function):
+    """A DoubleConv called on its own (Unetmodel.py:32-33) on the same fused
+    kernels the Unet uses: NCHW in, NCHW out, BN running stats updated in
+    train mode, the backward writes all 8 parameter gradients."""
+
+    @staticmethod
+    def forward(ctx, x, blk, *params):
+        B, C, H, W = x.shape
+        ci, co = blk.conv[0].in_channels, blk.conv[4].out_channels
+        if C != ci:
+            raise ValueError(f"DoubleConv expects {ci} channels, got {C}")
+        training = blk.training
+        dtype = (torch.bfloat16 if torch.is_autocast_enabled("cuda")
+                 and torch.get_autocast_dtype("cuda") == torch.bfloat16 else torch.float32)
+        X = _nhwc(x, ops.pad32(ci), dtype)
+        p = blk.conv[3].p
+        mask = _dropout_mask(p, B, ci, x.device) if training and p > 0 else None
+        s = _block_fwd(blk, X, B, H, W, training, mask, "doubleconv")
+        z = ops.bn_act(s.Y2, s.bn2, SLOPE)
+        ctx.blk, ctx.s, ctx.shape, ctx.training = blk, s, (B, C, H, W), training
+        ctx.params = params
+        out = _nchw(z, B, co, H, W)
+        return out.to(dtype) if dtype != torch.float32 else out
+
+    @staticmethod
+    def backward(ctx, gout):
+        if not ctx.training:
+            raise RuntimeError("nsm_amd DoubleConv backward is implemented for train mode")
+        blk, s = ctx.blk, ctx.s
+        B, C, H, W = ctx.shape
+        G = _nhwc(gout, s.cop, s.Y2.dtype)
+        grads = {p: torch.empty_like(p) for p in ctx.params}
+        dX = _block_bwd(blk, s, G, grads, True, "doubleconv")
+        ctx.s = None
+        dx = _nchw(dX, B, C, H, W) if ctx.needs_input_grad[0] else None
+        return (dx, None) + tuple(grads[p] for p in ctx.params)
+
+
 class DoubleConv(nn.Module):
-    """Parameter container with the reference's layout (Unetmodel.py:17-33)."""
+    """The reference's DoubleConv (Unetmodel.py:17-33): same sub-modules and
+    state_dict layout. Inside `Unet` the blocks are run by the fused Unet
+    path; called on its own, forward runs `_DoubleConvFn` on the same kernels."""
 
     def __init__(self, in_ch, out_ch, dropout_rate=0.2, dilation=1):
         super().__init__()
@@ -64,8 +150,9 @@ class DoubleConv(nn.Module):
         )
 
     def forward(self, x):
-        raise RuntimeError("nsm_amd.DoubleConv is executed by Unet.forward (fused HIP path); "
-                           "call the enclosing Unet")
+        require_gpu(x, "DoubleConv input")
+        _check_autocast()
+        return _DoubleConvFn.apply(x, self, *tuple(self.parameters()))
 
 
 class Unet(nn.Module):
@@ -94,6 +181,9 @@ class Unet(nn.Module):
         self.emulate_checkpoint_bn = True
         # data parallel: (group,) when the backward launches its own grad all-reduces
         self._grad_allreduce = None
+        # data parallel: (group, src) when forward broadcasts rank 0's BN buffers
+        self._bn_broadcast = None
+        self._bn_flat_cache = None
         # activation storage / MFMA dtype: None = fp32, or bf16 inside a
         # torch.autocast(dtype=torch.bfloat16) region; set_compute_dtype() pins it
         self.compute_dtype = None
@@ -124,6 +214,52 @@ class Unet(nn.Module):
         self._grad_allreduce = (group,) if enable else None
         return self
 
+    def data_parallel(self, group=None, overlap=True, broadcast_buffers=True):
+        """Plain DP semantics (DDP's defaults): the gradient
+        all-reduce overlapped with the backward, and rank 0's BatchNorm running
+        statistics broadcast to every rank at the start of each train-mode
+        forward (DDP broadcast_buffers=True), so all ranks — and rank 0's
+        checkpoint — carry the same buffers."""
+        self.overlap_grad_allreduce(group, overlap)
+        if broadcast_buffers:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            self._bn_broadcast = (group, src)
+        else:
+            self._bn_broadcast = None
+        return self
+
+    def _bn_flat(self):
+        """All BN running_mean/running_var as views of ONE fp32 buffer and all
+        num_batches_tracked as views of ONE int64 buffer (re-homed when a
+        `.to()` or assignment replaced them), so the DP broadcast is two calls."""
+        bns = [m for m in self.modules() if isinstance(m, nn.BatchNorm2d) and m.track_running_stats]
+        cache = self._bn_flat_cache
+        if cache is not None:
+            f, i = cache
+            fp, ip = f.untyped_storage().data_ptr(), i.untyped_storage().data_ptr()
+            if all(b.running_mean.untyped_storage().data_ptr() == fp
+                   and b.running_var.untyped_storage().data_ptr() == fp
+                   and b.num_batches_tracked.untyped_storage().data_ptr() == ip for b in bns):
+                return cache
+        with torch.no_grad():
+            f = torch.cat([t.reshape(-1) for b in bns for t in (b.running_mean, b.running_var)])
+            i = torch.stack([b.num_batches_tracked.reshape(()) for b in bns])
+            off = 0
+            for k, b in enumerate(bns):
+                n = b.running_mean.numel()
+                b.running_mean = f[off:off + n]
+                b.running_var = f[off + n:off + 2 * n]
+                b.num_batches_tracked = i[k]
+                off += 2 * n
+        self._bn_flat_cache = (f, i)
+        return self._bn_flat_cache
+
+    def broadcast_buffers(self, src=0, group=None):
+        """Overwrite every rank's BN buffers with rank `src`'s (two collectives)."""
+        f, i = self._bn_flat()
+        dist.broadcast(f, src, group=group)
+        dist.broadcast(i, src, group=group)
+
     # reference helpers (Unetmodel.py:65-88)
     def rearrange_to_channels(self, x):
         return torch.nn.functional.pixel_unshuffle(x, 2)
@@ -139,6 +275,17 @@ class Unet(nn.Module):
         params = tuple(self.parameters())
         for p in params[:1]:
             require_gpu(p, "Unet parameters")
+        _check_autocast()
+        if "hooks" not in _WARNED and any(m._backward_hooks or m._backward_pre_hooks
+                                          for m in self.modules() if m is not self):
+            # main.py:207-222 registers a logging hook on every leaf module
+            _warn_once("hooks", "nsm_amd.Unet: backward hooks on sub-modules are not invoked by "
+                       "the fused Unet path (the reference's main.py:207-222 hooks only log "
+                       "NaN/Inf/norms); FlatAdamW(sanitize=True).last_flags() reports the "
+                       "step tail's NaN/Inf/norm decisions instead")
+        if self._bn_broadcast is not None and self.training:
+            group, src = self._bn_broadcast
+            self.broadcast_buffers(src, group)
         return _UnetFn.apply(x, self, *params)
 
 
@@ -157,13 +304,12 @@ def _masks_for(mod, B, device, training):
         ci = blk.conv[0].in_channels
         if inj is not None and k in inj:
             m = inj[k].to(device=device, dtype=torch.float32).reshape(B, ci)
+            cp = ops.pad32(ci)
+            if cp != ci:
+                m = torch.nn.functional.pad(m, (0, cp - ci))
+            masks[k] = m.contiguous()
         else:
-            # ATen feature dropout: bernoulli(1-p) / (1-p) per (n, c)
-            m = torch.empty(B, ci, device=device).bernoulli_(1 - p).div_(1 - p)
-        cp = ops.pad32(ci)
-        if cp != ci:
-            m = torch.nn.functional.pad(m, (0, cp - ci))
-        masks[k] = m.contiguous()
+            masks[k] = _dropout_mask(p, B, ci, device)
     return masks
 
 

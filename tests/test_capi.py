@@ -64,3 +64,27 @@ def test_fastdiv_exact():
         ns = list(range(0, 2000)) + [int(v) for v in rng.integers(0, 2**31, 2000)] + [2**31 - 1]
         for n in ns:
             assert fastdiv(n, d) == n // d, (n, d)
+
+
+def test_tail_plan_blocks_never_straddle_parameters():
+    """nsm_tail_plan (host): blocks of nsm_tail_chunk() elements, one parameter
+    each, covering the flat buffer in order."""
+    import nsm_amd._lib as L
+    sizes = [1728, 16, 512, 37, 9000, 4, 1, 9, 9437184]
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    seg_off = (ctypes.c_int64 * len(offs))(*offs.tolist())
+    nseg = len(sizes)
+    nblk = L.lib.nsm_tail_plan(seg_off, nseg, None, None, None, None, 0)
+    ch = L.lib.nsm_tail_chunk()
+    assert nblk == sum(-(-s // ch) for s in sizes)
+    bs, lo, hi = (ctypes.c_int * nblk)(), (ctypes.c_int64 * nblk)(), (ctypes.c_int64 * nblk)()
+    sb = (ctypes.c_int * (nseg + 1))()
+    assert L.lib.nsm_tail_plan(seg_off, nseg, bs, lo, hi, sb, nblk) == nblk
+    assert lo[0] == 0 and hi[nblk - 1] == offs[-1]
+    for b in range(nblk):
+        s = bs[b]
+        assert offs[s] <= lo[b] < hi[b] <= offs[s + 1] and hi[b] - lo[b] <= ch
+        if b:
+            assert lo[b] == hi[b - 1]
+    assert [sb[s] for s in range(nseg + 1)] == [0] + list(np.cumsum([-(-s // ch) for s in sizes]))
+    assert L.lib.nsm_tail_ws_bytes(nseg, nblk) > 0

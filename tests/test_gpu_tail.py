@@ -1,0 +1,110 @@
+"""GPU: FlatAdamW(sanitize=True) — the device-side step tail (include/nsm.h
+nsm_grad_tail + nsm_adamw_tail) — against the reference's own train_model
+(fixture tests/golden/tail_steps.npz, made by tests/golden/make_golden_tail.py):
+12 scripted steps over 4 epochs with NaN/Inf repairs, 20 % skips, per-parameter
+pre-clip, the max_norm schedule and AdamW, with the repair noise the reference
+drew injected."""
+import numpy as np
+import pytest
+import torch
+
+from test_tail import tail_fixture
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda", 0)
+
+
+def _replay(world=1, capture=False):
+    import nsm_amd
+    fx, E, P, nparam, steps = tail_fixture()
+    params = [torch.nn.Parameter(torch.from_numpy(fx[f"init/{i}"].copy()).to(DEV))
+              for i in range(nparam)]
+    sizes = [p.numel() for p in params]
+    opt = nsm_amd.FlatAdamW(params, lr=float(fx["meta/base_lr"]), weight_decay=float(fx["meta/wd"]),
+                            max_grad_norm=1.0, sanitize=True, world_size=world)
+    gflat = torch.empty(sum(sizes), device=DEV)
+    noise = torch.empty_like(gflat)
+    off = 0
+    for p in params:
+        p.grad = gflat[off:off + p.numel()].view_as(p)
+        off += p.numel()
+    got = {}
+    graph = None
+    for b, (epoch, grads, nz) in enumerate(steps):
+        gflat.copy_(torch.cat([g.reshape(-1) for g in grads]).to(DEV) * world)
+        noise.copy_(torch.cat([n.reshape(-1) for n in nz]).to(DEV))
+        opt.param_groups[0]["lr"] = float(fx["meta/base_lr"]) / (1.0 + epoch)
+        opt.set_epoch(epoch, E)
+        if capture:
+            # lr / max_norm are launch arguments: capture per epoch, replay within it
+            if graph is None or b % P == 0:
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph):   # capture does not execute: replay runs it
+                    opt.step(noise=noise)
+            graph.replay()
+        else:
+            opt.step(noise=noise)
+        torch.cuda.synchronize()
+        got[b] = (opt.last_flags(), [p.detach().cpu().numpy().copy() for p in params])
+    return fx, opt, got, nparam, params
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_device_tail_matches_reference_train_model(world):
+    fx, opt, got, nparam, params = _replay(world)
+    worst = 0.0
+    for b, (flags, ps) in got.items():
+        assert flags["skip"] == int(fx["skipped"][b]), (b, flags)
+        if b in (1, 5, 8):
+            assert flags["repaired"] == 1, (b, flags)
+        if b == 4:
+            assert flags["total_norm"] <= 1e3 * 1.0001
+        if not fx["skipped"][b]:
+            for i in range(nparam):
+                ref = fx[f"param/{b}/{i}"]
+                err = np.abs(ps[i] - ref).max()
+                worst = max(worst, float(err))
+                np.testing.assert_allclose(ps[i], ref, rtol=1e-5, atol=2e-6, err_msg=f"step {b} p{i}")
+    assert opt.steps_taken() == int(fx["opt_step/0"])
+    sd = opt.state_dict()
+    for i in range(nparam):
+        np.testing.assert_allclose(sd["state"][i]["exp_avg"].numpy(), fx[f"exp_avg/{i}"],
+                                   rtol=1e-4, atol=1e-7)
+        np.testing.assert_allclose(sd["state"][i]["exp_avg_sq"].numpy(), fx[f"exp_avg_sq/{i}"],
+                                   rtol=1e-4, atol=1e-10)
+    print(f"world {world}: max |param - reference| over 9 steps = {worst:.3e}")
+
+
+def test_device_tail_is_graph_capturable():
+    """No host synchronisation anywhere in the tail: the whole step captures
+    into a HIP graph and replays to the same result as eager."""
+    _, _, eager, nparam, _ = _replay()
+    _, _, graphed, _, _ = _replay(capture=True)
+    for b in eager:
+        assert eager[b][0]["skip"] == graphed[b][0]["skip"]
+        for i in range(nparam):
+            assert np.array_equal(eager[b][1][i], graphed[b][1][i]), (b, i)
+
+
+def test_device_noise_repair_stays_finite_and_close():
+    """Without injected noise the device draws its own normals: the repaired
+    values must be mean + O(0.1 std) and the step must match the injected run
+    everywhere the NaNs were not."""
+    import nsm_amd
+    torch.manual_seed(0)
+    p = torch.nn.Parameter(torch.zeros(20000, device=DEV))
+    opt = nsm_amd.FlatAdamW([p], lr=1e-3, weight_decay=0.0, max_grad_norm=1e9, sanitize=True)
+    g = torch.randn(20000, device=DEV) * 0.01
+    bad = torch.randperm(20000, device=DEV)[:500]
+    g[bad] = float("nan")
+    p.grad = g.clone()
+    opt.step()
+    fl = opt.last_flags()
+    assert fl["repaired"] == 1 and fl["skip"] == 0
+    rep = p.grad[bad]
+    assert torch.isfinite(rep).all()
+    ok = torch.ones(20000, dtype=torch.bool, device=DEV)
+    ok[bad] = False
+    mu, sd = g[ok].mean(), g[ok].std()
+    z = (rep - mu) / (sd * 0.1)
+    assert abs(z.mean().item()) < 0.2 and 0.8 < z.std().item() < 1.2

@@ -1,0 +1,58 @@
+"""Per-launch duration of the dominant convolution from a rocprofv3
+kernel_trace.csv, to cross-check bench.py's HIP-event `roofline.avg_launch_ms`.
+
+usage: python tools/conv6_trace.py {f32|bf16} TRACE_CSV OUT_JSON
+  f32 : conv6.conv.0 fwd (+ dgrad twin) = wino_input + Winograd GEMM
+        (gemm_f32_kernel grid 16x8x36 blocks) + wino_output, consecutive
+        dispatches; reports each kernel's mean and the span first-start ..
+        last-end (what a HIP event pair around the three launches measures)
+  bf16: the LDS-DMA implicit GEMM of conv6.conv.0 (grid 4x1024 blocks of 512)
+"""
+import csv
+import json
+import statistics
+import sys
+
+
+def grid_blocks(r):
+    return (int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]),
+            int(r["Grid_Size_Y"]) // int(r["Workgroup_Size_Y"]),
+            int(r["Grid_Size_Z"]) // int(r["Workgroup_Size_Z"]))
+
+
+KINDS = {
+    "f32": (lambda r: "gemm_f32_kernel" in r["Kernel_Name"]
+            and r["Kernel_Name"].count("RowsKLoader<128, 256>") == 2
+            and grid_blocks(r) == (16, 8, 36), True),
+    "bf16": (lambda r: "gemm_bf16_dma_kernel<256, 256" in r["Kernel_Name"]
+             and "ConvActDma" in r["Kernel_Name"] and grid_blocks(r)[:2] in ((4, 1024), (1024, 4)),
+             False),
+}
+
+kind, path, outp = sys.argv[1], sys.argv[2], sys.argv[3]
+match, triple = KINDS[kind]
+rows = list(csv.DictReader(open(path)))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # noqa: E731
+spans, parts = [], [[], [], []]
+for i, r in enumerate(rows):
+    if not match(r):
+        continue
+    if triple:
+        if i == 0 or i + 1 >= len(rows):
+            continue
+        a, c = rows[i - 1], rows[i + 1]
+        spans.append((int(c["End_Timestamp"]) - int(a["Start_Timestamp"])) / 1e6)
+        for k, x in enumerate((a, r, c)):
+            parts[k].append(dur(x))
+    else:
+        spans.append(dur(r))
+out = {"kind": kind, "launches": len(spans), "span_ms_mean": statistics.mean(spans),
+       "span_ms_median": statistics.median(spans)}
+if triple:
+    out.update({"wino_input_ms": statistics.mean(parts[0]), "gemm_ms": statistics.mean(parts[1]),
+                "wino_output_ms": statistics.mean(parts[2]),
+                "sum_of_kernels_ms": statistics.mean(parts[0]) + statistics.mean(parts[1])
+                + statistics.mean(parts[2])})
+json.dump(out, open(outp, "w"), indent=1)
+print(json.dumps(out, indent=1))

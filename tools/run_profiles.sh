@@ -1,13 +1,13 @@
 #!/bin/bash
 # Regenerate the profiles committed under profiles/<round>/ on a 1-GPU MI355X box:
-#   gpurun -- bash tools/run_profiles.sh r01
+#   gpurun -- bash tools/run_profiles.sh r02
 # For the default bench (B=8, 7x512x512, fp32) and configs[2] (B=64 bf16):
 # 1) kernel trace + stats;
 # 2) two separate PMC passes (FETCH_SIZE, WRITE_SIZE: they do not fit one pass)
 #    with kernel trace only, summarised by tools/pmc_traffic.py for the
 #    dominant kernel of each (bench.py reads the JSON into roofline.traffic).
 set -euo pipefail
-R=${1:-r01}
+R=${1:-r02}
 OUT=gpurun_out/prof_$R
 mkdir -p "$OUT" "profiles/$R"
 export TMPDIR=/tmp
@@ -26,10 +26,12 @@ run() {  # tag, extra bench args...
 }
 run f32
 cp "$(f trace_f32 run_kernel_stats.csv)" "profiles/$R/kernel_stats_bench_b8_f32.csv"
+python3 tools/conv6_trace.py f32 "$(f trace_f32 run_kernel_trace.csv)" "profiles/$R/trace_conv6_fwd_f32.json"
 python3 tools/pmc_traffic.py f32 "$OUT/fetch_csv_f32" "$OUT/write_csv_f32" \
-    "profiles/$R/traffic_wino_gemm_conv6.json"
+    "profiles/$R/traffic_conv6_fwd_f32.json"
 run bf16 --dtype bf16 --batch 64
 cp "$(f trace_bf16 run_kernel_stats.csv)" "profiles/$R/kernel_stats_bench_b64_bf16.csv"
+python3 tools/conv6_trace.py bf16 "$(f trace_bf16 run_kernel_trace.csv)" "profiles/$R/trace_conv6_fwd_bf16.json"
 python3 tools/pmc_traffic.py bf16 "$OUT/fetch_csv_bf16" "$OUT/write_csv_bf16" \
     "profiles/$R/traffic_conv6_fwd_bf16.json"
 cp -r "profiles/$R" "$OUT/profiles_copy"
