@@ -137,6 +137,8 @@ class CustomLoss(nn.Module):
         super().__init__()
         self.alpha = alpha
         self.l1 = L1Loss()
+        if vgg is not None and isinstance(vgg_weights, str) and vgg_weights == "auto":
+            vgg_weights = None           # an explicit vgg callable wins
         if vgg is None and isinstance(vgg_weights, str) and vgg_weights == "auto":
             vgg_weights = find_vgg19_checkpoint()
             if vgg_weights is None and not _VGG_WARNED:

@@ -243,7 +243,9 @@ def test_standalone_double_conv_vs_oracle(device, k, training):
     for name, prm in blk.named_parameters():
         r = sd[f"conv{k}." + name].grad
         if name.endswith("0.bias") or name.endswith("4.bias"):
-            assert (prm.grad.cpu() - r).abs().max().item() <= 1e-5, name
+            # feeds a train-mode BN: analytically 0, both sides are rounding
+            # noise of O(1) upstream gradients summed over B*H*W pixels
+            assert (prm.grad.cpu() - r).abs().max().item() <= 2e-3, name
         else:
             assert _rel(prm.grad.cpu(), r) <= GRAD_REL_L2, name
     assert _rel(x.grad.cpu(), xo.grad) <= GRAD_REL_L2

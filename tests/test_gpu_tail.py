@@ -68,9 +68,9 @@ def test_device_tail_matches_reference_train_model(world):
     assert opt.steps_taken() == int(fx["opt_step/0"])
     sd = opt.state_dict()
     for i in range(nparam):
-        np.testing.assert_allclose(sd["state"][i]["exp_avg"].numpy(), fx[f"exp_avg/{i}"],
+        np.testing.assert_allclose(sd["state"][i]["exp_avg"].cpu().numpy(), fx[f"exp_avg/{i}"],
                                    rtol=1e-4, atol=1e-7)
-        np.testing.assert_allclose(sd["state"][i]["exp_avg_sq"].numpy(), fx[f"exp_avg_sq/{i}"],
+        np.testing.assert_allclose(sd["state"][i]["exp_avg_sq"].cpu().numpy(), fx[f"exp_avg_sq/{i}"],
                                    rtol=1e-4, atol=1e-10)
     print(f"world {world}: max |param - reference| over 9 steps = {worst:.3e}")
 
@@ -88,8 +88,7 @@ def test_device_tail_is_graph_capturable():
 
 def test_device_noise_repair_stays_finite_and_close():
     """Without injected noise the device draws its own normals: the repaired
-    values must be mean + O(0.1 std) and the step must match the injected run
-    everywhere the NaNs were not."""
+    values must be distributed as mean + N(0,1) * 0.1 std."""
     import nsm_amd
     torch.manual_seed(0)
     p = torch.nn.Parameter(torch.zeros(20000, device=DEV))
