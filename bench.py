@@ -307,6 +307,57 @@ def run_dry(args):
 
 def run_train(args):
     world, rank, dev = init_dist(args)
+    res = train_measure(args, world, rank, dev)
+    if rank == 0 and world == 1 and not args.no_secondary:
+        res["secondary"] = secondary_configs(args, world, rank, dev)
+    C, H, W = args.in_ch, args.res, args.res
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(C, H, W)
+        if args.dtype == "bf16":
+            res["cpu_baseline"]["sample"] += " (fp32: the reference's CPU path)"
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def _summary(r):
+    """The fields of a secondary measurement kept in the headline JSON line."""
+    roof = r["roofline"]
+    return {"metric": r["metric"], "value": r["value"], "unit": r["unit"],
+            "ms_per_step": r["ms_per_step"], "steps": r["steps"], "warmup": r["warmup"],
+            "dtype": r["dtype"], "config": r["config"],
+            "model_tflops_per_s": r["model_tflops_per_s"],
+            "roofline": {k: roof.get(k) for k in ("kernel", "bound", "achieved", "peak", "unit",
+                                                  "frac", "executed_frac", "avg_launch_ms",
+                                                  "traffic", "traffic_source")},
+            "stages": r["stages"]}
+
+
+def secondary_configs(args, world, rank, dev):
+    """The other BASELINE.json configs measured in the same run (so the
+    driver's record carries them): configs[2] (B=64 bf16 train step, the
+    per-GPU share of configs[3]'s batch 512 on 8 GPUs), configs[4] (1080p
+    hipGraph inference, fp32 and bf16) and configs[0] (1x7x256x256 eval)."""
+    import argparse as _ap
+    out = []
+    base = dict(vars(args))
+    for kw in (dict(workload="train", dtype="bf16", batch=64, steps=max(10, args.steps // 5),
+                    warmup=3),
+               dict(workload="infer1080", dtype="bf16", batch=1, steps=100, warmup=5),
+               dict(workload="infer1080", dtype="f32", batch=1, steps=50, warmup=5),
+               dict(workload="infer256", dtype="f32", batch=1, steps=100, warmup=5)):
+        a = _ap.Namespace(**{**base, **kw, "vgg": False})
+        torch.cuda.empty_cache()
+        r = train_measure(a, world, rank, dev) if a.workload == "train" else \
+            infer_measure(a, world, rank, dev)
+        out.append(_summary(r))
+    torch.cuda.empty_cache()
+    return out
+
+
+def train_measure(args, world, rank, dev):
     import nsm_amd
     from nsm_amd import ops as nops
     from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
@@ -412,10 +463,17 @@ def run_train(args):
         vms = mean_ms(vgg_evs)
         res["vgg_perceptual"] = {"ms": round(vms, 3), "direct_equiv_gflop": round(vfl / 1e9, 1),
                                  "tflops": round(vfl / (vms * 1e-3) / 1e12, 2)}
+    return res
+
+
+def run_infer(args):
+    """configs[4]: 1x7x1080x1920 eval forward, hipGraph-captured (replicas only
+    for N > 1: frames are independent, no collective); configs[0] at 256x256."""
+    world, rank, dev = init_dist(args)
+    res = infer_measure(args, world, rank, dev)
+    H, W = (1080, 1920) if args.workload == "infer1080" else (256, 256)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(C, H, W)
-        if bf16:
-            res["cpu_baseline"]["sample"] += " (fp32: the reference's CPU path)"
+        res["cpu_baseline"] = cpu_baseline(args.in_ch, H, W, frames=1, reps=3, train=False)
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:
@@ -423,16 +481,14 @@ def run_train(args):
         dist.destroy_process_group()
 
 
-def run_infer(args):
-    """configs[4]: 1x7x1080x1920 eval forward, hipGraph-captured (replicas only
-    for N > 1: frames are independent, no collective)."""
-    world, rank, dev = init_dist(args)
+def infer_measure(args, world, rank, dev):
     import nsm_amd
     from nsm_amd import ops as nops
     from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
 
     torch.manual_seed(1234 + rank)
-    B, C, H, W = args.batch, args.in_ch, 1080, 1920
+    B, C = args.batch, args.in_ch
+    H, W = (1080, 1920) if args.workload == "infer1080" else (256, 256)
     bf16 = args.dtype == "bf16"
     model = nsm_amd.Unet(in_ch=C, dropout_rate=0.2).to(dev).eval()
     if bf16:
@@ -467,8 +523,9 @@ def run_infer(args):
         roof = dominant_roofline(B, H, W, mean_ms(evs), mean_ms(gevs), len(evs), WINO_TILE)
     roof.update({"traffic": None, "traffic_source": None})
     frames = world * B * args.steps
+    cfg = "configs[4]" if args.workload == "infer1080" else "configs[0]"
     res = {
-        "metric": "frames/sec 7x1080x1920 U-Net inference (eval fwd, hipGraph)",
+        "metric": f"frames/sec {C}x{H}x{W} U-Net inference (eval fwd, hipGraph)",
         "value": round(frames / elapsed, 3),
         "unit": "frames/s",
         "n_gpus": world,
@@ -480,7 +537,7 @@ def run_infer(args):
         "vs_baseline": None,
         "dtype": "bf16" if bf16 else "f32",
         "data": "synthetic (x~N(0,1)), random-init weights, eval-mode BN (running stats)",
-        "config": {"workload": f"configs[4]: batch={B}/GPU {C}x{H}x{W} {args.dtype} eval forward, "
+        "config": {"workload": f"{cfg}: batch={B}/GPU {C}x{H}x{W} {args.dtype} eval forward, "
                                "one hipGraph replay per step",
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"replicas{world}"},
@@ -488,13 +545,7 @@ def run_infer(args):
         "roofline": roof,
         "stages": stage_table(work, times, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(C, H, W, frames=1, reps=3, train=False)
-    if rank == 0:
-        print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    return res
 
 
 def _free_port():
@@ -529,7 +580,9 @@ def main():
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (train 8, infer 1)")
     ap.add_argument("--in-ch", type=int, default=7)
     ap.add_argument("--res", type=int, default=512)
-    ap.add_argument("--workload", choices=["train", "infer1080"], default="train")
+    ap.add_argument("--workload", choices=["train", "infer1080", "infer256"], default="train")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="train, N=1: skip the other configs measured after the headline one")
     ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32",
                     help="bf16: configs[2] (use --batch 64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")

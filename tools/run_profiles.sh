@@ -15,11 +15,11 @@ f() { find "$OUT/$1" -name "$2" -print -quit; }
 run() {  # tag, extra bench args...
   local tag=$1; shift
   timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_$tag" -o run -- \
-      python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline "$@" > "$OUT/bench_trace_$tag.log" 2>&1
+      python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-secondary "$@" > "$OUT/bench_trace_$tag.log" 2>&1
   timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch_$tag" -o run -- \
-      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > "$OUT/bench_fetch_$tag.log" 2>&1
+      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary "$@" > "$OUT/bench_fetch_$tag.log" 2>&1
   timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write_$tag" -o run -- \
-      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > "$OUT/bench_write_$tag.log" 2>&1
+      python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-secondary "$@" > "$OUT/bench_write_$tag.log" 2>&1
   mkdir -p "$OUT/fetch_csv_$tag" "$OUT/write_csv_$tag"
   cp "$(f fetch_$tag run_counter_collection.csv)" "$OUT/fetch_csv_$tag/run_counter_collection.csv"
   cp "$(f write_$tag run_counter_collection.csv)" "$OUT/write_csv_$tag/run_counter_collection.csv"
