@@ -101,9 +101,10 @@ def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=128, tile=4, passes=3):
         h, w = res[k]
         px = B * h * w
         f = 2.0 * px * (ci * ci * 9 + ci * co)
-        T = B * ((h + tile - 1) // tile) * ((w + tile - 1) // tile)
         cp = (ci + 31) // 32 * 32
-        f3 = 2.0 * (tile + 2) ** 2 * T * ci * ci if cp >= wino_min else 18.0 * px * ci * ci
+        m = tile(cp, h, w) if callable(tile) else tile
+        T = B * ((h + m - 1) // m) * ((w + m - 1) // m)
+        f3 = 2.0 * (m + 2) ** 2 * T * ci * ci if cp >= wino_min else 18.0 * px * ci * ci
         f1 = 2.0 * px * ci * co
         by = ((ci + ci) * px + 9 * ci * ci + (ci + co) * px + ci * co) * bytes_per
         out[f"conv{k}"] = (passes * f, passes * (f3 + f1), passes * by)
@@ -360,7 +361,7 @@ def secondary_configs(args, world, rank, dev):
 def train_measure(args, world, rank, dev):
     import nsm_amd
     from nsm_amd import ops as nops
-    from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
+    from nsm_amd.unet import WINOGRAD_MIN_CHANNELS, wino_tile
 
     torch.manual_seed(1234 + rank)
     B, C, H, W = args.batch, args.in_ch, args.res, args.res
@@ -426,9 +427,9 @@ def train_measure(args, world, rank, dev):
                                 else (None, None))
         roof.update({"traffic": traffic, "traffic_source": traffic_src})
     else:
-        work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE)
+        work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=wino_tile)
         traffic, traffic_src = load_traffic("traffic_conv6_fwd_f32.json")
-        roof = dominant_roofline(B, H, W, kern_ms, gemm_ms, len(evs), WINO_TILE)
+        roof = dominant_roofline(B, H, W, kern_ms, gemm_ms, len(evs), wino_tile(1024, H // 8, W // 8))
         roof.update({"traffic": traffic, "traffic_source": traffic_src})
 
     frames = world * B * args.steps
@@ -484,7 +485,7 @@ def run_infer(args):
 def infer_measure(args, world, rank, dev):
     import nsm_amd
     from nsm_amd import ops as nops
-    from nsm_amd.unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
+    from nsm_amd.unet import WINOGRAD_MIN_CHANNELS, wino_tile
 
     torch.manual_seed(1234 + rank)
     B, C = args.batch, args.in_ch
@@ -519,8 +520,8 @@ def infer_measure(args, world, rank, dev):
         work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30, passes=1)
         roof = direct_roofline(B, H, W, mean_ms(evs), len(evs))
     else:
-        work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=WINO_TILE, passes=1)
-        roof = dominant_roofline(B, H, W, mean_ms(evs), mean_ms(gevs), len(evs), WINO_TILE)
+        work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=wino_tile, passes=1)
+        roof = dominant_roofline(B, H, W, mean_ms(evs), mean_ms(gevs), len(evs), wino_tile(1024, H // 8, W // 8))
     roof.update({"traffic": None, "traffic_source": None})
     frames = world * B * args.steps
     cfg = "configs[4]" if args.workload == "infer1080" else "configs[0]"

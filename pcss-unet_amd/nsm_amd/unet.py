@@ -32,10 +32,28 @@ SLOPE = 0.2
 # 3x3 convolutions with at least this many (padded) input channels use the
 # Winograd F(m x m, 3x3) path for forward, input- and weight-gradient
 # (MFMA-bound layers); NSM_WINOGRAD=0 disables it (direct implicit GEMM
-# everywhere), NSM_WINO_TILE=2 selects F(2x2,3x3) instead of F(4x4,3x3).
+# everywhere). The tile m of F(m x m, 3x3) per layer: wino_tile(); NSM_WINO_TILE=2/4/6
+# forces one tile everywhere.
 WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "128"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
-WINO_TILE = int(os.environ.get("NSM_WINO_TILE", "4"))
+_WINO_ENV = os.environ.get("NSM_WINO_TILE", "")
+WINO_TILE = int(_WINO_ENV) if _WINO_ENV else 4   # the tile of the VGG stack
+
+
+def wino_tile(cin_p, H, W):
+    """F(m x m, 3x3) tile of a Winograd layer (cin_p channels at H x W).
+
+    F(6x6) needs 64 GEMMs per 36 outputs, F(4x4) 36 per 16: F(6x6) when its
+    MFMA work, tiling padding included, is below 0.9x F(4x4)'s (measured B=8
+    7x512^2 fp32 step: conv6 5.67 -> 5.29 ms, conv7 6.02 -> 5.45, conv8 3.28 ->
+    3.00, but conv5 at 32x32, where both tilings issue the same work, 0.86 ->
+    0.93). Fwd, dgrad and wgrad of a layer share the tile (the wgrad reuses V).
+    NSM_WINO_TILE=2/4/6 forces one tile."""
+    if _WINO_ENV:
+        return int(_WINO_ENV)
+    f6 = 64 * -(-H // 6) * -(-W // 6)
+    f4 = 36 * -(-H // 4) * -(-W // 4)
+    return 6 if f6 < 0.9 * f4 else 4
 # Materialise the activated 3x3 output A1 = lrelu(BN(Y1))*mask once (one
 # streaming pass) so the 1x1 conv and its weight gradient run prologue-free on
 # the LDS-DMA GEMMs, instead of re-applying BN+LReLU+mask in both operand
@@ -326,8 +344,9 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
     V = None
     dtype = X.dtype
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
-        U1 = ops.wino_weight(c0.weight.detach(), cip, cip, flip=False, tile=WINO_TILE)
-        Y1, V = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tile=WINO_TILE, tag=name + ".conv.0.fwd",
+        tile = wino_tile(cip, H, W)
+        U1 = ops.wino_weight(c0.weight.detach(), cip, cip, flip=False, tile=tile)
+        Y1, V = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tile=tile, tag=name + ".conv.0.fwd",
                                  keep_v=True)
         part1 = ops.bn_partials(Y1) if training else None
     else:
@@ -381,7 +400,8 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
                        pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
     dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias], g[c0.bias])
     if s.V is not None:
-        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=WINO_TILE,
+        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight],
+                               tile=wino_tile(s.cip, H, W),
                                tag=name + ".conv.0.wgrad")
         s.V = None
     else:
@@ -389,8 +409,9 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
     if not need_dx:
         return None
     if s.cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
-        U1d = ops.wino_weight(c0.weight.detach(), s.cip, s.cip, flip=True, tile=WINO_TILE)
-        return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=WINO_TILE,
+        tile = wino_tile(s.cip, H, W)
+        U1d = ops.wino_weight(c0.weight.detach(), s.cip, s.cip, flip=True, tile=tile)
+        return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=tile,
                                 tag=name + ".conv.0.dgrad")
     w1d = ops.pack_conv_weight(c0.weight.detach(), s.cip, s.cip, ops.PACK_DGRAD, dtype)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")

@@ -20,10 +20,13 @@ def grid_blocks(r):
             int(r["Grid_Size_Z"]) // int(r["Workgroup_Size_Z"]))
 
 
+# conv6.conv.0's Winograd GEMM at B=8, 64x64, 1024 channels: F(6x6) (the
+# default there) grid 8x8x64 blocks, F(4x4) 16x8x36
+CONV6_GRIDS = ((8, 8, 64), (16, 8, 36))
 KINDS = {
     "f32": (lambda r: "gemm_f32_kernel" in r["Kernel_Name"]
             and r["Kernel_Name"].count("RowsKLoader<128, 256>") == 2
-            and grid_blocks(r) == (16, 8, 36), True),
+            and grid_blocks(r) in CONV6_GRIDS, True),
     "bf16": (lambda r: "gemm_bf16_dma_kernel<256, 256" in r["Kernel_Name"]
              and "ConvActDma" in r["Kernel_Name"] and grid_blocks(r)[:2] in ((4, 1024), (1024, 4)),
              False),

@@ -9,8 +9,8 @@ WRITE_SIZE (KB) is exact for 16-B/lane stores and reported as measured.
 
 usage: python tools/pmc_traffic.py {f32|bf16} FETCH_DIR WRITE_DIR OUT_JSON
   f32 : conv6.conv.0 forward as a whole = the three consecutive dispatches
-        wino_input -> Winograd F(4x4,3x3) batched GEMM (grid 16x8x36 blocks,
-        B=8) -> wino_output (the dgrad twin has the same shapes and is
+        wino_input -> Winograd batched GEMM (F(6x6,3x3): grid 8x8x64 blocks,
+        F(4x4): 16x8x36; B=8) -> wino_output (the dgrad twin has the same shapes and is
         averaged in); algorithmic bytes = x + y + weights (direct conv)
   bf16: LDS-DMA implicit GEMM of conv6.conv.0 fwd (+ its dgrad twin, same
         shape), gemm_bf16_dma_kernel<256,256>, grid 4x1024 blocks of 512, B=64
@@ -24,13 +24,14 @@ KINDS = {
     "f32": dict(
         match=lambda n: n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n
         and "gemm_f32_kernel" in n,
-        grid=16 * 8 * 36 * 256, triple=True,
+        grid=(8 * 8 * 64 * 256, 16 * 8 * 36 * 256), triple=True,
         alg=(2 * B8_CONV6 * 1024 + 9 * 1024 * 1024 + 1024) * 4,
         desc="conv6.conv.0 fwd (+ dgrad twin), B=8: wino_input + gemm_f32_kernel<128,128,2,2,"
-             "RowsKLoader<128,256>x2,EpiStore> grid 16x8x36 + wino_output"),
+             "RowsKLoader<128,256>x2,EpiStore> (F(6x6): grid 8x8x64; F(4x4): 16x8x36) + "
+             "wino_output"),
     "bf16": dict(
         match=lambda n: "gemm_bf16_dma_kernel<256, 256" in n and "ConvActDma" in n,
-        grid=4 * 1024 * 512, triple=False,
+        grid=(4 * 1024 * 512,), triple=False,
         alg=(2 * 262144 * 1024 + 9 * 1024 * 1024) * 2,
         desc="gemm_bf16_dma_kernel<256,256,2,4,2,...,ConvActDma,RowsKDma,EpiStoreB> grid 4x1024 "
              "(implicit-GEMM 3x3 conv6.conv.0 fwd + dgrad, M=262144 N=1024 K=9216, B=64)"),
@@ -51,7 +52,7 @@ def per_launch(d, counter, k):
     rs = rows(d, counter)
     vals, names = [], set()
     for did, (name, grid, v) in sorted(rs.items()):
-        if not (k["match"](name) and grid == str(k["grid"])):
+        if not (k["match"](name) and grid in {str(g) for g in k["grid"]}):
             continue
         if k["triple"]:
             if did - 1 not in rs or did + 1 not in rs:

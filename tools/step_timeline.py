@@ -1,0 +1,28 @@
+#!/usr/bin/env python3
+"""One train step's launches from a rocprofv3 kernel_trace.csv (steps end at
+the AdamW kernel): duration, grid (blocks), short name; then totals per kernel
+family. usage: python tools/step_timeline.py TRACE_CSV [step_index_from_end=1]"""
+import collections
+import csv
+import re
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+k = int(sys.argv[2]) if len(sys.argv) > 2 else 1
+ends = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
+a, b = ends[-1 - k] + 1, ends[-k] + 1
+fam = collections.Counter()
+tot = 0.0
+for r in rows[a:b]:
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    tot += d
+    n = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").replace("nsm::", "")
+    g = (int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]), int(r["Grid_Size_Y"]) //
+         int(r["Workgroup_Size_Y"]), int(r["Grid_Size_Z"]) // int(r["Workgroup_Size_Z"]))
+    print(f"{d:8.1f} {str(g):18s} {n[:110]}")
+    fam[re.sub(r"<.*", "", n)] += d
+span = (int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
+print(f"\nkernels {tot:.0f} us, span {span:.0f} us, launches {b - a}")
+for n, d in fam.most_common():
+    print(f"{d:9.1f} us {100 * d / tot:5.1f}%  {n}")

@@ -6,7 +6,9 @@ Finite interpolation points p_0..p_{n-2} plus the point at infinity, n = m + 2:
   G[j][k]   = p_j^k / prod_{l!=j}(p_j-p_l),  G[n-1][k] = [k == 2]
   B^T[j]    = coefficients (x^0..x^{n-1}) of prod_{l!=j}(x - p_l);  B^T[n-1] = of prod_l (x - p_l)
 F(2x2): points (0, 1, -1); F(4x4): points (0, 1, -1, 1/2, -2), which in fp32 gives
-~3x less error than the textbook (0, +-1, +-2) set (measured: tools/wino_coeffs.py --check).
+~3x less error than the textbook (0, +-1, +-2) set (measured: tools/wino_coeffs.py --check);
+F(6x6): points (0, +-1, +-2, +-1/2): 8.8e-6 rms vs 2.9e-6 (F4) and 4.0e-7 (direct) on a
+512-channel fp32 layer with O(1) outputs (the lowest of the 7-point sets tried).
 Prints the C++ tables used in pcss-unet_amd/csrc/nsm_conv.hip (WinoMats<m>).
 """
 import sys
@@ -14,7 +16,8 @@ from fractions import Fraction as Fr
 
 import numpy as np
 
-POINTS = {2: [Fr(0), Fr(1), Fr(-1)], 4: [Fr(0), Fr(1), Fr(-1), Fr(1, 2), Fr(-2)]}
+POINTS = {2: [Fr(0), Fr(1), Fr(-1)], 4: [Fr(0), Fr(1), Fr(-1), Fr(1, 2), Fr(-2)],
+          6: [Fr(0), Fr(1), Fr(-1), Fr(2), Fr(-2), Fr(1, 2), Fr(-1, 2)]}
 
 
 def polymul(a, b):
@@ -65,7 +68,7 @@ def cxx(name, M):
 
 
 if __name__ == "__main__":
-    for m in (2, 4):
+    for m in (2, 4, 6):
         assert check(m) < 1e-12, m
         AT, G, BT = mats(m)
         print(f"// F({m}x{m},3x3), points {[str(v) for v in POINTS[m]]} + inf")
