@@ -52,6 +52,24 @@ int nsm_pack_conv_weight(const float* w, int cout, int cin, int ksize, int cout_
                          int mode, float* out, void* stream);
 int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
 
+/* All weight layouts of one training step in ONE launch (replaces the per-layer
+ * nsm_pack_conv_weight / nsm_pack_conv_weight_bf16 / nsm_wino_weight / nsm_pad_vec
+ * calls). kind 0: pack fp32, 1: pack bf16, a = {cout, cin, taps, cout_p, cin_p,
+ * mode}; kind 2: Winograd U, a = {cout, cin, n_p, k_p, flip, tile}; kind 3: pad
+ * vector, a = {n, n_p}. `base` = the job's first item in the launch (jobs in
+ * ascending base order, consecutive); nsm_prep_items() = the job's extent in
+ * the launch (its item count rounded up to whole 2048-item blocks: add it to
+ * get the next base; total_items = the sum). jobs_dev: a device copy. */
+typedef struct {
+  int kind;
+  int a[7];
+  long long base;
+  const float* src;
+  void* dst;
+} NsmPrepJob;
+long long nsm_prep_items(const NsmPrepJob* job);
+int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items, void* stream);
+
 /* ---- convolution as MFMA implicit GEMM (fp32 in, fp32 accumulate) ----------
  * nsm_conv_fwd: y[p][co] = bias[co] + sum_{tap,ci} pro(x[p+off(tap)][ci]) * W
  *   Replaces F.conv2d 3x3 pad 1 / 1x1 of DoubleConv (Unetmodel.py:21,26) and,
@@ -78,13 +96,13 @@ int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, int cin_p, 
                        float slope, float* stats, void* stream);
 
 /* Winograd F(m x m, 3x3) 3x3 convolution (same padding 1) for deep layers,
- * tile m in {2, 4}, alpha = m + 2, T = B*ceil(H/m)*ceil(W/m) tiles:
+ * tile m in {2, 4, 6}, alpha = m + 2, T = B*ceil(H/m)*ceil(W/m) tiles:
  * nsm_wino_weight transforms w[co][ci][3][3] into U[alpha^2][n_p][k_p]
  * (flip=0: forward, n=co, k=ci; flip=1: input-gradient, n=ci, k=co, filter
  * rotated 180 deg); nsm_conv3x3_wino then computes y = conv(x, W) + bias
  * through alpha^2 batched MFMA GEMMs, using nsm_wino_ws() floats of workspace.
  * Replaces the same F.conv2d 3x3 / ConvolutionBackward dgrad as nsm_conv_fwd
- * (Unetmodel.py:21) with 2.25x (m=2) or 4x (m=4) fewer multiplies. */
+ * (Unetmodel.py:21) with 2.25x (m=2), 4x (m=4) or 5.06x (m=6) fewer multiplies. */
 size_t nsm_wino_ws(int B, int H, int W, int cin_p, int cout_p, int tile);
 int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k_p, int flip, int tile,
                     float* U, void* stream);
@@ -274,6 +292,11 @@ int nsm_nchw_to_nhwc(const float* x, int B, int C, int H, int W, void* y, int cp
 int nsm_nhwc_to_nchw(const void* z, int ldz, int B, int C, int H, int W, float* x, int dtype,
                      void* stream);
 int nsm_range_flag(const float* o, int64_t n, float lo, float hi, int* flag, void* stream);
+/* Dropout2d masks (Unetmodel.py:24,61) of all blocks of one forward in one
+ * launch: job j writes out[off_j + b*cp_j + c] = (u < keep_j) / keep_j for
+ * c < c_j and 0 for c_j <= c < cp_j, u ~ U[0,1) from a counter-based hash of
+ * (seed, j, b, c). desc (device) = njobs x {off, c, cp, keep as float bits}. */
+int nsm_dropout_masks(const int* desc, int njobs, int B, uint64_t seed, float* out, void* stream);
 
 /* ---- bf16 convolutions (BASELINE config 3) ---------------------------------
  * Same contracts as nsm_pack_conv_weight / nsm_conv_fwd_stats / nsm_conv_wgrad

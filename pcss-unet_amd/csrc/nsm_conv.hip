@@ -1117,6 +1117,90 @@ __global__ void __launch_bounds__(256) wino_wgrad_out_kernel(const float* __rest
     for (int e = 0; e < 3; ++e) out[r * 3 + e] = o[r][e];
 }
 
+// ---- all weight layouts of one step in ONE launch ----------------------------
+// Jobs (include/nsm.h NsmPrepJob): 0 = pack fp32, 1 = pack bf16 (a[] = cout,
+// cin, taps, cout_p, cin_p, mode), 2 = Winograd U (a[] = cout, cin, n_p, k_p,
+// flip, tile), 3 = pad vector (a[] = n, n_p). Items are output elements
+// (pack, pad) or (n, k) filter pairs (Winograd); `base` is the job's first
+// item in the launch-wide numbering (ascending), found by binary search.
+__host__ __device__ inline long long nsm_prep_items_dev(const NsmPrepJob& j) {
+  switch (j.kind) {
+    case 0:
+    case 1: return (long long)j.a[3] * j.a[4] * j.a[2];
+    case 2: return (long long)j.a[2] * j.a[3];
+    case 3: return j.a[1];
+    default: return -1;
+  }
+}
+
+template <int MT>
+__device__ __forceinline__ void wino_weight_item(const float* __restrict__ w, int cout, int cin,
+                                                 int n_p, int k_p, int flip, float* __restrict__ U,
+                                                 int idx) {
+  constexpr int A = MT + 2;
+  const int k = idx % k_p, n = idx / k_p;
+  const int co = flip ? k : n, ci = flip ? n : k;
+  float g[3][3];
+  const bool ok = co < cout && ci < cin;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const int sa = flip ? 2 - a : a, sb = flip ? 2 - b : b;
+      g[a][b] = ok ? w[((size_t)co * cin + ci) * 9 + sa * 3 + sb] : 0.f;
+    }
+  float u[A][A];
+  wmat2<CG<MT>>(g, u);
+  const size_t plane = (size_t)n_p * k_p;
+#pragma unroll
+  for (int a = 0; a < A; ++a)
+#pragma unroll
+    for (int b = 0; b < A; ++b) U[(a * A + b) * plane + (size_t)n * k_p + k] = u[a][b];
+}
+
+constexpr int PREP_ITEMS = 2048;  // items per block: 8 per thread
+
+// blockIdx -> job by a (uniform) binary search over the jobs' first blocks
+// (job.base / PREP_ITEMS: every job starts on a block boundary, see
+// nsm_prep_items), then the block's items of that job, coalesced
+__global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __restrict__ jobs,
+                                                           int njobs) {
+  const long long blk0 = (long long)blockIdx.x * PREP_ITEMS;
+  int lo = 0, hi = njobs - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (jobs[mid].base <= blk0) lo = mid; else hi = mid - 1;
+  }
+  const NsmPrepJob& j = jobs[lo];
+  const long long items = nsm_prep_items_dev(j);
+  for (int r = 0; r < PREP_ITEMS / 256; ++r) {
+    const long long li = blk0 - j.base + r * 256 + threadIdx.x;
+    if (li >= items) break;
+    const int idx = (int)li;
+    if (j.kind <= 1) {
+      const int cout = j.a[0], cin = j.a[1], taps = j.a[2], cout_p = j.a[3], cin_p = j.a[4];
+      float v;
+      if (j.a[5] == NSM_PACK_FWD) {
+        const int ci = idx % cin_p, t = idx / cin_p, tap = t % taps, co = t / taps;
+        v = (co < cout && ci < cin) ? j.src[((size_t)co * cin + ci) * taps + tap] : 0.f;
+      } else {
+        const int co = idx % cout_p, t = idx / cout_p, tap = t % taps, ci = t / taps;
+        v = (co < cout && ci < cin) ? j.src[((size_t)co * cin + ci) * taps + (taps - 1 - tap)]
+                                    : 0.f;
+      }
+      if (j.kind == 0) ((float*)j.dst)[idx] = v;
+      else ((bf16_t*)j.dst)[idx] = (bf16_t)(pack_bf2(v, 0.f) & 0xFFFFu);
+    } else if (j.kind == 2) {
+      float* U = (float*)j.dst;
+      if (j.a[5] == 6) wino_weight_item<6>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx);
+      else if (j.a[5] == 4) wino_weight_item<4>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx);
+      else wino_weight_item<2>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx);
+    } else {
+      ((float*)j.dst)[idx] = idx < j.a[0] ? j.src[idx] : 0.f;
+    }
+  }
+}
+
 template <int BM, int BN, int WM, int WN>
 static int launch_wino_gemm(const RowsKP& ap, const RowsKP& bp, const EpiStoreP& ep, int M, int N,
                             int K, int nb, hipStream_t s) {
@@ -1158,6 +1242,25 @@ extern "C" int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* str
   hipLaunchKernelGGL(pad_vec_kernel, dim3(ceil_div(n_p, 256)), dim3(256), 0, as_stream(stream), v,
                      n, n_p, out);
   NSM_LAUNCH_CHECK("pad_vec");
+  return 0;
+}
+
+// the job's item count ROUNDED UP to whole blocks of the launch, i.e. the
+// amount to advance `base` by (jobs start on block boundaries)
+extern "C" long long nsm_prep_items(const NsmPrepJob* j) {
+  if (!j) return -1;
+  const long long n = nsm_prep_items_dev(*j);
+  return n < 0 ? -1 : (n + PREP_ITEMS - 1) / PREP_ITEMS * PREP_ITEMS;
+}
+
+extern "C" int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items,
+                                void* stream) {
+  NSM_CHECK_ARG(jobs_dev && njobs > 0 && total_items > 0 && total_items % PREP_ITEMS == 0,
+                "prep_weights: bad args");
+  NSM_CHECK_ARG(total_items / PREP_ITEMS < (1ll << 31), "prep_weights: too many items");
+  hipLaunchKernelGGL(prep_weights_kernel, dim3((unsigned)(total_items / PREP_ITEMS)), dim3(256), 0,
+                     as_stream(stream), jobs_dev, njobs);
+  NSM_LAUNCH_CHECK("prep_weights");
   return 0;
 }
 

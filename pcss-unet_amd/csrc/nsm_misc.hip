@@ -65,9 +65,51 @@ __global__ void __launch_bounds__(256) range_flag_kernel(const float* __restrict
   if (__any(bad) && (threadIdx.x & 63) == 0) flag[0] = 1;
 }
 
+// Dropout2d masks of every block of one forward in ONE launch: job j covers
+// rows [B] x channels [cp_j] at offset off_j of `out`; m = (u < keep) / keep
+// for c < c_real, 0 in the padded channels; u from a counter-based hash of
+// (seed, job, b, c). desc[j] = {offset, c_real, cp, keep (float bits)}.
+__device__ __forceinline__ uint32_t hash32(uint64_t x) {
+  x ^= x >> 33;
+  x *= 0xFF51AFD7ED558CCDull;
+  x ^= x >> 33;
+  x *= 0xC4CEB9FE1A85EC53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+__global__ void __launch_bounds__(256) dropout_masks_kernel(const int* __restrict__ desc, int njobs,
+                                                            int B, uint64_t seed,
+                                                            float* __restrict__ out) {
+  const int j = blockIdx.y;
+  if (j >= njobs) return;
+  const int off = desc[4 * j], creal = desc[4 * j + 1], cp = desc[4 * j + 2];
+  const float keep = __int_as_float(desc[4 * j + 3]);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * cp; i += gridDim.x * blockDim.x) {
+    const int c = i % cp, b = i / cp;
+    float v = 0.f;
+    if (c < creal) {
+      const uint32_t h = hash32(seed + 0x9E3779B97F4A7C15ull * (uint64_t)(((uint64_t)j << 40) |
+                                                                      ((uint64_t)b << 20) | c));
+      const float u = (float)(h >> 8) * (1.f / 16777216.f);  // [0, 1)
+      v = u < keep ? 1.f / keep : 0.f;
+    }
+    out[off + i] = v;
+  }
+}
+
 }  // namespace nsm
 
 using namespace nsm;
+
+extern "C" int nsm_dropout_masks(const int* desc, int njobs, int B, uint64_t seed, float* out,
+                                 void* stream) {
+  NSM_CHECK_ARG(desc && out && njobs > 0 && B > 0, "dropout_masks: bad args");
+  hipLaunchKernelGGL(dropout_masks_kernel, dim3(8, njobs), dim3(256), 0, as_stream(stream), desc,
+                     njobs, B, seed, out);
+  NSM_LAUNCH_CHECK("dropout_masks");
+  return 0;
+}
 
 extern "C" int nsm_nchw_to_nhwc(const float* x, int B, int C, int H, int W, void* y, int cp,
                                 int ldy, int dtype, void* stream) {

@@ -91,6 +91,9 @@ _SIGS = {
     "nsm_nchw_to_nhwc": (I, [P, I, I, I, I, P, I, I, I, P]),
     "nsm_nhwc_to_nchw": (I, [P, I, I, I, I, I, P, I, P]),
     "nsm_range_flag": (I, [P, L, F, F, P, P]),
+    "nsm_dropout_masks": (I, [P, I, I, U64, P, P]),
+    "nsm_prep_items": (L, [P]),
+    "nsm_prep_weights": (I, [P, I, L, P]),
 }
 
 

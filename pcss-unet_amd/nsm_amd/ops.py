@@ -217,7 +217,7 @@ def reduce_chunks(M, C):
 
 class BNState:
     """Per-BN tensors the backward needs (all [C_padded])."""
-    __slots__ = ("scale", "shift", "mean", "invstd", "part", "nchunk", "gamma")
+    __slots__ = ("scale", "shift", "mean", "invstd", "part", "nchunk", "gamma", "beta")
 
     def __init__(self, C, device):
         self.scale = empty(C, device=device)
@@ -227,6 +227,7 @@ class BNState:
         self.part = None
         self.nchunk = 0
         self.gamma = None
+        self.beta = None
 
 
 def bn_partials(y):
@@ -256,9 +257,10 @@ def merged(part, M, C):
     return part._merged
 
 
-def _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, gamma):
+def _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, gamma, beta=None):
     part = merged(part, M, C)
-    beta = pad_vec(bn_mod.bias.detach(), C)
+    if beta is None:
+        beta = pad_vec(bn_mod.bias.detach(), C)
     track = bn_mod.track_running_stats
     call("nsm_bn_finalize_train", ptr(part.buf), part.nchunk, part.rpc, M, C, c_real, ptr(gamma),
          ptr(beta), ptr(bn_mod.running_mean if track else None),
@@ -267,17 +269,19 @@ def _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, gamma):
          ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift), stream())
 
 
-def bn_train(y, bn_mod, c_real, momentum, eps, n_updates=1, part=None):
+def bn_train(y, bn_mod, c_real, momentum, eps, n_updates=1, part=None, gamma=None, beta=None):
     """Train-mode BN: batch statistics of y [M, C] (given as fused GEMM
     partials, or computed here) + running-stat update in place on the module's
-    buffers -> BNState with scale/shift for the fused apply."""
+    buffers -> BNState with scale/shift for the fused apply. gamma / beta: the
+    affine parameters padded to C (pad_vec'd here when not given)."""
     M, C = y.shape
     if part is None:
         part = bn_partials(y)
     st = BNState(C, y.device)
     st.part, st.nchunk = part, part.nchunk
-    st.gamma = pad_vec(bn_mod.weight.detach(), C)
-    _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, st.gamma)
+    st.gamma = gamma if gamma is not None else pad_vec(bn_mod.weight.detach(), C)
+    st.beta = beta if beta is not None else pad_vec(bn_mod.bias.detach(), C)
+    _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, st.gamma, st.beta)
     return st
 
 
@@ -285,13 +289,14 @@ def bn_running_update(st, M, C, bn_mod, c_real, momentum, eps, n_updates=1):
     """Re-apply the running-stat update from saved partials (the conv5
     checkpoint recompute in the reference's backward)."""
     scratch = BNState(C, st.part.buf.device)
-    _finalize(st.part, M, C, bn_mod, c_real, momentum, eps, n_updates, scratch, st.gamma)
+    _finalize(st.part, M, C, bn_mod, c_real, momentum, eps, n_updates, scratch, st.gamma, st.beta)
 
 
-def bn_eval(bn_mod, C, c_real, eps, device):
+def bn_eval(bn_mod, C, c_real, eps, device, gamma=None, beta=None):
     st = BNState(C, device)
-    st.gamma = pad_vec(bn_mod.weight.detach(), C)
-    beta = pad_vec(bn_mod.bias.detach(), C)
+    st.gamma = gamma if gamma is not None else pad_vec(bn_mod.weight.detach(), C)
+    beta = beta if beta is not None else pad_vec(bn_mod.bias.detach(), C)
+    st.beta = beta
     call("nsm_bn_finalize_eval", ptr(bn_mod.running_mean), ptr(bn_mod.running_var), ptr(st.gamma),
          ptr(beta), C, c_real, eps, ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift),
          stream())

@@ -1,0 +1,148 @@
+"""Weight layouts of one step, prepared in ONE launch (include/nsm.h
+`nsm_prep_weights`).
+
+Every convolution of the U-Net (Unetmodel.py:21,26) reads its weight in an
+MFMA operand layout: packed [co][tap][ci] for the direct forward, flipped
+[ci][tap'][co] for the input gradient, Winograd-domain U = G g G^T (forward and
+rotated for the input gradient), bias / BN affine vectors padded to the NHWC
+channel count. The weights change every optimizer step, so these layouts are
+rebuilt every step: `StepWeights` writes all of them with one kernel launch
+into persistent buffers (the job table holds raw pointers, uploaded once per
+parameter storage), instead of ~40 small launches. `LazyBlockWeights` is the
+per-call path (a standalone DoubleConv).
+"""
+import ctypes
+
+import torch
+
+from . import ops
+from ._lib import call, lib, ptr, stream
+
+
+class NsmPrepJob(ctypes.Structure):
+    _fields_ = [("kind", ctypes.c_int), ("a", ctypes.c_int * 7), ("base", ctypes.c_longlong),
+                ("src", ctypes.c_void_p), ("dst", ctypes.c_void_p)]
+
+
+KIND_PACK_F32, KIND_PACK_BF16, KIND_WINO, KIND_PAD = 0, 1, 2, 3
+
+
+class LazyBlockWeights:
+    """Layouts of one DoubleConv computed on demand (one launch each)."""
+
+    def __init__(self, blk, dtype):
+        self.blk, self.dtype = blk, dtype
+        self.cip = ops.pad32(blk.conv[0].in_channels)
+        self.cop = ops.pad32(blk.conv[4].out_channels)
+
+    def vec(self, name):
+        c0, bn1, c4, bn2 = (self.blk.conv[i] for i in (0, 1, 4, 5))
+        t, n = {"b1": (c0.bias, self.cip), "g1": (bn1.weight, self.cip), "be1": (bn1.bias, self.cip),
+                "b2": (c4.bias, self.cop), "g2": (bn2.weight, self.cop),
+                "be2": (bn2.bias, self.cop)}[name]
+        return ops.pad_vec(t.detach(), n)
+
+    def U1(self, tile, flip):
+        return ops.wino_weight(self.blk.conv[0].weight.detach(), self.cip, self.cip, flip=flip,
+                               tile=tile)
+
+    def w1(self, mode):
+        return ops.pack_conv_weight(self.blk.conv[0].weight.detach(), self.cip, self.cip, mode,
+                                    self.dtype)
+
+    def w2(self, mode):
+        return ops.pack_conv_weight(self.blk.conv[4].weight.detach(), self.cop, self.cip, mode,
+                                    self.dtype)
+
+
+class _PreparedBlock:
+    __slots__ = ("t",)
+
+    def __init__(self):
+        self.t = {}
+
+    def vec(self, name):
+        return self.t[name]
+
+    def U1(self, tile, flip):
+        return self.t[("U1", flip)]
+
+    def w1(self, mode):
+        return self.t[("w1", mode)]
+
+    def w2(self, mode):
+        return self.t[("w2", mode)]
+
+
+class StepWeights:
+    """All layouts of a Unet for one (dtype, input size, train/eval) signature.
+    `run()` launches the single preparation kernel; `block(k)` returns the
+    layouts of DoubleConv k. Valid while the parameters keep their storage
+    (`valid()` checks the pointers)."""
+
+    def __init__(self, mod, dtype, shapes, training, wino_min, wino_tile):
+        dev = mod.conv10.weight.device
+        self.params = [p for p in mod.parameters()]
+        self.ptrs = [p.data_ptr() for p in self.params]
+        self.blocks = {}
+        jobs, keep = [], []
+        base = 0
+
+        def add(kind, a, src, shape_numel, out_dtype):
+            nonlocal base
+            out = torch.empty(shape_numel, dtype=out_dtype, device=dev)
+            j = NsmPrepJob()
+            j.kind = kind
+            for i, v in enumerate(a):
+                j.a[i] = int(v)
+            j.base = base
+            j.src = src.data_ptr()
+            j.dst = out.data_ptr()
+            n = int(lib.nsm_prep_items(ctypes.byref(j)))
+            assert n > 0, (kind, a)
+            base += n
+            jobs.append(j)
+            keep.append(out)
+            return out
+
+        for k, (h, w) in shapes.items():
+            blk = mod.block(k)
+            c0, bn1, c4, bn2 = (blk.conv[i] for i in (0, 1, 4, 5))
+            ci, co = c0.in_channels, c4.out_channels
+            cip, cop = ops.pad32(ci), ops.pad32(co)
+            pb = _PreparedBlock()
+            for name, t, n in (("b1", c0.bias, cip), ("g1", bn1.weight, cip), ("be1", bn1.bias, cip),
+                               ("b2", c4.bias, cop), ("g2", bn2.weight, cop),
+                               ("be2", bn2.bias, cop)):
+                pb.t[name] = (t.detach() if t.numel() == n else
+                              add(KIND_PAD, (t.numel(), n), t, n, torch.float32))
+            pk = KIND_PACK_BF16 if dtype == torch.bfloat16 else KIND_PACK_F32
+            modes = (ops.PACK_FWD, ops.PACK_DGRAD) if training else (ops.PACK_FWD,)
+            if cip >= wino_min and dtype == torch.float32:
+                tile = wino_tile(cip, h, w)
+                for flip in ((False, True) if training else (False,)):
+                    pb.t[("U1", flip)] = add(KIND_WINO, (ci, ci, cip, cip, int(flip), tile),
+                                             c0.weight, (tile + 2) ** 2 * cip * cip, torch.float32)
+            else:
+                for mode in modes:
+                    pb.t[("w1", mode)] = add(pk, (ci, ci, 9, cip, cip, mode), c0.weight,
+                                             cip * 9 * cip, dtype)
+            for mode in modes:
+                pb.t[("w2", mode)] = add(pk, (co, ci, 1, cop, cip, mode), c4.weight, cop * cip, dtype)
+            self.blocks[k] = pb
+        self.total = base
+        self.njobs = len(jobs)
+        raw = (NsmPrepJob * len(jobs))(*jobs)
+        host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
+        self.table = host.to(dev)
+        self.keep = keep
+
+    def valid(self, mod):
+        ps = list(mod.parameters())
+        return len(ps) == len(self.ptrs) and all(p.data_ptr() == q for p, q in zip(ps, self.ptrs))
+
+    def run(self):
+        call("nsm_prep_weights", ptr(self.table), self.njobs, self.total, stream())
+
+    def block(self, k):
+        return self.blocks[k]

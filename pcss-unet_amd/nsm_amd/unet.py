@@ -27,6 +27,7 @@ import torch.nn as nn
 
 from . import ops, optim
 from ._lib import call, ptr, require_gpu, stream
+from .prep import LazyBlockWeights, StepWeights
 
 SLOPE = 0.2
 # 3x3 convolutions with at least this many (padded) input channels use the
@@ -311,55 +312,86 @@ class Unet(nn.Module):
 # forward / backward orchestration
 # ---------------------------------------------------------------------------
 def _masks_for(mod, B, device, training):
+    """[B, C_in_padded] Dropout2d masks of the blocks with p > 0: injected ones
+    (parity), else all drawn in ONE nsm_dropout_masks launch seeded from torch's
+    default CPU generator (so torch.manual_seed makes them reproducible)."""
     masks = {}
     inj = mod._inject_masks
     mod._inject_masks = None
+    jobs = []
     for k in ENCODER + DECODER:
         blk = mod.block(k)
         p = blk.conv[3].p
         if not training or p == 0:
             continue
         ci = blk.conv[0].in_channels
+        cp = ops.pad32(ci)
         if inj is not None and k in inj:
             m = inj[k].to(device=device, dtype=torch.float32).reshape(B, ci)
-            cp = ops.pad32(ci)
             if cp != ci:
                 m = torch.nn.functional.pad(m, (0, cp - ci))
             masks[k] = m.contiguous()
         else:
-            masks[k] = _dropout_mask(p, B, ci, device)
+            jobs.append((k, ci, cp, 1.0 - p))
+    if jobs:
+        import struct
+        desc, off = [], 0
+        for k, ci, cp, keep in jobs:
+            fb = struct.unpack("<i", struct.pack("<f", keep))[0]
+            desc += [off, ci, cp, fb]
+            off += B * cp
+        flat = torch.empty(off, dtype=torch.float32, device=device)
+        # the descriptor depends only on (B, blocks): uploaded once, then cached
+        # (a per-forward H2D copy from pageable memory would synchronise the host)
+        key = (B, str(device), tuple(desc))
+        cache = mod.__dict__.setdefault("_mask_desc", {})
+        dev_desc = cache.get(key)
+        if dev_desc is None:
+            dev_desc = cache[key] = torch.tensor(desc, dtype=torch.int32).to(device)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        call("nsm_dropout_masks", ptr(dev_desc), len(jobs), B, seed, ptr(flat), stream())
+        off = 0
+        for k, ci, cp, keep in jobs:
+            masks[k] = flat[off:off + B * cp].view(B, cp)
+            off += B * cp
     return masks
 
 
 class _BlockSaved:
-    __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop", "V", "A1")
+    __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop", "V", "A1",
+                 "pw")
 
 
-def _block_fwd(blk, X, B, H, W, training, mask, name=""):
+def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None):
+    """pw: the block's weight layouts (prep.StepWeights.block, all written by the
+    step's single preparation launch), or None to build them here per call."""
     c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
     ci, co = c0.in_channels, c4.out_channels
     cip, cop = ops.pad32(ci), ops.pad32(co)
     assert X.shape[1] == cip, (X.shape, cip)
-    b1 = ops.pad_vec(c0.bias.detach(), cip)
-    V = None
     dtype = X.dtype
+    if pw is None:
+        pw = LazyBlockWeights(blk, dtype)
+    b1 = pw.vec("b1")
+    V = None
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         tile = wino_tile(cip, H, W)
-        U1 = ops.wino_weight(c0.weight.detach(), cip, cip, flip=False, tile=tile)
+        U1 = pw.U1(tile, False)
         Y1, V = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tile=tile, tag=name + ".conv.0.fwd",
                                  keep_v=True)
         part1 = ops.bn_partials(Y1) if training else None
     else:
-        w1 = ops.pack_conv_weight(c0.weight.detach(), cip, cip, ops.PACK_FWD, dtype)
+        w1 = pw.w1(ops.PACK_FWD)
         Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd",
                                     stats=training)
     eps1, eps2 = bn1m.eps, bn2m.eps
     if training:
-        bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1)
+        bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1, gamma=pw.vec("g1"),
+                           beta=pw.vec("be1"))
     else:
-        bn1 = ops.bn_eval(bn1m, cip, ci, eps1, X.device)
-    w2 = ops.pack_conv_weight(c4.weight.detach(), cop, cip, ops.PACK_FWD, dtype)
-    b2 = ops.pad_vec(c4.bias.detach(), cop)
+        bn1 = ops.bn_eval(bn1m, cip, ci, eps1, X.device, gamma=pw.vec("g1"), beta=pw.vec("be1"))
+    w2 = pw.w2(ops.PACK_FWD)
+    b2 = pw.vec("b2")
     A1 = None
     if BF16_MATERIALIZE_ACT if dtype == torch.bfloat16 else F32_MATERIALIZE_ACT:
         # the same fp32 arithmetic and bf16 rounding as the fused operand prologue
@@ -370,11 +402,13 @@ def _block_fwd(blk, X, B, H, W, training, mask, name=""):
         Y2, part2 = ops.conv_fwd_bn(Y1, B, H, W, w2, b2, cop, 1, pro=(bn1.scale, bn1.shift, mask),
                                     tag=name + ".conv.4.fwd", stats=training)
     if training:
-        bn2 = ops.bn_train(Y2, bn2m, co, bn2m.momentum, eps2, part=part2)
+        bn2 = ops.bn_train(Y2, bn2m, co, bn2m.momentum, eps2, part=part2, gamma=pw.vec("g2"),
+                           beta=pw.vec("be2"))
     else:
-        bn2 = ops.bn_eval(bn2m, cop, co, eps2, X.device)
+        bn2 = ops.bn_eval(bn2m, cop, co, eps2, X.device, gamma=pw.vec("g2"), beta=pw.vec("be2"))
     s = _BlockSaved()
     s.X, s.Y1, s.Y2, s.bn1, s.bn2, s.mask = X, Y1, Y2, bn1, bn2, mask
+    s.pw = pw
     s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
     s.V = V if training else None  # Winograd-domain input, reused by the weight gradient
     s.A1 = A1 if training else None  # activated 1x1 operand, reused by its weight gradient
@@ -390,7 +424,7 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
     g = grads
     dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias])
     dtype = G.dtype
-    w2d = ops.pack_conv_weight(c4.weight.detach(), s.cop, s.cip, ops.PACK_DGRAD, dtype)
+    w2d = s.pw.w2(ops.PACK_DGRAD)
     dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
     if s.A1 is not None:
         ops.conv_wgrad(dY2, s.A1, B, H, W, 1, ci, co, g[c4.weight], tag=name + ".conv.4.wgrad")
@@ -410,11 +444,40 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
         return None
     if s.cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         tile = wino_tile(s.cip, H, W)
-        U1d = ops.wino_weight(c0.weight.detach(), s.cip, s.cip, flip=True, tile=tile)
+        U1d = s.pw.U1(tile, True)
         return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=tile,
                                 tag=name + ".conv.0.dgrad")
-    w1d = ops.pack_conv_weight(c0.weight.detach(), s.cip, s.cip, ops.PACK_DGRAD, dtype)
+    w1d = s.pw.w1(ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
+
+
+def block_shapes(Rh, Rw):
+    """(h, w) each DoubleConv runs at, for the half-resolution input Rh x Rw
+    (Unetmodel.py:104-142: floor halving by AvgPool2d, decoder at the skip size)."""
+    enc, h, w = {}, Rh, Rw
+    for k in ENCODER:
+        enc[k] = (h, w)
+        h, w = h // 2, w // 2
+    return {**enc, 6: enc[4], 7: enc[3], 8: enc[2], 9: (Rh, Rw)}
+
+
+PREP_BATCH = os.environ.get("NSM_PREP_BATCH", "1") != "0"
+
+
+def _step_weights(mod, dtype, Rh, Rw, training):
+    """The step's weight layouts, written by ONE prep launch (cached per
+    signature; rebuilt when the parameters moved, e.g. FlatAdamW re-homing).
+    NSM_PREP_BATCH=0: None (every block packs its own, one launch per layout)."""
+    if not PREP_BATCH:
+        return None
+    key = (dtype, Rh, Rw, bool(training), WINOGRAD_MIN_CHANNELS)
+    cache = mod.__dict__.setdefault("_step_weights", {})
+    sw = cache.get(key)
+    if sw is None or not sw.valid(mod):
+        sw = cache[key] = StepWeights(mod, dtype, block_shapes(Rh, Rw), training,
+                                      WINOGRAD_MIN_CHANNELS, wino_tile)
+    sw.run()
+    return sw
 
 
 class _UnetFn(torch.autograd.Function):
@@ -437,12 +500,14 @@ class _UnetFn(torch.autograd.Function):
         cdt = mod.activation_dtype()
         X = ops.input_prep(x32, cin_p, cdt)
         masks = _masks_for(mod, B, dev, training)
+        sw = _step_weights(mod, cdt, Rh, Rw, training)
 
         saved, c, shapes = {}, {}, {}
         inp, h, w = X, Rh, Rw
         for k in ENCODER:
             with ops.stage(f"conv{k}.fwd"):
-                s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}")
+                s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}",
+                               pw=sw.block(k) if sw else None)
                 saved[k], shapes[k] = s, (h, w)
                 c[k] = ops.bn_act(s.Y2, s.bn2, SLOPE)
                 if k < 5:
@@ -460,7 +525,8 @@ class _UnetFn(torch.autograd.Function):
                 else:                      # match is the identity (bitwise, as in ATen)
                     up = ops.resize(cur, B, h, w, h2, w2)
                 ups[k] = (h, w, h2, w2, th, tw)
-                s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}")
+                s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}",
+                               pw=sw.block(k) if sw else None)
                 saved[k] = s
                 res = c[SKIP_OF[k]] if k in SKIP_OF else None
                 cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
