@@ -35,7 +35,7 @@ SLOPE = 0.2
 # (MFMA-bound layers); NSM_WINOGRAD=0 disables it (direct implicit GEMM
 # everywhere). The tile m of F(m x m, 3x3) per layer: wino_tile(); NSM_WINO_TILE=2/4/6
 # forces one tile everywhere.
-WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "128"))
+WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "64"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
 _WINO_ENV = os.environ.get("NSM_WINO_TILE", "")
 WINO_TILE = int(_WINO_ENV) if _WINO_ENV else 4   # the tile of the VGG stack

@@ -32,7 +32,10 @@ import torch.nn as nn
 
 from . import ops
 from ._lib import require_gpu
-from .unet import WINO_TILE, WINOGRAD_MIN_CHANNELS
+from .unet import WINO_TILE
+
+# VGG19's 3x3 convs with >= 128 input channels run Winograd F(4x4,3x3)
+WINOGRAD_MIN_CHANNELS = 128
 
 VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M",
              512, 512, 512, 512, "M", 512, 512, 512, 512, "M"]
