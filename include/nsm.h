@@ -178,6 +178,10 @@ int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy, int M, int
 int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int C, int c_real,
                         const float* gamma, const float* invstd, float* dgamma, float* dbeta,
                         float* dbias_prev, float* coef, void* stream);
+/* plain-sum merge: out[g][j] = sum of rows [g*group, (g+1)*group) of part[nrows][width]
+ * (fixed order): the BN-backward partials of nsm_conv1x1_dgrad_bnbwd before
+ * nsm_bn_bwd_finalize */
+int nsm_sum_rows(const float* part, int nrows, int width, int group, float* out, void* stream);
 /* dy = coef0*dz + coef1*(y-mean) + coef2 */
 int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, int M, int C, int HW,
                      const float* scale, const float* shift, float slope, const float* mask,
@@ -309,6 +313,26 @@ int nsm_conv_fwd_bf16(const void* x, int ldx, int B, int H, int W, int cin_p, co
                       const float* bias, int cout_p, int ksize, void* y, int ldy,
                       const float* pro_scale, const float* pro_shift, const float* pro_mask,
                       float slope, float* stats, void* stream);
+/* The 1x1 input gradient of a DoubleConv (dA1 = dY2 W2, Unetmodel.py:26) with
+ * the backward of the first BN + LeakyReLU + Dropout2d (:22-24) in the GEMM
+ * epilogue; y1 = that BN's input (Y1), scale/shift/mean/invstd its train-mode
+ * vectors, mask [B][cip] or NULL, w2d the PACK_DGRAD layout of conv.4's weight.
+ *   mode 0: partial[nchunk][2][cip] = {sum dz, sum dz*xhat} per chunk (the
+ *           nsm_bn_bwd_reduce format; nchunk = nsm_conv1x1_bnbwd_chunks), dA1
+ *           not written
+ *   mode 1: mode 0 and dA1 written to out (then nsm_bn_bwd_apply)
+ *   mode 2: out = dY1 = coef0*dz + coef1*(y1-mean) + coef2 (coef from
+ *           nsm_bn_bwd_finalize); modes 0 + 2 run the GEMM twice so dA1 never
+ *           reaches HBM.
+ * Replaces ConvolutionBackward(conv.4) + BatchNorm/LeakyReLU/Dropout2d
+ * backward of conv.1-3 (autograd of Unetmodel.py:21-26). dtype NSM_F32 | NSM_BF16. */
+int nsm_conv1x1_dgrad_bnbwd(const void* dy2, int lddy2, int B, int H, int W, int cop,
+                            const void* w2d, int cip, const void* y1, int ldy1,
+                            const float* scale, const float* shift, const float* mean,
+                            const float* invstd, const float* mask, float slope, int mode,
+                            float* partial, const float* coef, void* out, int ldo, int dtype,
+                            void* stream);
+int nsm_conv1x1_bnbwd_chunks(int B, int H, int W, int cip, int dtype);
 /* rows per BN-partial chunk of nsm_conv_fwd_bf16 (its M tile) */
 int nsm_conv_stat_rows_bf16(int B, int H, int W, int cout_p);
 size_t nsm_conv_wgrad_bf16_ws(int B, int H, int W, int cin_p, int cout_p, int ksize);

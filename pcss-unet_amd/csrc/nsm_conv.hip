@@ -20,6 +20,8 @@
 // Global -> LDS staging goes through registers (float4 per lane, coalesced
 // along channels), double-buffered: the next slab's global loads are issued
 // before the current slab's MFMAs, and written to the other LDS stage after.
+#include <type_traits>
+
 #include "nsm_common.h"
 
 namespace nsm {
@@ -420,6 +422,133 @@ struct EpiStore {
   }
 };
 
+// BN-backward epilogue of the 1x1 input-gradient GEMM of a DoubleConv
+// (g = dA1 = dY2 W2, the gradient wrt the activated output of the block's
+// first BN; Unetmodel.py:22-26). With y = Y1 (that BN's input):
+//   dz = g * lrelu'(y*scale + shift) * mask[b][c]
+// mode 0: partials {sum dz, sum dz*(y-mean)*invstd} per row chunk (the
+//         nsm_bn_bwd_reduce format; chunk = nsm_conv_stat_rows rows), g not stored
+// mode 1: mode 0 and g stored (nsm_bn_bwd_apply then reads it)
+// mode 2: dy = k1*dz + k2*(y-mean) + k3 stored (coef from nsm_bn_bwd_finalize)
+// Modes 0 then 2 run the same GEMM twice, so dA1 never goes through HBM.
+struct BnBwdEpiP {
+  void* out;
+  int ldo;
+  const void* y;
+  int ldy;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* invstd;
+  const float* coef;
+  const float* mask;  // [B][N] or null
+  FastDiv fdHW;
+  float slope;
+  float* partial;  // [nchunk][2][N]
+  int mode;
+};
+
+__device__ __forceinline__ f32x4 lrelu_grad_v4(f32x4 z, float slope) {
+  return f32x4{lrelu_grad(z.x, slope), lrelu_grad(z.y, slope), lrelu_grad(z.z, slope),
+               lrelu_grad(z.w, slope)};
+}
+__device__ __forceinline__ f32x4 shfl_xor_v4(f32x4 v, int o) {
+  return f32x4{__shfl_xor(v.x, o, 64), __shfl_xor(v.y, o, 64), __shfl_xor(v.z, o, 64),
+               __shfl_xor(v.w, o, 64)};
+}
+
+// Each wave stages its accumulator tile as rows in LDS (row stride WC + 4
+// floats: the two row halves of a store land on different banks), then every
+// lane keeps ONE 4-column group and walks the rows with 16-B accesses: all Y1
+// loads of the lane issue back to back, the accumulators are dead by then, so
+// the epilogue adds no register pressure to the GEMM loop.
+struct EpiBnBwd {
+  using P = BnBwdEpiP;
+  template <int TM, int TN, int WM, int WN>
+  __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
+                               int) {
+    const int col = cx.lane & 31, h = cx.lane >> 5;
+    constexpr int BNT = WN * TN * 32, WR = TM * 32, WC = TN * 32, WCP = WC + 4;
+    constexpr int CPR = WC / 4;  // 16-B chunks per row
+    constexpr int NIT = WR * CPR / 64;
+    static_assert(64 % CPR == 0, "a lane keeps one column group");
+    float* reg = cx.lds + (cx.wm * WN + cx.wn) * (WR * WCP);
+    __syncthreads();  // the GEMM's last LDS reads are done everywhere
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          reg[(tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * WCP + tn * 32 + col] = acc[tm][tn][i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float* __restrict__ Y = (const float*)e.y;
+    float* __restrict__ O = (float*)e.out;
+    const float* __restrict__ mk = e.mask;
+    const bool red = e.mode != 2;
+    const int cc = cx.lane % CPR, n = cx.nb + cc * 4;
+    const bool nok = n < N;
+    const int nc = nok ? n : 0;
+    f32x4 yv[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int m = min(cx.mb + (it * 64 + cx.lane) / CPR, M - 1);
+      yv[it] = *(const f32x4*)(Y + (size_t)m * e.ldy + nc);
+    }
+    const f32x4 sc = *(const f32x4*)(e.scale + nc), sh = *(const f32x4*)(e.shift + nc),
+                mu = *(const f32x4*)(e.mean + nc);
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    const f32x4 is = red ? *(const f32x4*)(e.invstd + nc) : zero;
+    const f32x4 k1 = red ? zero : *(const f32x4*)(e.coef + nc),
+                k2 = red ? zero : *(const f32x4*)(e.coef + N + nc),
+                k3 = red ? zero : *(const f32x4*)(e.coef + 2 * N + nc);
+    f32x4 s1 = zero, s2 = zero;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int r = (it * 64 + cx.lane) / CPR, m = cx.mb + r;
+      const bool ok = m < M && nok;
+      const f32x4 g = *(const f32x4*)&reg[r * WCP + cc * 4], v = yv[it];
+      f32x4 dz = g * lrelu_grad_v4(v * sc + sh, e.slope);
+      if (mk) dz = dz * *(const f32x4*)(mk + (size_t)fdiv((uint32_t)min(m, M - 1), e.fdHW) * N + nc);
+      if (!red) {
+        if (ok) *(f32x4*)(O + (size_t)m * e.ldo + n) = k1 * dz + k2 * (v - mu) + k3;
+      } else if (ok) {
+        s1 += dz;
+        s2 += dz * ((v - mu) * is);
+        if (e.mode == 1) *(f32x4*)(O + (size_t)m * e.ldo + n) = g;
+      }
+    }
+    if (!red) return;
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+      s1 += shfl_xor_v4(s1, o);
+      s2 += shfl_xor_v4(s2, o);
+    }
+    // one partial row per block (RPP = BM = nsm_conv_stat_rows): the waves of
+    // one column range meet in LDS, fixed order
+    __syncthreads();
+    float* lds = cx.lds;  // [WM][2][BNT]
+    if (cx.lane < CPR) {
+      *(f32x4*)(lds + (cx.wm * 2) * BNT + cx.wn * WC + cc * 4) = s1;
+      *(f32x4*)(lds + (cx.wm * 2 + 1) * BNT + cx.wn * WC + cc * 4) = s2;
+    }
+    __syncthreads();
+    if (cx.wm == 0) {
+      float* pr = e.partial + (size_t)cx.mblk * 2 * N;
+      for (int j = cx.lane; j < 2 * WC; j += 64) {
+        const int k = j / WC, c = j - k * WC, nn = cx.nb + c;
+        if (nn >= N) continue;
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) t += lds[(w * 2 + k) * BNT + cx.wn * WC + c];
+        pr[k * N + nn] = t;
+      }
+    }
+  }
+};
+
 struct EpiSlabP {
   float* ws;
 };
@@ -564,14 +693,14 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN, bool PRO>
-static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const EpiStoreP& ep, int M, int N,
-                           int K, hipStream_t s) {
+template <int BM, int BN, int WM, int WN, bool PRO, class EP = EpiStore>
+static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const typename EP::P& ep, int M,
+                           int N, int K, hipStream_t s) {
   constexpr int NT = WM * WN * 64;
   using AL = ConvActLoader<BM, NT, PRO>;
   using BL = RowsKLoader<BN, NT>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 1);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiStore, ConvActP, RowsKP>), grid,
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EP, ConvActP, RowsKP>), grid,
                      dim3(NT), 0, s, ap, bp, ep, M, N, K, K, 1);
   NSM_LAUNCH_CHECK("conv_fwd");
   return 0;
@@ -585,8 +714,8 @@ static int conv_fwd_bm(long long M, int N) {
   return mb128 >= 512 ? 128 : 64;
 }
 
-template <bool PRO>
-static int dispatch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const EpiStoreP& ep, int M,
+template <bool PRO, class EP = EpiStore>
+static int dispatch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const typename EP::P& ep, int M,
                              int N, int K, hipStream_t s) {
   // Tile choice: 128x128 (2x2 waves of 64x64) wherever N allows; narrower N
   // tiles for the 32/64-channel layers; BM=64 when the grid would not cover
@@ -594,16 +723,16 @@ static int dispatch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const EpiStor
   long long mb128 = ceil_div(M, 128);
   if (N >= 128) {
     if (mb128 * ceil_div(N, 128) >= 512)
-      return launch_conv_fwd<128, 128, 2, 2, PRO>(ap, bp, ep, M, N, K, s);
-    return launch_conv_fwd<64, 128, 2, 2, PRO>(ap, bp, ep, M, N, K, s);
+      return launch_conv_fwd<128, 128, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
+    return launch_conv_fwd<64, 128, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
   }
   if (N >= 64) {
     if (mb128 * ceil_div(N, 64) >= 512)
-      return launch_conv_fwd<128, 64, 2, 2, PRO>(ap, bp, ep, M, N, K, s);
-    return launch_conv_fwd<64, 64, 2, 2, PRO>(ap, bp, ep, M, N, K, s);
+      return launch_conv_fwd<128, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
+    return launch_conv_fwd<64, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
   }
-  if (mb128 >= 512) return launch_conv_fwd<128, 32, 4, 1, PRO>(ap, bp, ep, M, N, K, s);
-  return launch_conv_fwd<64, 32, 2, 1, PRO>(ap, bp, ep, M, N, K, s);
+  if (mb128 >= 512) return launch_conv_fwd<128, 32, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
+  return launch_conv_fwd<64, 32, 2, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
 }
 
 template <int BM, int BN, int WM, int WN, bool SHIFT, bool PRO>

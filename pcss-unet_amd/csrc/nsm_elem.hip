@@ -182,6 +182,19 @@ __global__ void bn_partials_merge_kernel(const float* __restrict__ partial, int 
   out[(size_t)g * 2 * C + C + c] = (float)m2;
 }
 
+// Plain-sum merge of partial rows (the BN-backward {sum dz, sum dz*xhat}
+// format): out[g][j] = sum over rows [g*G, (g+1)*G) of part[.][j], fixed
+// order, one thread per column (coalesced along the row)
+__global__ void sum_rows_kernel(const float* __restrict__ part, int nrows, int width, int G,
+                                float* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
+  if (j >= width) return;
+  const int k0 = g * G, k1 = min(nrows, k0 + G);
+  double s = 0.0;
+  for (int k = k0; k < k1; ++k) s += part[(size_t)k * width + j];
+  out[(size_t)g * width + j] = (float)s;
+}
+
 __global__ void bn_finalize_eval_kernel(const float* __restrict__ rm, const float* __restrict__ rv,
                                         const float* __restrict__ gamma,
                                         const float* __restrict__ beta, int C, int c_real, float eps,
@@ -1360,6 +1373,16 @@ extern "C" int nsm_bn_partials_merge(const float* partial, int nchunk, int rows_
   hipLaunchKernelGGL(bn_partials_merge_kernel, grid, dim3(256), 0, as_stream(stream), partial,
                      nchunk, rows_per_chunk, M, C, group, out);
   NSM_LAUNCH_CHECK("bn_partials_merge");
+  return 0;
+}
+
+extern "C" int nsm_sum_rows(const float* part, int nrows, int width, int group, float* out,
+                            void* stream) {
+  NSM_CHECK_ARG(part && out && nrows >= 1 && width >= 1 && group >= 1, "sum_rows: bad args");
+  dim3 grid(ceil_div(width, 256), ceil_div(nrows, group));
+  hipLaunchKernelGGL(sum_rows_kernel, grid, dim3(256), 0, as_stream(stream), part, nrows, width,
+                     group, out);
+  NSM_LAUNCH_CHECK("sum_rows");
   return 0;
 }
 

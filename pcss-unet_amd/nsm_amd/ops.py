@@ -335,6 +335,54 @@ def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2):
     return dy
 
 
+SUM_ROWS_ABOVE = 512  # BN-backward partial rows beyond which nsm_sum_rows merges them first
+
+
+def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
+                         recompute, slope=0.2, tag=None):
+    """dY1 of a DoubleConv's first BN from dY2 (grad wrt the 1x1 conv output):
+    the 1x1 input gradient dA1 = dY2 W2 with the BN + LeakyReLU + Dropout2d
+    backward in its epilogue (nsm_conv1x1_dgrad_bnbwd) — the same values as
+    bn_bwd(conv_fwd(dY2, w2d, ...), y, ...) without the separate reduce pass.
+    recompute=True: a partials-only GEMM pass, then the GEMM again writing dY1
+    (dA1 never stored); False: one pass storing dA1 + partials, then
+    nsm_bn_bwd_apply."""
+    from ._lib import lib
+    M, cop = dY2.shape
+    C = y.shape[1]
+    if dY2.dtype != y.dtype or w2d.dtype != y.dtype:
+        raise TypeError("conv1x1_dgrad_bn_bwd: dY2, packed weight and Y1 must share a dtype")
+    dtc = dt(y)
+    nchunk = int(lib.nsm_conv1x1_bnbwd_chunks(B, H, W, C, dtc))
+    partial = empty(nchunk * 2 * C, device=y.device)
+    dA1 = None if recompute else like(M, C, y)
+    args = (ptr(dY2), dY2.stride(0), B, H, W, cop, ptr(w2d), C, ptr(y), y.stride(0),
+            ptr(st.scale), ptr(st.shift), ptr(st.mean), ptr(st.invstd), ptr(mask), slope)
+    ev = _probe(tag)
+    call("nsm_conv1x1_dgrad_bnbwd", *args, 0 if recompute else 1, ptr(partial), None, ptr(dA1),
+         dA1.stride(0) if dA1 is not None else 0, dtc, stream())
+    if nchunk > SUM_ROWS_ABOVE:
+        G = -(-nchunk // SUM_ROWS_ABOVE)
+        n2 = -(-nchunk // G)
+        buf = empty(n2 * 2 * C, device=y.device)
+        call("nsm_sum_rows", ptr(partial), nchunk, 2 * C, G, ptr(buf), stream())
+        partial, nchunk = buf, n2
+    coef = empty(3 * C, device=y.device)
+    call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
+         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
+    dy = like(M, C, y)
+    if recompute:
+        call("nsm_conv1x1_dgrad_bnbwd", *args, 2, None, ptr(coef), ptr(dy), dy.stride(0), dtc,
+             stream())
+    else:
+        call("nsm_bn_bwd_apply", ptr(dA1), dA1.stride(0), ptr(y), y.stride(0), M, C, H * W,
+             ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy),
+             dy.stride(0), dtc, stream())
+    if ev is not None:
+        ev.record()
+    return dy
+
+
 # ---- resampling --------------------------------------------------------------
 def avgpool2(x, B, H, W):
     C = x.shape[1]

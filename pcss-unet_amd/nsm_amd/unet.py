@@ -62,6 +62,33 @@ def wino_tile(cin_p, H, W):
 # the fused-prologue path.
 BF16_MATERIALIZE_ACT = os.environ.get("NSM_BF16_ACT", "1") != "0"
 F32_MATERIALIZE_ACT = os.environ.get("NSM_F32_ACT", "1") != "0"
+
+# The backward of the first BN (+ LeakyReLU + Dropout2d) rides in the epilogue
+# of the 1x1 input-gradient GEMM that produces its input gradient dA1
+# (ops.conv1x1_dgrad_bn_bwd). NSM_BNB=0: separate reduce / apply passes
+# everywhere; 1: the fused epilogue wherever it is used, storing dA1 + the
+# partials (the reduce pass's dA1 read is gone); 2 (default): per layer, see
+# bnb_mode.
+BNB_MODE = int(os.environ.get("NSM_BNB", "2"))
+
+
+def bnb_mode(cip, cop, dtype):
+    """0: conv_fwd + bn_bwd; 1: fused epilogue storing dA1, then bn_bwd_apply;
+    2: fused epilogue twice (partials, then dY1; dA1 never stored) where the
+    HBM bytes saved, (2*cip - cop) elements per pixel, outweigh the second
+    pass's 2*cip*cop MFMA FLOPs (at ~5 TB/s and ~0.6 PF bf16 / ~0.12 PF fp32 for
+    these K <= 512 GEMMs). bf16 keeps the separate passes where the GEMM is
+    not an LDS-DMA tile with N >= 128 (conv2/conv3/conv9): one 92-160 KB block
+    per CU leaves the epilogue's loads exposed there (measured: conv9 782 ->
+    892 us, conv2 462 -> 533 us fused), while conv6/7/8 gain 77-170 us each."""
+    if BNB_MODE == 0:
+        return 0
+    if dtype == torch.bfloat16 and (cop % 64 or cip < 128):
+        return 0 if BNB_MODE == 2 else 1
+    if BNB_MODE == 1:
+        return 1
+    s, rate = (2, 6e14) if dtype == torch.bfloat16 else (4, 1.2e14)
+    return 2 if (2 * cip - cop) * s / 5e12 > 2 * cip * cop / rate else 1
 ENCODER = (2, 3, 4, 5)
 DECODER = (6, 7, 8, 9)
 SKIP_OF = {6: 4, 7: 3, 8: 2}          # merge_k = conv_k(...) + c_skip  (Unetmodel.py:125,131,137)
@@ -425,14 +452,21 @@ def _block_bwd(blk, s, G, grads, need_dx, name=""):
     dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias])
     dtype = G.dtype
     w2d = s.pw.w2(ops.PACK_DGRAD)
-    dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
     if s.A1 is not None:
         ops.conv_wgrad(dY2, s.A1, B, H, W, 1, ci, co, g[c4.weight], tag=name + ".conv.4.wgrad")
         s.A1 = None
     else:
         ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
                        pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
-    dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias], g[c0.bias])
+    mode = bnb_mode(s.cip, s.cop, dtype)
+    if mode:
+        dY1 = ops.conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
+                                       g[bn1m.bias], g[c0.bias], mode == 2,
+                                       tag=name + ".conv.4.dgrad")
+    else:
+        dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
+        dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias],
+                         g[c0.bias])
     if s.V is not None:
         ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight],
                                tile=wino_tile(s.cip, H, W),

@@ -207,6 +207,67 @@ def test_bn_act_and_bwd(ops, device):
     assert dbias.abs().max().item() <= 1e-5
 
 
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("recompute", [False, True])
+@pytest.mark.parametrize("B,H,W,cip,cop,drop", [(2, 9, 11, 32, 64, True), (2, 16, 16, 64, 32, False),
+                                                (2, 16, 16, 128, 64, True), (1, 32, 32, 512, 128, True),
+                                                (2, 8, 8, 1024, 512, False), (2, 24, 40, 128, 512, True),
+                                                (9, 128, 128, 64, 32, True)])
+def test_conv1x1_dgrad_bn_bwd(ops, device, B, H, W, cip, cop, drop, recompute, dtype):
+    """1x1 input gradient with the first BN's backward in the GEMM epilogue
+    (nsm_conv1x1_dgrad_bnbwd, both schedules) vs autograd of
+    conv1x1(lrelu(BN(y1)) * mask) and vs the unfused conv_fwd + bn_bwd path.
+    The last shape has > 512 partial rows (nsm_sum_rows merge)."""
+    g = torch.Generator().manual_seed(B * H + cip + cop)
+    y1 = (torch.randn(B, cip, H, W, generator=g) * 1.5 + 0.3)
+    w2 = torch.randn(cop, cip, 1, 1, generator=g) / cip ** 0.5
+    dy2 = torch.randn(B, cop, H, W, generator=g)
+    gamma = torch.rand(cip, generator=g) + 0.5
+    beta = torch.randn(cip, generator=g) * 0.2
+    mask = (torch.rand(B, cip, generator=g) > 0.2).float() / 0.8 if drop else None
+    bf = dtype == "bf16"
+    tdt = torch.bfloat16 if bf else torch.float32
+    if bf:  # the reference sees the same bf16-representable inputs
+        y1, w2, dy2 = (t.to(torch.bfloat16).float() for t in (y1, w2, dy2))
+    yr = y1.clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    a = F.leaky_relu(F.batch_norm(yr, None, None, gr, br, training=True), 0.2)
+    if drop:
+        a = a * mask[:, :, None, None]
+    F.conv2d(a, w2).backward(dy2)
+
+    bn = torch.nn.BatchNorm2d(cip).to(device)
+    with torch.no_grad():
+        bn.weight.copy_(gamma)
+        bn.bias.copy_(beta)
+    yd = nhwc(y1).to(device=device, dtype=tdt)
+    st = ops.bn_train(yd, bn, cip, 0.1, 1e-5)
+    wd = ops.pack_conv_weight(w2.to(device), cop, cip, ops.PACK_DGRAD, tdt)
+    dyd = nhwc(dy2).to(device=device, dtype=tdt)
+    md = mask.to(device) if drop else None
+    outs = {}
+    for fused in (True, False):
+        dg, db, dbias = (torch.empty(cip, device=device) for _ in range(3))
+        if fused:
+            dy1 = ops.conv1x1_dgrad_bn_bwd(dyd, B, H, W, wd, yd, st, md, cip, dg, db, dbias,
+                                           recompute)
+        else:
+            dA1 = ops.conv_fwd(dyd, B, H, W, wd, None, cip, 1)
+            dy1 = ops.bn_bwd(dA1, yd, st, H * W, md, cip, dg, db, dbias)
+        outs[fused] = (nchw(dy1.float().cpu(), B, H, W), dg.cpu(), db.cpu(), dbias.cpu())
+    tol = 2e-2 if bf else 1e-5
+    for fused in (True, False):
+        dy1, dg, db, dbias = outs[fused]
+        assert rel(dy1, yr.grad) <= tol, (fused, rel(dy1, yr.grad))
+        assert rel(dg, gr.grad) <= tol
+        assert rel(db, br.grad) <= tol
+        assert dbias.abs().max().item() <= 1e-3 * max(1.0, br.grad.abs().max().item())
+    # fused vs unfused: the same rounded dA1 and formulas, only the reduction order differs
+    assert rel(outs[True][0], outs[False][0]) <= (4e-3 if bf else 2e-6)
+    assert rel(outs[True][1], outs[False][1]) <= 1e-5
+    assert rel(outs[True][2], outs[False][2]) <= 1e-5
+
+
 @pytest.mark.parametrize("Hi,Wi,Ho,Wo", [(4, 5, 8, 10), (8, 10, 4, 5), (2, 4, 4, 8), (4, 8, 5, 9),
                                          (67, 120, 134, 240), (134, 240, 135, 240), (1, 1, 2, 2),
                                          (5, 5, 5, 5), (64, 64, 32, 32)])

@@ -1,13 +1,27 @@
 #!/usr/bin/env python3
 """One train step's launches from a rocprofv3 kernel_trace.csv (steps end at
 the AdamW kernel): duration, grid (blocks), short name; then totals per kernel
-family. usage: python tools/step_timeline.py TRACE_CSV [step_index_from_end=1]"""
+family. usage: python tools/step_timeline.py TRACE_CSV|RESULTS_DB [step_index_from_end=1]
+(RESULTS_DB: the rocpd sqlite file rocprofv3 writes without --output-format csv)"""
 import collections
 import csv
 import re
 import sys
 
-rows = list(csv.DictReader(open(sys.argv[1])))
+def load(path):
+    if not path.endswith(".db"):
+        return list(csv.DictReader(open(path)))
+    import sqlite3
+    c = sqlite3.connect(path)
+    q = ("select s.display_name, d.start, d.end, d.grid_size_x, d.grid_size_y, d.grid_size_z, "
+         "d.workgroup_size_x, d.workgroup_size_y, d.workgroup_size_z from rocpd_kernel_dispatch d "
+         "join rocpd_info_kernel_symbol s on d.kernel_id = s.id")
+    keys = ["Kernel_Name", "Start_Timestamp", "End_Timestamp", "Grid_Size_X", "Grid_Size_Y",
+            "Grid_Size_Z", "Workgroup_Size_X", "Workgroup_Size_Y", "Workgroup_Size_Z"]
+    return [dict(zip(keys, r)) for r in c.execute(q)]
+
+
+rows = load(sys.argv[1])
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 k = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 ends = [i for i, r in enumerate(rows) if "adamw" in r["Kernel_Name"]]
