@@ -114,10 +114,25 @@ int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p, co
  * Mb[alpha^2][T][cout_p] = V . U^T (batched MFMA GEMMs); y = A^T Mb A + bias */
 int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile, int relu,
                    float* V, void* stream);
+/* nsm_wino_input of the bilinear align_corners resize of x [B][hi][wi][ldx] to
+ * H x W (Unetmodel.py:51-60,122-130: the decoder's x2 upsample feeding a
+ * Winograd conv): the resized tensor is sampled inside the transform and never
+ * written (relu must be 0 when hi, wi != H, W). */
+int nsm_wino_input_resize(const float* x, int ldx, int B, int hi, int wi, int H, int W, int cin_p,
+                          int tile, int relu, float* V, void* stream);
 int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
                   int tile, float* Mb, void* stream);
 int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, int tile, const float* bias,
                     float* y, int ldy, void* stream);
+/* nsm_wino_output that also emits the BatchNorm batch statistics of y
+ * (Unetmodel.py:21-22, the BN after a Winograd 3x3 conv) as counted partials
+ * partial[nslot][3][cout_p] = {sum, M2, count}. nslot: a multiple of
+ * 256 / gcd(cout_p / (tile == 6 ? 1 : 4), 256); nsm_wino_stat_slots gives the
+ * tuned count (0 there: the separate nsm_bn_stats pass is faster). */
+int nsm_wino_output_stats(const float* Mb, int B, int H, int W, int cout_p, int tile,
+                          const float* bias, float* y, int ldy, float* partial, int nslot,
+                          void* stream);
+int nsm_wino_stat_slots(int B, int H, int W, int cout_p, int tile);
 
 /* Winograd weight gradient of the same 3x3 conv: dw[co][ci][3][3] (reference
  * layout, real dims) from dy [pixels][cout_p] and the forward's transformed
@@ -147,7 +162,9 @@ int nsm_bn_stats(const void* y, int ld, int M, int C, float* partial, int nchunk
 /* merge partials; batch mean/biased var normalise; unbiased var feeds running
  * stats, applied n_updates times (2 for conv5: checkpoint recompute,
  * Unetmodel.py:114-116); num_batches_tracked += n_updates.
- * Emits scale=gamma*invstd, shift=beta-mean*scale, mean, invstd. */
+ * Emits scale=gamma*invstd, shift=beta-mean*scale, mean, invstd.
+ * rows_per_chunk == 0: counted partials [nchunk][3][C] = {sum, M2, count}
+ * (nsm_wino_output_stats); nsm_bn_partials_merge keeps that layout. */
 int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_per_chunk, int M, int C,
                           int c_real,
                           const float* gamma, const float* beta, float* run_mean, float* run_var,

@@ -70,6 +70,25 @@ __device__ __forceinline__ float lrelu_grad(float z, float slope) {
 
 inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }
 
+// Bilinear resize, align_corners=True (ATen upsample_bilinear2d semantics:
+// scale=(in-1)/(out-1) in fp32, src=scale*dst, i0=floor, i1=i0+(i0<in-1),
+// l1=src-i0, l0=1-l1): the source taps of destination index dst.
+__device__ __forceinline__ void lin_idx(float scale, int dst, int in, int& i0, int& i1, float& l0,
+                                        float& l1) {
+  // keep src rounded to fp32 as ATen does; letting the compiler contract
+  // scale*dst - i0 into one FMA shifts lambda by up to ~1e-5.
+#pragma clang fp contract(off)
+  float src = scale * (float)dst;
+  i0 = min((int)src, in - 1);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+  i1 = i0 + (i0 < in - 1 ? 1 : 0);
+}
+
+static inline float ac_scale(int in, int out) {  // align_corners source step
+  return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
+}
+
 // ---- bf16 storage (NSM_BF16 tensors): raw 16-bit words, fp32 arithmetic ------
 typedef unsigned short bf16_t;
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));

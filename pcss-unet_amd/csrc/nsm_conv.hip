@@ -1087,11 +1087,16 @@ __global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int ci
 }
 
 // RELU: the input is a pre-activation tensor whose consumer applies max(x, 0)
-// (VGG19 feature stack: ReLU folded into the next conv's operand load)
-template <int MT, bool RELU>
+// (VGG19 feature stack: ReLU folded into the next conv's operand load).
+// UP: x is the low-resolution tensor [B][hi][wi] of a bilinear align_corners
+// resize to H x W (the decoder's x2 upsample, Unetmodel.py:122-130); every
+// patch value is sampled from it as nsm_resize_fwd computes it, so the
+// resized activation is never written to HBM.
+template <int MT, bool RELU, bool UP>
 __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict__ x, int ld, int H,
                                                          int W, int C, int TH, int TW, long long T,
-                                                         float* __restrict__ V) {
+                                                         float* __restrict__ V, int hi, int wi,
+                                                         float sh, float sw) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int C4 = C / CW;
@@ -1105,16 +1110,42 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
     const int ty = (int)(r % TH);
     const long long b = r / TH;
     VT d[A][A];
+    if constexpr (UP) {
+      int x0[A], x1[A];
+      float lx0[A], lx1[A];
 #pragma unroll
-    for (int a = 0; a < A; ++a) {
-      const int yy = MT * ty - 1 + a;
+      for (int e = 0; e < A; ++e)
+        lin_idx(sw, min(max(MT * tx - 1 + e, 0), W - 1), wi, x0[e], x1[e], lx0[e], lx1[e]);
 #pragma unroll
-      for (int e = 0; e < A; ++e) {
-        const int xx = MT * tx - 1 + e;
-        d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
-                      ? *(const VT*)(x + ((size_t)(b * H + yy) * W + xx) * ld + c)
-                      : VT{};
-        if (RELU) d[a][e] = vrelu(d[a][e]);
+      for (int a = 0; a < A; ++a) {
+        const int yy = MT * ty - 1 + a;
+        int y0, y1;
+        float ly0, ly1;
+        lin_idx(sh, min(max(yy, 0), H - 1), hi, y0, y1, ly0, ly1);
+        const float* r0 = x + ((size_t)b * hi + y0) * wi * ld + c;
+        const float* r1 = x + ((size_t)b * hi + y1) * wi * ld + c;
+#pragma unroll
+        for (int e = 0; e < A; ++e) {
+          const int xx = MT * tx - 1 + e;
+          const VT v = ly0 * (lx0[e] * *(const VT*)(r0 + (size_t)x0[e] * ld) +
+                              lx1[e] * *(const VT*)(r0 + (size_t)x1[e] * ld)) +
+                       ly1 * (lx0[e] * *(const VT*)(r1 + (size_t)x0[e] * ld) +
+                              lx1[e] * *(const VT*)(r1 + (size_t)x1[e] * ld));
+          d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) ? v : VT{};
+        }
+      }
+    } else {
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        const int yy = MT * ty - 1 + a;
+#pragma unroll
+        for (int e = 0; e < A; ++e) {
+          const int xx = MT * tx - 1 + e;
+          d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                        ? *(const VT*)(x + ((size_t)(b * H + yy) * W + xx) * ld + c)
+                        : VT{};
+          if (RELU) d[a][e] = vrelu(d[a][e]);
+        }
       }
     }
     VT v[A][A];
@@ -1128,17 +1159,27 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
   }
 }
 
-template <int MT>
+// STATS: also the BatchNorm batch statistics of the written values (the
+// Winograd layers' BN input, Unetmodel.py:21-22), so no separate bn_stats pass
+// re-reads Y. The grid is sized so each thread keeps ONE channel group for the
+// whole grid-stride loop (gridDim.x * 256 = nslot * N4); it Chan-merges each
+// tile's {count, mean, M2} into its own and writes partial[slot][3][N] =
+// {sum, M2 about the slot mean, count}, slot = (global thread id) / N4 (the
+// counted partial layout nsm_bn_finalize_train takes with rows_per_chunk 0).
+template <int MT, bool STATS>
 __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
                                                           int W, int TH, int TW, long long T,
                                                           const float* __restrict__ bias,
-                                                          float* __restrict__ y, int ldy) {
+                                                          float* __restrict__ y, int ldy,
+                                                          float* __restrict__ partial) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int N4 = N / CW;
   const long long total = T * N4;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  VT s_sum{}, s_mean{}, s_m2{};
+  float s_n = 0.f;
+  for (long long i = i0; i < total; i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % N4) * CW;
     const long long t = i / N4;
     const int tx = (int)(t % TW);
@@ -1154,6 +1195,7 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
       for (int e = 0; e < A; ++e) m[a][e] = *(const VT*)(in + (a * A + e) * plane);
     wmat2<CAt<MT>>(m, o);
     const VT bv = bias ? *(const VT*)(bias + c) : VT{};
+    VT ts{};
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
       const int yy = MT * ty + a;
@@ -1161,8 +1203,38 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
       float* row = y + ((size_t)(b * H + yy) * W + MT * tx) * ldy + c;
 #pragma unroll
       for (int e = 0; e < MT; ++e)
-        if (MT * tx + e < W) *(VT*)(row + (size_t)e * ldy) = o[a][e] + bv;
+        if (MT * tx + e < W) {
+          o[a][e] = o[a][e] + bv;
+          *(VT*)(row + (size_t)e * ldy) = o[a][e];
+          if (STATS) ts = ts + o[a][e];
+        }
     }
+    if (STATS) {
+      const int nv = min(MT, H - MT * ty) * min(MT, W - MT * tx);
+      const VT tmean = ts * (1.f / (float)nv);
+      VT tq{};
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int e = 0; e < MT; ++e)
+          if (MT * ty + a < H && MT * tx + e < W) {
+            const VT d = o[a][e] - tmean;
+            tq = tq + d * d;
+          }
+      const float n2 = s_n + (float)nv;
+      const VT delta = tmean - s_mean;
+      s_mean = s_mean + delta * ((float)nv / n2);
+      s_m2 = s_m2 + tq + delta * delta * (s_n * (float)nv / n2);
+      s_sum = s_sum + ts;
+      s_n = n2;
+    }
+  }
+  if (STATS && i0 < (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i0 % N4) * CW;
+    float* pr = partial + (size_t)(i0 / N4) * 3 * N + c;
+    *(VT*)pr = s_sum;
+    *(VT*)(pr + N) = s_m2;
+    *(VT*)(pr + 2 * N) = VT{} + s_n;
   }
 }
 
@@ -1544,26 +1616,35 @@ extern "C" int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k
   return 0;
 }
 
-extern "C" int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile,
-                              int relu, float* V, void* stream) {
-  NSM_CHECK_ARG(x && V && cin_p % 32 == 0 && ldx % 4 == 0, "wino_input: bad args");
+extern "C" int nsm_wino_input_resize(const float* x, int ldx, int B, int hi, int wi, int H, int W,
+                                     int cin_p, int tile, int relu, float* V, void* stream) {
+  NSM_CHECK_ARG(x && V && cin_p % 32 == 0 && ldx % 4 == 0 && ldx >= cin_p, "wino_input: bad args");
+  NSM_CHECK_ARG(hi > 0 && wi > 0, "wino_input: bad source shape");
+  NSM_CHECK_ARG(!(relu && (hi != H || wi != W)), "wino_input: relu with a resize");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input: bad tile or shape");
   dim3 grid(grid_1d(g.T * cin_p / (tile == 6 ? 1 : 4)));
   hipStream_t s = as_stream(stream);
-#define NSM_WI(m, r)                                                                            \
-  hipLaunchKernelGGL((wino_input_kernel<m, r>), grid, dim3(256), 0, s, x, ldx, H, W, cin_p, g.TH, \
-                     g.TW, g.T, V)
+  const bool up = hi != H || wi != W;
+  const float sh = ac_scale(hi, H), sw = ac_scale(wi, W);
+#define NSM_WI(m, r, u)                                                                           \
+  hipLaunchKernelGGL((wino_input_kernel<m, r, u>), grid, dim3(256), 0, s, x, ldx, H, W, cin_p,     \
+                     g.TH, g.TW, g.T, V, hi, wi, sh, sw)
   if (tile == 2) {
-    if (relu) NSM_WI(2, true); else NSM_WI(2, false);
+    if (up) NSM_WI(2, false, true); else if (relu) NSM_WI(2, true, false); else NSM_WI(2, false, false);
   } else if (tile == 4) {
-    if (relu) NSM_WI(4, true); else NSM_WI(4, false);
+    if (up) NSM_WI(4, false, true); else if (relu) NSM_WI(4, true, false); else NSM_WI(4, false, false);
   } else {
-    if (relu) NSM_WI(6, true); else NSM_WI(6, false);
+    if (up) NSM_WI(6, false, true); else if (relu) NSM_WI(6, true, false); else NSM_WI(6, false, false);
   }
 #undef NSM_WI
   NSM_LAUNCH_CHECK("wino_input");
   return 0;
+}
+
+extern "C" int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile,
+                              int relu, float* V, void* stream) {
+  return nsm_wino_input_resize(x, ldx, B, H, W, H, W, cin_p, tile, relu, V, stream);
 }
 
 extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p,
@@ -1585,23 +1666,73 @@ extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W
   return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, nb, s);
 }
 
-extern "C" int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, int tile,
-                               const float* bias, float* y, int ldy, void* stream) {
+// thread slots per channel of the statistics form of the output transform:
+// nslot * N4 must fill whole 256-thread blocks (nslot a multiple of
+// wino_stat_step). The policy: ~1024 blocks, and 0 (= separate bn_stats pass)
+// under 2 tiles per thread, where the grid-stride form loses more parallelism
+// than the extra pass costs (measured: conv3-conv5 slower, conv6 even).
+static int wino_stat_step(int cout_p, int tile) {
+  int a = cout_p / (tile == 6 ? 1 : 4), b = 256;
+  while (b) {
+    const int r = a % b;
+    a = b;
+    b = r;
+  }
+  return 256 / a;
+}
+static long long wino_stat_slots(long long T, int cout_p, int tile) {
+  const int N4 = cout_p / (tile == 6 ? 1 : 4), step = wino_stat_step(cout_p, tile);
+  long long ns = (1024ll * 256) / N4;
+  if (ns < 512) ns = 512;
+  ns = ns / step * step;
+  if (ns < step) ns = step;
+  if (T < 2 * ns) return 0;
+  return ns;
+}
+
+extern "C" int nsm_wino_stat_slots(int B, int H, int W, int cout_p, int tile) {
+  WinoGeom g;
+  if (!wino_geom(tile, B, H, W, g) || cout_p % 32 != 0) return 0;
+  return (int)wino_stat_slots(g.T, cout_p, tile);
+}
+
+template <int MT>
+static void launch_wino_output(dim3 grid, hipStream_t s, const float* Mb, int cout_p, int H, int W,
+                               const WinoGeom& g, const float* bias, float* y, int ldy,
+                               float* partial) {
+  if (partial)
+    hipLaunchKernelGGL((wino_output_kernel<MT, true>), grid, dim3(256), 0, s, Mb, cout_p, H, W,
+                       g.TH, g.TW, g.T, bias, y, ldy, partial);
+  else
+    hipLaunchKernelGGL((wino_output_kernel<MT, false>), grid, dim3(256), 0, s, Mb, cout_p, H, W,
+                       g.TH, g.TW, g.T, bias, y, ldy, partial);
+}
+
+extern "C" int nsm_wino_output_stats(const float* Mb, int B, int H, int W, int cout_p, int tile,
+                                     const float* bias, float* y, int ldy, float* partial,
+                                     int nslot, void* stream) {
   NSM_CHECK_ARG(Mb && y && cout_p % 32 == 0 && ldy % 4 == 0, "wino_output: bad args");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output: bad tile or shape");
-  dim3 grid(grid_1d(g.T * cout_p / (tile == 6 ? 1 : 4)));
-  if (tile == 2)
-    hipLaunchKernelGGL(wino_output_kernel<2>, grid, dim3(256), 0, as_stream(stream), Mb, cout_p, H,
-                       W, g.TH, g.TW, g.T, bias, y, ldy);
-  else if (tile == 4)
-    hipLaunchKernelGGL(wino_output_kernel<4>, grid, dim3(256), 0, as_stream(stream), Mb, cout_p, H,
-                       W, g.TH, g.TW, g.T, bias, y, ldy);
-  else
-    hipLaunchKernelGGL(wino_output_kernel<6>, grid, dim3(256), 0, as_stream(stream), Mb, cout_p, H,
-                       W, g.TH, g.TW, g.T, bias, y, ldy);
+  const int N4 = cout_p / (tile == 6 ? 1 : 4);
+  dim3 grid(grid_1d(g.T * N4));
+  if (partial) {
+    NSM_CHECK_ARG(nslot > 0 && nslot % wino_stat_step(cout_p, tile) == 0 && nslot <= (1 << 20),
+                  "wino_output: nslot %d not a multiple of %d", nslot,
+                  wino_stat_step(cout_p, tile));
+    grid = dim3((unsigned)((long long)nslot * N4 / 256));
+  }
+  hipStream_t s = as_stream(stream);
+  if (tile == 2) launch_wino_output<2>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
+  else if (tile == 4) launch_wino_output<4>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
+  else launch_wino_output<6>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
   NSM_LAUNCH_CHECK("wino_output");
   return 0;
+}
+
+extern "C" int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, int tile,
+                               const float* bias, float* y, int ldy, void* stream) {
+  return nsm_wino_output_stats(Mb, B, H, W, cout_p, tile, bias, y, ldy, nullptr, 0, stream);
 }
 
 extern "C" int nsm_conv3x3_wino(const float* x, int ldx, int B, int H, int W, int cin_p,

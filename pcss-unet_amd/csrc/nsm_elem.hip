@@ -106,7 +106,9 @@ __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
   const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) *num_batches += n_updates;
   if (c >= C) return;
-  const size_t st = (size_t)2 * C;
+  // rpc == 0: counted partials [nchunk][3][C] = {sum, M2, count} (the Winograd
+  // output transform's slots); else {sum, M2} of rpc-row chunks
+  const size_t st = (size_t)(rpc ? 2 : 3) * C;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
   int k = lane;
   for (; k + 192 < nchunk; k += 256) {
@@ -119,14 +121,14 @@ __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
   const double mean = wave_sum_d((s0 + s1) + (s2 + s3)) / M;
   double q0 = 0.0, q1 = 0.0;
   for (k = lane; k < nchunk; k += 128) {
-    int n0 = min(M, k * rpc + rpc) - k * rpc;
+    int n0 = rpc ? min(M, k * rpc + rpc) - k * rpc : (int)partial[k * st + 2 * C + c];
     if (n0 > 0) {
       double d = partial[k * st + c] / n0 - mean;
       q0 += partial[k * st + C + c] + n0 * d * d;
     }
     int k1 = k + 64;
     if (k1 < nchunk) {
-      int n1 = min(M, k1 * rpc + rpc) - k1 * rpc;
+      int n1 = rpc ? min(M, k1 * rpc + rpc) - k1 * rpc : (int)partial[k1 * st + 2 * C + c];
       if (n1 > 0) {
         double d = partial[k1 * st + c] / n1 - mean;
         q1 += partial[k1 * st + C + c] + n1 * d * d;
@@ -158,28 +160,31 @@ __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
 // First level of the BN-partial merge for grids with many row chunks:
 // out[g] = Chan merge of chunks [g*G, (g+1)*G) (fixed order, double), one
 // thread per (group, channel), coalesced along channels.
+// rpc == 0: counted rows in and out ({sum, M2, count}, stride 3C)
 __global__ void bn_partials_merge_kernel(const float* __restrict__ partial, int nchunk, int rpc,
                                          int M, int C, int G, float* __restrict__ out) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   const int g = blockIdx.y;
   if (c >= C) return;
+  const size_t st = (size_t)(rpc ? 2 : 3) * C;
   const int k0 = g * G, k1 = min(nchunk, k0 + G);
   double s = 0.0;
   long long n = 0;
   for (int k = k0; k < k1; ++k) {
-    s += partial[(size_t)k * 2 * C + c];
-    n += max(0, min(M, (k + 1) * rpc) - k * rpc);
+    s += partial[(size_t)k * st + c];
+    n += rpc ? max(0, min(M, (k + 1) * rpc) - k * rpc) : (long long)partial[(size_t)k * st + 2 * C + c];
   }
   const double mean = n > 0 ? s / (double)n : 0.0;
   double m2 = 0.0;
   for (int k = k0; k < k1; ++k) {
-    const int nk = min(M, (k + 1) * rpc) - k * rpc;
+    const int nk = rpc ? min(M, (k + 1) * rpc) - k * rpc : (int)partial[(size_t)k * st + 2 * C + c];
     if (nk <= 0) continue;
-    const double d = partial[(size_t)k * 2 * C + c] / nk - mean;
-    m2 += partial[(size_t)k * 2 * C + C + c] + nk * d * d;
+    const double d = partial[(size_t)k * st + c] / nk - mean;
+    m2 += partial[(size_t)k * st + C + c] + nk * d * d;
   }
-  out[(size_t)g * 2 * C + c] = (float)s;
-  out[(size_t)g * 2 * C + C + c] = (float)m2;
+  out[(size_t)g * st + c] = (float)s;
+  out[(size_t)g * st + C + c] = (float)m2;
+  if (!rpc) out[(size_t)g * st + 2 * C + c] = (float)n;
 }
 
 // Plain-sum merge of partial rows (the BN-backward {sum dz, sum dz*xhat}
@@ -407,21 +412,7 @@ __global__ void __launch_bounds__(256) avgpool2_bwd_add_kernel(const T* __restri
 // scale=(in-1)/(out-1) in fp32, src=scale*dst, i0=floor, i1=i0+(i0<in-1),
 // l1=src-i0, l0=1-l1).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void lin_idx(float scale, int dst, int in, int& i0, int& i1, float& l0,
-                                        float& l1) {
-  // keep src rounded to fp32 as ATen does; letting the compiler contract
-  // scale*dst - i0 into one FMA shifts lambda by up to ~1e-5.
-#pragma clang fp contract(off)
-  float src = scale * (float)dst;
-  i0 = min((int)src, in - 1);
-  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
-  l0 = 1.f - l1;
-  i1 = i0 + (i0 < in - 1 ? 1 : 0);
-}
-
-static inline float ac_scale(int in, int out) {  // align_corners source step
-  return out > 1 ? (float)(in - 1) / (float)(out - 1) : 0.f;
-}
+// lin_idx / ac_scale: nsm_common.h
 
 // (pixel, 8-channel group) of a flat index over [B][H][W][C8] (32-bit fast division)
 struct Pix8 {
@@ -1355,7 +1346,8 @@ extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_
                                      float* invstd, float* scale, float* shift, void* stream) {
   NSM_CHECK_ARG(partial && gamma && beta && mean && invstd && scale && shift, "bn_finalize: null");
   NSM_CHECK_ARG(M > 1, "bn_finalize: Expected more than 1 value per channel when training");
-  NSM_CHECK_ARG(nchunk >= 1 && rows_per_chunk >= 1 && (long long)nchunk * rows_per_chunk >= M,
+  NSM_CHECK_ARG(nchunk >= 1 && (rows_per_chunk == 0 ||
+                                (rows_per_chunk >= 1 && (long long)nchunk * rows_per_chunk >= M)),
                 "bn_finalize: chunks do not cover M");
   hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(ceil_div(C, 4)), dim3(256), 0,
                      as_stream(stream), partial, nchunk, rows_per_chunk, M, C, c_real, gamma, beta,
@@ -1367,7 +1359,7 @@ extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_
 
 extern "C" int nsm_bn_partials_merge(const float* partial, int nchunk, int rows_per_chunk, int M,
                                      int C, int group, float* out, void* stream) {
-  NSM_CHECK_ARG(partial && out && nchunk >= 1 && group >= 1 && rows_per_chunk >= 1,
+  NSM_CHECK_ARG(partial && out && nchunk >= 1 && group >= 1 && rows_per_chunk >= 0,
                 "bn_partials_merge: bad args");
   dim3 grid(ceil_div(C, 256), ceil_div(nchunk, group));
   hipLaunchKernelGGL(bn_partials_merge_kernel, grid, dim3(256), 0, as_stream(stream), partial,

@@ -72,7 +72,8 @@ def _probe(tag):
 
 
 class Partials:
-    """Per-channel BN partials {sum, M2} over row chunks: [nchunk][2][C]."""
+    """Per-channel BN partials {sum, M2} over row chunks of rpc rows:
+    [nchunk][2][C]; rpc == 0: counted partials [nchunk][3][C] {sum, M2, count}."""
     __slots__ = ("buf", "nchunk", "rpc", "_merged")
 
     def __init__(self, buf, nchunk, rpc):
@@ -148,25 +149,49 @@ def wino_weight(w, n_p, k_p, flip, tile=4):
     return U
 
 
-def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, relu=False):
+def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, relu=False,
+                 stats=False, nslot=None, src_hw=None):
     """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(tile x tile, 3x3).
     keep_v=True also returns the transformed input V [(tile+2)^2][T][cin_p],
-    reused by the Winograd weight gradient."""
-    M, cin_p = x.shape
+    reused by the Winograd weight gradient. stats=True returns (y, V|None,
+    Partials|None): the BN batch-statistics partials of y written by the output
+    transform (counted layout, rpc 0), None where nsm_wino_stat_slots says the
+    separate pass is faster (nslot: override the slot count, tests).
+    src_hw=(hi, wi): x is [B*hi*wi, cin_p], convolved after a bilinear
+    align_corners resize to H x W that the input transform samples on the fly."""
+    from ._lib import lib
+    cin_p = x.shape[1]
+    M = B * H * W
+    hi, wi = src_hw if src_hw is not None else (H, W)
+    assert x.shape[0] == B * hi * wi, (x.shape, B, hi, wi)
     nb, T = (tile + 2) ** 2, wino_tiles(B, H, W, tile)
     V = empty(nb * T * cin_p, device=x.device)    # kept alive for the wgrad
     Mb = empty(nb * T * cout_p, device=x.device)
     y = empty(M, cout_p, device=x.device)
     st = stream()
     ev_all = _probe(tag)  # the whole convolution: input transform + GEMM + output transform
-    call("nsm_wino_input", ptr(x), x.stride(0), B, H, W, cin_p, tile, int(relu), ptr(V), st)
+    call("nsm_wino_input_resize", ptr(x), x.stride(0), B, hi, wi, H, W, cin_p, tile, int(relu),
+         ptr(V), st)
     ev = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
     call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb), st)
     if ev is not None:
         ev.record()
-    call("nsm_wino_output", ptr(Mb), B, H, W, cout_p, tile, ptr(bias), ptr(y), y.stride(0), st)
+    part = None
+    if not stats:
+        nslot = 0
+    elif nslot is None:
+        nslot = int(lib.nsm_wino_stat_slots(B, H, W, cout_p, tile))
+    if nslot > 0:
+        part = Partials(empty(nslot * 3 * cout_p, device=x.device), nslot, 0)
+        call("nsm_wino_output_stats", ptr(Mb), B, H, W, cout_p, tile, ptr(bias), ptr(y),
+             y.stride(0), ptr(part.buf), nslot, st)
+    else:
+        call("nsm_wino_output", ptr(Mb), B, H, W, cout_p, tile, ptr(bias), ptr(y), y.stride(0),
+             st)
     if ev_all is not None:
         ev_all.record()
+    if stats:
+        return y, (V if keep_v else None), part
     return (y, V) if keep_v else y
 
 
@@ -250,7 +275,7 @@ def merged(part, M, C):
     if part._merged is None:
         G = -(-part.nchunk // MERGE_ABOVE)
         n2 = -(-part.nchunk // G)
-        buf = empty(n2 * 2 * C, device=part.buf.device)
+        buf = empty(n2 * (2 if part.rpc else 3) * C, device=part.buf.device)
         call("nsm_bn_partials_merge", ptr(part.buf), part.nchunk, part.rpc, M, C, G, ptr(buf),
              stream())
         part._merged = Partials(buf, n2, part.rpc * G)

@@ -37,6 +37,12 @@ SLOPE = 0.2
 # forces one tile everywhere.
 WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "64"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
+# NSM_UP_WINO=0: materialise the decoder's x2-upsampled input of a Winograd
+# conv (nsm_resize_fwd) instead of sampling it inside the input transform
+UP_IN_WINO = os.environ.get("NSM_UP_WINO", "1") != "0"
+# NSM_WINO_STATS=0: the BN statistics of the Winograd layers by a separate
+# bn_stats pass instead of the output transform
+WINO_BN_STATS = os.environ.get("NSM_WINO_STATS", "1") != "0"
 _WINO_ENV = os.environ.get("NSM_WINO_TILE", "")
 WINO_TILE = int(_WINO_ENV) if _WINO_ENV else 4   # the tile of the VGG stack
 
@@ -389,14 +395,26 @@ class _BlockSaved:
                  "pw")
 
 
-def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None):
+def fuses_resize(blk, dtype):
+    """True when the block's 3x3 conv runs on Winograd and can sample the
+    decoder's x2 upsample inside its input transform (UP_IN_WINO)."""
+    return (UP_IN_WINO and dtype == torch.float32
+            and ops.pad32(blk.conv[0].in_channels) >= WINOGRAD_MIN_CHANNELS)
+
+
+def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None):
     """pw: the block's weight layouts (prep.StepWeights.block, all written by the
-    step's single preparation launch), or None to build them here per call."""
+    step's single preparation launch), or None to build them here per call.
+    src=(x_low, hi, wi): X is the bilinear resize of x_low to H x W, sampled
+    inside the Winograd input transform (X is None then; fuses_resize)."""
     c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
     ci, co = c0.in_channels, c4.out_channels
     cip, cop = ops.pad32(ci), ops.pad32(co)
-    assert X.shape[1] == cip, (X.shape, cip)
-    dtype = X.dtype
+    xin = X if src is None else src[0]
+    src_hw = None if src is None else (src[1], src[2])
+    assert xin.shape[1] == cip, (xin.shape, cip)
+    assert src is None or fuses_resize(blk, xin.dtype)
+    dtype = xin.dtype
     if pw is None:
         pw = LazyBlockWeights(blk, dtype)
     b1 = pw.vec("b1")
@@ -404,9 +422,17 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None):
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         tile = wino_tile(cip, H, W)
         U1 = pw.U1(tile, False)
-        Y1, V = ops.conv3x3_wino(X, B, H, W, U1, b1, cip, tile=tile, tag=name + ".conv.0.fwd",
-                                 keep_v=True)
-        part1 = ops.bn_partials(Y1) if training else None
+        part1 = None
+        if training and WINO_BN_STATS:
+            # the output transform also writes the BN batch-statistics partials
+            Y1, V, part1 = ops.conv3x3_wino(xin, B, H, W, U1, b1, cip, tile=tile,
+                                            tag=name + ".conv.0.fwd", keep_v=True, stats=True,
+                                            src_hw=src_hw)
+        else:
+            Y1, V = ops.conv3x3_wino(xin, B, H, W, U1, b1, cip, tile=tile,
+                                     tag=name + ".conv.0.fwd", keep_v=True, src_hw=src_hw)
+        if training and part1 is None:
+            part1 = ops.bn_partials(Y1)
     else:
         w1 = pw.w1(ops.PACK_FWD)
         Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd",
@@ -416,7 +442,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None):
         bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1, gamma=pw.vec("g1"),
                            beta=pw.vec("be1"))
     else:
-        bn1 = ops.bn_eval(bn1m, cip, ci, eps1, X.device, gamma=pw.vec("g1"), beta=pw.vec("be1"))
+        bn1 = ops.bn_eval(bn1m, cip, ci, eps1, xin.device, gamma=pw.vec("g1"), beta=pw.vec("be1"))
     w2 = pw.w2(ops.PACK_FWD)
     b2 = pw.vec("b2")
     A1 = None
@@ -432,7 +458,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None):
         bn2 = ops.bn_train(Y2, bn2m, co, bn2m.momentum, eps2, part=part2, gamma=pw.vec("g2"),
                            beta=pw.vec("be2"))
     else:
-        bn2 = ops.bn_eval(bn2m, cop, co, eps2, X.device, gamma=pw.vec("g2"), beta=pw.vec("be2"))
+        bn2 = ops.bn_eval(bn2m, cop, co, eps2, xin.device, gamma=pw.vec("g2"), beta=pw.vec("be2"))
     s = _BlockSaved()
     s.X, s.Y1, s.Y2, s.bn1, s.bn2, s.mask = X, Y1, Y2, bn1, bn2, mask
     s.pw = pw
@@ -554,13 +580,16 @@ class _UnetFn(torch.autograd.Function):
             with ops.stage(f"conv{k}.fwd"):
                 h2, w2 = 2 * h, 2 * w
                 th, tw = skip_shape[k]
+                src = None
                 if (th, tw) != (h2, w2):   # up x2 then _upsample_and_match, fused
                     up = ops.up2_resize(cur, B, h, w, th, tw)
+                elif fuses_resize(mod.block(k), cdt):  # sampled by the Winograd input transform
+                    up, src = None, (cur, h, w)
                 else:                      # match is the identity (bitwise, as in ATen)
                     up = ops.resize(cur, B, h, w, h2, w2)
                 ups[k] = (h, w, h2, w2, th, tw)
                 s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}",
-                               pw=sw.block(k) if sw else None)
+                               pw=sw.block(k) if sw else None, src=src)
                 saved[k] = s
                 res = c[SKIP_OF[k]] if k in SKIP_OF else None
                 cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)

@@ -143,6 +143,68 @@ def test_conv3x3_wgrad_winograd(ops, device, B, H, W, ci, co, tile):
     assert err <= WINO_TOL[tile]["wgrad"]
 
 
+@pytest.mark.parametrize("tile", [2, 4, 6])
+@pytest.mark.parametrize("B,hi,wi,H,W,ci,co", [(2, 8, 10, 16, 20, 64, 32), (1, 16, 16, 32, 32, 128, 128),
+                                              (2, 5, 7, 10, 14, 32, 64), (1, 67, 120, 134, 240, 64, 32),
+                                              (2, 4, 5, 7, 9, 32, 32)])
+def test_wino_input_fused_resize(ops, device, B, hi, wi, H, W, ci, co, tile):
+    """Winograd conv sampling a bilinear align_corners resize inside its input
+    transform (nsm_wino_input_resize) == resize then Winograd conv, and == the
+    PyTorch reference of interpolate + conv2d."""
+    g = torch.Generator().manual_seed(hi * wi + ci + tile)
+    x = torch.randn(B, ci, hi, wi, generator=g)
+    w = torch.randn(co, ci, 3, 3, generator=g) / (ci * 9) ** 0.5
+    b = torch.randn(co, generator=g)
+    ref = F.conv2d(F.interpolate(x, size=(H, W), mode="bilinear", align_corners=True), w, b,
+                   padding=1)
+    U = ops.wino_weight(w.to(device), co, ci, flip=False, tile=tile)
+    xl = nhwc(x).to(device)
+    y_f, V_f = ops.conv3x3_wino(xl, B, H, W, U, b.to(device), co, tile=tile, keep_v=True,
+                                src_hw=(hi, wi))
+    up = ops.resize(xl, B, hi, wi, H, W)
+    y_u, V_u = ops.conv3x3_wino(up, B, H, W, U, b.to(device), co, tile=tile, keep_v=True)
+    # the same interpolation formula; only FMA contraction may differ (1 ulp),
+    # which the F(6x6) transforms amplify a few times
+    assert rel(V_f.cpu(), V_u.cpu()) <= 2e-6
+    assert rel(y_f.cpu(), y_u.cpu()) <= 1e-5
+    err = (nchw(y_f.cpu(), B, H, W) - ref).abs().max().item() / max(1.0, ref.abs().max().item())
+    assert err <= WINO_TOL[tile]["fwd"]
+
+
+@pytest.mark.parametrize("tile", [2, 4, 6])
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 9, 11, 32, 64), (1, 16, 16, 128, 128), (3, 7, 5, 64, 32),
+                                        (2, 32, 32, 256, 1024), (8, 64, 64, 64, 64),
+                                        (1, 67, 120, 32, 96), (8, 256, 256, 64, 64)])
+def test_wino_output_bn_stats(ops, device, B, H, W, ci, co, tile):
+    """BN batch statistics written by the Winograd output transform (counted
+    partials, merged when > 1024 slots) == float64 statistics of the stored y,
+    and the running-stat update of bn_train on them: the tuned slot count where
+    it applies, the smallest valid one, and one > 1024 (merge)."""
+    import math
+    from nsm_amd._lib import lib
+    g = torch.Generator().manual_seed(ci + co + H * tile)
+    x = torch.randn(B, ci, H, W, generator=g)
+    w = torch.randn(co, ci, 3, 3, generator=g) / (ci * 9) ** 0.5
+    b = torch.randn(co, generator=g) * 2 + 1  # a large mean, as a pre-BN conv output has
+    U = ops.wino_weight(w.to(device), co, ci, flip=False, tile=tile)
+    step = 256 // math.gcd(co // (1 if tile == 6 else 4), 256)
+    tuned = int(lib.nsm_wino_stat_slots(B, H, W, co, tile))
+    if (B, H, W) == (8, 256, 256):
+        assert tuned > 1024  # conv8 / conv9 geometry: the stats form with a merge
+    for ns in sorted({tuned, step, step * -(-1100 // step)} - {0}):
+        y, _, part = ops.conv3x3_wino(nhwc(x).to(device), B, H, W, U, b.to(device), co, tile=tile,
+                                      stats=True, nslot=ns)
+        assert part is not None and part.rpc == 0 and part.nchunk == ns
+        yc = y.cpu().double()
+        bn = torch.nn.BatchNorm2d(co).to(device)
+        st = ops.bn_train(y, bn, co, 0.1, 1e-5, part=part)
+        mean, var_b, var_u = yc.mean(0), yc.var(0, unbiased=False), yc.var(0, unbiased=True)
+        inv = 1 / (var_b + 1e-5).sqrt()
+        assert (st.mean.cpu().double() - mean).abs().max() <= 2e-6 * max(1.0, mean.abs().max().item())
+        assert (st.invstd.cpu().double() - inv).abs().max() <= 2e-5 * inv.max()
+        assert (bn.running_var.cpu().double() - (0.9 + 0.1 * var_u)).abs().max() <= 1e-4 * max(1.0, var_u.max().item())
+
+
 def test_conv_padded_channels(ops, device):
     """conv2 of the 7-channel model: 28 real channels padded to 32."""
     B, H, W, ci, co = 2, 10, 12, 28, 28
