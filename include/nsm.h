@@ -223,6 +223,26 @@ int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, void* y, int t
                        int dtype, void* stream);
 int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th, int tw,
                        int dtype, void* stream);
+/* The same three gradient producers, also writing the BN-backward partials
+ * {sum dz, sum dz*xhat} (nsm_bn_bwd_reduce's format, one row per kernel
+ * block) of the block output they produce the gradient of: y2 = that block's
+ * second BN input (Unetmodel.py:26-28), dz = g * lrelu'(y2*scale+shift), g
+ * as written. partial[nchunk][2][C], nchunk = nsm_bnred_chunks(kind, ...)
+ * (kind 0 avgpool2_bwd_add with H, W of dx; 1 resize_bwd with Hi, Wi; 2
+ * up2_resize_bwd with h, w); 0 there = not available for this shape. */
+int nsm_bnred_chunks(int kind, int B, int H, int W, int C);
+int nsm_avgpool2_bwd_add_bnred(const void* dy, int B, int H, int W, int C, const void* skip,
+                               void* dx, int dtype, const void* y2, const float* scale,
+                               const float* shift, const float* mean, const float* invstd,
+                               float slope, float* partial, void* stream);
+int nsm_resize_bwd_bnred(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho, int Wo,
+                         int dtype, const void* y2, const float* scale, const float* shift,
+                         const float* mean, const float* invstd, float slope, float* partial,
+                         void* stream);
+int nsm_up2_resize_bwd_bnred(const void* dy, int B, int h, int w, int C, void* dx, int th, int tw,
+                             int dtype, const void* y2, const float* scale, const float* shift,
+                             const float* mean, const float* invstd, float slope, float* partial,
+                             void* stream);
 
 /* ---- model boundary ---------------------------------------------------------
  * pixel_unshuffle(2) + NCHW->NHWC + channel pad (Unetmodel.py:65-67,101) */

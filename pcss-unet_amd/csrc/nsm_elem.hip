@@ -358,6 +358,69 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   }
 }
 
+// BN-backward reduction fused into the kernel that PRODUCES a block output's
+// gradient g (the pooling / resize backward): with y = that block's BN input
+// Y2, {sum dz, sum dz*xhat} per channel of dz = g * lrelu'(y*scale+shift)
+// (no dropout after the second BN, Unetmodel.py:27-28), summed over the
+// kernel's block and written as partial row blockIdx.x of [gridDim.x][2][C]
+// (the nsm_bn_bwd_reduce format) — the separate reduce pass and its read of g
+// are gone. Each thread keeps ONE 8-channel group (C/8 divides 256).
+struct BnRedP {
+  const void* y;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* invstd;
+  float slope;
+  float* partial;
+};
+template <typename T>
+__device__ __forceinline__ F8 as_stored8(F8 v);
+template <>
+__device__ __forceinline__ F8 as_stored8<float>(F8 v) { return v; }
+template <>
+__device__ __forceinline__ F8 as_stored8<bf16_t>(F8 v) {
+  const u32x4 w = u32x4{pack_bf2(v.a.x, v.a.y), pack_bf2(v.a.z, v.a.w), pack_bf2(v.b.x, v.b.y),
+                        pack_bf2(v.b.z, v.b.w)};
+  return F8{f32x4{bf_lo(w.x), bf_hi(w.x), bf_lo(w.y), bf_hi(w.y)},
+            f32x4{bf_lo(w.z), bf_hi(w.z), bf_lo(w.w), bf_hi(w.w)}};
+}
+struct BnRedAcc {
+  F8 sc, sh, mu, is, s1, s2;
+  __device__ void init(const BnRedP& r, int c) {
+    sc = ldf8(r.scale + c);
+    sh = ldf8(r.shift + c);
+    mu = ldf8(r.mean + c);
+    is = ldf8(r.invstd + c);
+    s1 = f8zero();
+    s2 = f8zero();
+  }
+  // g: the value as written (T-rounded); p: its pixel row in y
+  template <typename T>
+  __device__ void add(const BnRedP& r, F8 g, size_t p, int C, int c) {
+    const F8 v = ld8((const T*)r.y + p * C + c);
+    const F8 dz = bn_dz8(g, v, sc, sh, r.slope, nullptr, 0, C, c);
+    s1 += dz;
+    s2 += dz * ((v - mu) * is);
+  }
+  // whole block (256 threads, group = tid % C8) -> partial row blockIdx.x
+  __device__ void write(const BnRedP& r, int C8) {
+    __shared__ F8 red[256];
+    const int tid = threadIdx.x, rl = 256 / C8, tc = tid % C8, C = C8 * 8;
+    red[tid] = s1;
+    col_tree_reduce(red, C8, rl, tid);
+    const F8 t1 = red[tc];
+    __syncthreads();
+    red[tid] = s2;
+    col_tree_reduce(red, C8, rl, tid);
+    if (tid < C8) {
+      float* pr = r.partial + (size_t)blockIdx.x * 2 * C;
+      st8(pr + tc * 8, t1);
+      st8(pr + C + tc * 8, red[tc]);
+    }
+  }
+};
+
 // ---------------------------------------------------------------------------
 // AvgPool2d(2), floor mode
 // ---------------------------------------------------------------------------
@@ -385,14 +448,16 @@ __global__ void __launch_bounds__(256) avgpool2_fwd_kernel(const T* __restrict__
   }
 }
 
-template <typename T>
+template <typename T, bool RED>
 __global__ void __launch_bounds__(256) avgpool2_bwd_add_kernel(const T* __restrict__ dy, int B,
                                                                int H, int W, int C8, FastDiv fdC8,
                                                                FastDiv fdW, FastDiv fdH,
                                                                const T* __restrict__ skip,
-                                                               T* __restrict__ dx) {
+                                                               T* __restrict__ dx, BnRedP rp) {
   const int Ho = H / 2, Wo = W / 2, C = C8 * 8;
   const uint32_t total = (uint32_t)B * H * W * C8;
+  BnRedAcc ra;
+  if (RED) ra.init(rp, (threadIdx.x % C8) * 8);
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     const uint32_t p = fdiv(i, fdC8);
     const int c = (int)(i - p * (uint32_t)C8) * 8;
@@ -404,7 +469,9 @@ __global__ void __launch_bounds__(256) avgpool2_bwd_add_kernel(const T* __restri
     const int oy = yy >> 1, ox = xx >> 1;
     if (oy < Ho && ox < Wo) v += 0.25f * ld8(dy + (((size_t)b * Ho + oy) * Wo + ox) * C + c);
     st8(dx + (size_t)p * C + c, v);
+    if (RED) ra.add<T>(rp, as_stored8<T>(v), p, C, c);
   }
+  if (RED) ra.write(rp, C8);
 }
 
 // ---------------------------------------------------------------------------
@@ -790,10 +857,10 @@ __global__ void __launch_bounds__(256) up2_resize_bwd8_kernel(const T* __restric
 // lane: ALU-bound), the row's y window once; the lanes then only gather.
 constexpr int U2_MAXW = 2048;  // widest row the LDS tables hold
 
-template <typename T>
+template <typename T, bool RED>
 __global__ void __launch_bounds__(256) up2_resize_bwd_rows_kernel(
     const T* __restrict__ dy, int h, int w, int C8, FastDiv fdC8, T* __restrict__ dx, int th,
-    int tw, float s1h, float s1w, float s2h, float s2w) {
+    int tw, float s1h, float s1w, float s2h, float s2w, BnRedP rp) {
   extern __shared__ float u2_tables[];  // [w][RS_W] weights, [w] window starts, [w] widths
   float* xw = u2_tables;
   int* xlo = (int*)(u2_tables + (size_t)w * RS_W);
@@ -834,6 +901,8 @@ __global__ void __launch_bounds__(256) up2_resize_bwd_rows_kernel(
   const T* base = dy + (size_t)b * th * tw * C;
   T* orow = dx + ((size_t)b * h + iy) * w * C;
   const uint32_t items = (uint32_t)w * (uint32_t)C8;
+  BnRedAcc ra;
+  if (RED) ra.init(rp, (threadIdx.x % C8) * 8);
   for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
     const int ix = (int)fdiv(it, fdC8);
     const int c = (int)(it - (uint32_t)ix * (uint32_t)C8) * 8;
@@ -863,14 +932,16 @@ __global__ void __launch_bounds__(256) up2_resize_bwd_rows_kernel(
       }
     }
     st8(orow + (size_t)ix * C + c, acc);
+    if (RED) ra.add<T>(rp, as_stored8<T>(acc), ((size_t)b * h + iy) * w + ix, C, c);
   }
+  if (RED) ra.write(rp, C8);
 }
 
 // Row-blocked single-step resize backward (same scheme as the composite's).
-template <typename T>
+template <typename T, bool RED>
 __global__ void __launch_bounds__(256) resize_bwd_rows_kernel(
     const T* __restrict__ dy, int h, int w, int C8, FastDiv fdC8, T* __restrict__ dx, int th,
-    int tw, float sh, float sw) {
+    int tw, float sh, float sw, BnRedP rp) {
   extern __shared__ float rs_tables[];  // [w][RS_W] weights, [w] window starts, [w] widths
   float* xw = rs_tables;
   int* xlo = (int*)(rs_tables + (size_t)w * RS_W);
@@ -903,6 +974,8 @@ __global__ void __launch_bounds__(256) resize_bwd_rows_kernel(
   const T* base = dy + (size_t)b * th * tw * C;
   T* orow = dx + ((size_t)b * h + iy) * w * C;
   const uint32_t items = (uint32_t)w * (uint32_t)C8;
+  BnRedAcc ra;
+  if (RED) ra.init(rp, (threadIdx.x % C8) * 8);
   for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
     const int ix = (int)fdiv(it, fdC8);
     const int c = (int)(it - (uint32_t)ix * (uint32_t)C8) * 8;
@@ -932,7 +1005,9 @@ __global__ void __launch_bounds__(256) resize_bwd_rows_kernel(
       }
     }
     st8(orow + (size_t)ix * C + c, acc);
+    if (RED) ra.add<T>(rp, as_stored8<T>(acc), ((size_t)b * h + iy) * w + ix, C, c);
   }
+  if (RED) ra.write(rp, C8);
 }
 
 // ---------------------------------------------------------------------------
@@ -1498,23 +1573,32 @@ extern "C" int nsm_avgpool2_fwd(const void* x, int B, int H, int W, int C, void*
   return 0;
 }
 
-extern "C" int nsm_avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, const void* skip,
-                                    void* dx, int dtype, void* stream) {
+static int avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, const void* skip, void* dx,
+                            int dtype, const BnRedP* rp, void* stream) {
   NSM_CHECK_ARG(dy && dx && C % 8 == 0, "avgpool2_bwd: bad args");
   long long work = (long long)B * H * W * (C / 8);
   NSM_CHECK_ARG(work < (1ll << 31), "avgpool2_bwd: too large");
+  NSM_CHECK_ARG(!rp || 256 % (C / 8) == 0, "avgpool2_bwd: fused BN reduction needs C/8 | 256");
   dim3 g(grid_for(work));
   const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(W), fh = make_fastdiv(H);
-  if (dtype == NSM_BF16)
-    hipLaunchKernelGGL(avgpool2_bwd_add_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(bf16_t, dy), B, H, W, C / 8, f8, fw, fh, NSM_CT(bf16_t, skip),
-                       NSM_T(bf16_t, dx));
-  else
-    hipLaunchKernelGGL(avgpool2_bwd_add_kernel<float>, g, dim3(256), 0, as_stream(stream),
-                       NSM_CT(float, dy), B, H, W, C / 8, f8, fw, fh, NSM_CT(float, skip),
-                       NSM_T(float, dx));
+  const BnRedP r = rp ? *rp : BnRedP{};
+  hipStream_t s = as_stream(stream);
+#define A_(T) NSM_CT(T, dy), B, H, W, C / 8, f8, fw, fh, NSM_CT(T, skip), NSM_T(T, dx), r
+  if (dtype == NSM_BF16) {
+    if (rp) hipLaunchKernelGGL((avgpool2_bwd_add_kernel<bf16_t, true>), g, dim3(256), 0, s, A_(bf16_t));
+    else hipLaunchKernelGGL((avgpool2_bwd_add_kernel<bf16_t, false>), g, dim3(256), 0, s, A_(bf16_t));
+  } else {
+    if (rp) hipLaunchKernelGGL((avgpool2_bwd_add_kernel<float, true>), g, dim3(256), 0, s, A_(float));
+    else hipLaunchKernelGGL((avgpool2_bwd_add_kernel<float, false>), g, dim3(256), 0, s, A_(float));
+  }
+#undef A_
   NSM_LAUNCH_CHECK("avgpool2_bwd");
   return 0;
+}
+
+extern "C" int nsm_avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, const void* skip,
+                                    void* dx, int dtype, void* stream) {
+  return avgpool2_bwd_add(dy, B, H, W, C, skip, dx, dtype, nullptr, stream);
 }
 
 // NSM_RESIZE_ROWS=0: per-element resize backward instead of the row-blocked one
@@ -1558,32 +1642,38 @@ extern "C" int nsm_resize_fwd(const void* x, int B, int Hi, int Wi, int C, void*
   return 0;
 }
 
-extern "C" int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho, int Wo,
-                              int dtype, void* stream) {
+static int resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho, int Wo,
+                      int dtype, const BnRedP* rp, void* stream) {
   NSM_CHECK_ARG(dy && dx && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 && C > 0,
                 "resize_bwd: bad args");
   const float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
   hipStream_t s = as_stream(stream);
   const long long tot8 = (long long)B * Hi * Wi * (C / 8);
+  const BnRedP r = rp ? *rp : BnRedP{};
   if (C % 8 == 0 && tot8 < (1ll << 31)) {
     dim3 g(xcd_grid(tot8));
     const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(Wi), fh = make_fastdiv(Hi);
     if (Wi <= U2_MAXW && (long long)B * Hi < (1ll << 31) && rows_resize()) {
+      NSM_CHECK_ARG(!rp || 256 % (C / 8) == 0, "resize_bwd: fused BN reduction needs C/8 | 256");
       const size_t lds = (size_t)Wi * (RS_W + 2) * 4;
-#define A_(T) NSM_CT(T, dy), Hi, Wi, C / 8, f8, NSM_T(T, dx), Ho, Wo, sh, sw
-      if (dtype == NSM_BF16)
-        hipLaunchKernelGGL(resize_bwd_rows_kernel<bf16_t>, dim3((unsigned)(B * Hi)), dim3(256), lds,
-                           s, A_(bf16_t));
-      else
-        hipLaunchKernelGGL(resize_bwd_rows_kernel<float>, dim3((unsigned)(B * Hi)), dim3(256), lds,
-                           s, A_(float));
+      const dim3 gr((unsigned)(B * Hi));
+#define A_(T) NSM_CT(T, dy), Hi, Wi, C / 8, f8, NSM_T(T, dx), Ho, Wo, sh, sw, r
+      if (dtype == NSM_BF16) {
+        if (rp) hipLaunchKernelGGL((resize_bwd_rows_kernel<bf16_t, true>), gr, dim3(256), lds, s, A_(bf16_t));
+        else hipLaunchKernelGGL((resize_bwd_rows_kernel<bf16_t, false>), gr, dim3(256), lds, s, A_(bf16_t));
+      } else {
+        if (rp) hipLaunchKernelGGL((resize_bwd_rows_kernel<float, true>), gr, dim3(256), lds, s, A_(float));
+        else hipLaunchKernelGGL((resize_bwd_rows_kernel<float, false>), gr, dim3(256), lds, s, A_(float));
+      }
 #undef A_
     } else {
+      NSM_CHECK_ARG(!rp, "resize_bwd: fused BN reduction needs the row-blocked kernel");
 #define A_(T) NSM_CT(T, dy), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), Ho, Wo, sh, sw
       NSM_DT(resize_bwd8_kernel, A_);
 #undef A_
     }
   } else {
+    NSM_CHECK_ARG(!rp, "resize_bwd: fused BN reduction needs C % 8 == 0");
     dim3 g(grid_for((long long)B * Hi * Wi * C));
 #define A_(T) NSM_CT(T, dy), B, Hi, Wi, C, NSM_T(T, dx), Ho, Wo, sh, sw
     NSM_DT(resize_bwd1_kernel, A_);
@@ -1591,6 +1681,11 @@ extern "C" int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void
   }
   NSM_LAUNCH_CHECK("resize_bwd");
   return 0;
+}
+
+extern "C" int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho, int Wo,
+                              int dtype, void* stream) {
+  return resize_bwd(dy, B, Hi, Wi, C, dx, Ho, Wo, dtype, nullptr, stream);
 }
 
 extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, void* y, int th,
@@ -1624,8 +1719,8 @@ extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, voi
   return 0;
 }
 
-extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th,
-                                  int tw, int dtype, void* stream) {
+static int up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th, int tw,
+                          int dtype, const BnRedP* rp, void* stream) {
   NSM_CHECK_ARG(dy && dx && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 && C % 8 == 0,
                 "up2_resize_bwd: bad args");
   const long long tot8 = (long long)B * h * w * (C / 8);
@@ -1635,17 +1730,22 @@ extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, vo
   const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
               d = ac_scale(2 * w, tw);
   const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(w), fh = make_fastdiv(h);
+  const BnRedP r = rp ? *rp : BnRedP{};
   if (w <= U2_MAXW && (long long)B * h < (1ll << 31)) {
+    NSM_CHECK_ARG(!rp || 256 % (C / 8) == 0, "up2_resize_bwd: fused BN reduction needs C/8 | 256");
     const size_t lds = (size_t)w * (RS_W + 2) * 4;
-#define A_(T) NSM_CT(T, dy), h, w, C / 8, f8, NSM_T(T, dx), th, tw, a, b, c, d
-    if (dtype == NSM_BF16)
-      hipLaunchKernelGGL(up2_resize_bwd_rows_kernel<bf16_t>, dim3((unsigned)(B * h)), dim3(256),
-                         lds, s, A_(bf16_t));
-    else
-      hipLaunchKernelGGL(up2_resize_bwd_rows_kernel<float>, dim3((unsigned)(B * h)), dim3(256),
-                         lds, s, A_(float));
+    const dim3 gr((unsigned)(B * h));
+#define A_(T) NSM_CT(T, dy), h, w, C / 8, f8, NSM_T(T, dx), th, tw, a, b, c, d, r
+    if (dtype == NSM_BF16) {
+      if (rp) hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<bf16_t, true>), gr, dim3(256), lds, s, A_(bf16_t));
+      else hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<bf16_t, false>), gr, dim3(256), lds, s, A_(bf16_t));
+    } else {
+      if (rp) hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<float, true>), gr, dim3(256), lds, s, A_(float));
+      else hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<float, false>), gr, dim3(256), lds, s, A_(float));
+    }
 #undef A_
   } else {
+    NSM_CHECK_ARG(!rp, "up2_resize_bwd: fused BN reduction needs the row-blocked kernel");
 #define A_(T) NSM_CT(T, dy), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, dx), th, tw, a, b, c, d
     NSM_DT(up2_resize_bwd8_kernel, A_);
 #undef A_
@@ -1653,6 +1753,54 @@ extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, vo
   NSM_LAUNCH_CHECK("up2_resize_bwd");
   return 0;
 }
+
+extern "C" int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th,
+                                  int tw, int dtype, void* stream) {
+  return up2_resize_bwd(dy, B, h, w, C, dx, th, tw, dtype, nullptr, stream);
+}
+
+// ---- gradient producers with the fused BN-backward reduction (BnRedP) ----
+// kind 0: nsm_avgpool2_bwd_add (H, W: dx's size), 1: nsm_resize_bwd (Hi, Wi),
+// 2: nsm_up2_resize_bwd (h, w). Partial rows the call writes; 0 = the fused
+// form does not apply (use the plain call + nsm_bn_bwd_reduce).
+extern "C" int nsm_bnred_chunks(int kind, int B, int H, int W, int C) {
+  if (B <= 0 || H <= 0 || W <= 0 || C % 8 || 256 % (C / 8)) return 0;
+  if (kind == 0) {
+    const long long work = (long long)B * H * W * (C / 8);
+    return work < (1ll << 31) ? grid_for(work) : 0;
+  }
+  if (kind == 1 && !rows_resize()) return 0;
+  if ((kind == 1 || kind == 2) && W <= U2_MAXW && (long long)B * H < (1ll << 31) &&
+      (long long)B * H * W * (C / 8) < (1ll << 31))
+    return B * H;
+  return 0;
+}
+
+#define NSM_BNRED_ARGS                                                                  \
+  const void *y2, const float *scale, const float *shift, const float *mean,            \
+      const float *invstd, float slope, float *partial
+#define NSM_BNRED_CHECK(what)                                                           \
+  NSM_CHECK_ARG(y2 && scale && shift && mean && invstd && partial, what ": null BN args"); \
+  const BnRedP rp{y2, scale, shift, mean, invstd, slope, partial}
+
+extern "C" int nsm_avgpool2_bwd_add_bnred(const void* dy, int B, int H, int W, int C,
+                                          const void* skip, void* dx, int dtype, NSM_BNRED_ARGS,
+                                          void* stream) {
+  NSM_BNRED_CHECK("avgpool2_bwd_add_bnred");
+  return avgpool2_bwd_add(dy, B, H, W, C, skip, dx, dtype, &rp, stream);
+}
+extern "C" int nsm_resize_bwd_bnred(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho,
+                                    int Wo, int dtype, NSM_BNRED_ARGS, void* stream) {
+  NSM_BNRED_CHECK("resize_bwd_bnred");
+  return resize_bwd(dy, B, Hi, Wi, C, dx, Ho, Wo, dtype, &rp, stream);
+}
+extern "C" int nsm_up2_resize_bwd_bnred(const void* dy, int B, int h, int w, int C, void* dx,
+                                        int th, int tw, int dtype, NSM_BNRED_ARGS, void* stream) {
+  NSM_BNRED_CHECK("up2_resize_bwd_bnred");
+  return up2_resize_bwd(dy, B, h, w, C, dx, th, tw, dtype, &rp, stream);
+}
+#undef NSM_BNRED_ARGS
+#undef NSM_BNRED_CHECK
 #undef NSM_DT
 
 extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, void* out, int cp,

@@ -50,6 +50,10 @@ _SIGS = {
     "nsm_bn_bwd_finalize": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
     "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
     "nsm_sum_rows": (I, [P, I, I, I, P, P]),
+    "nsm_bnred_chunks": (I, [I, I, I, I, I]),
+    "nsm_avgpool2_bwd_add_bnred": (I, [P, I, I, I, I, P, P, I, P, P, P, P, P, F, P, P]),
+    "nsm_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P]),
+    "nsm_up2_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P]),
     "nsm_wino_input_resize": (I, [P, I, I, I, I, I, I, I, I, I, P, P]),
     "nsm_wino_output_stats": (I, [P, I, I, I, I, I, P, P, I, P, I, P]),
     "nsm_wino_stat_slots": (I, [I, I, I, I, I]),

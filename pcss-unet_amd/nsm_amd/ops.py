@@ -340,16 +340,27 @@ def bn_act(y, st, slope=0.2, res=None, out=None, mask=None, HW=0):
     return o
 
 
-def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2):
+def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, part=None):
     """Backward through lrelu(.)*mask after a train-mode BN: returns dy
-    (grad wrt the BN input) and writes dgamma/dbeta/dbias_prev (real chans)."""
+    (grad wrt the BN input) and writes dgamma/dbeta/dbias_prev (real chans).
+    part=(partial, nchunk): the {sum dz, sum dz*xhat} partials already written
+    by g's producer (GradPart), so the reduce pass is skipped."""
     M, C = y.shape
-    nchunk = reduce_chunks(M, C)
-    partial = empty(nchunk * 2 * C, device=y.device)
     assert g.dtype == y.dtype
-    call("nsm_bn_bwd_reduce", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
-         ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(st.invstd), ptr(partial), nchunk,
-         dt(y), stream())
+    if part is None:
+        nchunk = reduce_chunks(M, C)
+        partial = empty(nchunk * 2 * C, device=y.device)
+        call("nsm_bn_bwd_reduce", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW,
+             ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(st.invstd),
+             ptr(partial), nchunk, dt(y), stream())
+    else:
+        partial, nchunk = part
+        if nchunk > SUM_ROWS_ABOVE:
+            G = -(-nchunk // SUM_ROWS_ABOVE)
+            n2 = -(-nchunk // G)
+            buf = empty(n2 * 2 * C, device=y.device)
+            call("nsm_sum_rows", ptr(partial), nchunk, 2 * C, G, ptr(buf), stream())
+            partial, nchunk = buf, n2
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
          ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
@@ -416,12 +427,36 @@ def avgpool2(x, B, H, W):
     return y
 
 
-def avgpool2_bwd_add(dy, B, H, W, skip):
+def _bnred(kind, B, H, W, C, bnred, device, slope=0.2):
+    """(extra C-ABI args, (partial, nchunk)) for a gradient producer that also
+    reduces the BN backward of bnred = (y2, BNState); (None, None) when the
+    fused form does not apply to this shape."""
+    from ._lib import lib
+    if bnred is None:
+        return None, None
+    n = int(lib.nsm_bnred_chunks(kind, B, H, W, C))
+    if n <= 0:
+        return None, None
+    y2, st = bnred
+    partial = empty(n * 2 * C, device=device)
+    return ((ptr(y2), ptr(st.scale), ptr(st.shift), ptr(st.mean), ptr(st.invstd), slope,
+             ptr(partial)), (partial, n))
+
+
+def avgpool2_bwd_add(dy, B, H, W, skip, bnred=None):
+    """AvgPool2d backward + skip-gradient add. bnred=(y2, BNState): returns
+    (dx, part) with the BN-backward partials of dx for that BN (part None
+    when the fused form does not apply)."""
     C = dy.shape[1]
     dx = like(B * H * W, C, dy)
     assert skip is None or skip.dtype == dy.dtype
-    call("nsm_avgpool2_bwd_add", ptr(dy), B, H, W, C, ptr(skip), ptr(dx), dt(dy), stream())
-    return dx
+    extra, part = _bnred(0, B, H, W, C, bnred, dy.device)
+    if extra is None:
+        call("nsm_avgpool2_bwd_add", ptr(dy), B, H, W, C, ptr(skip), ptr(dx), dt(dy), stream())
+    else:
+        call("nsm_avgpool2_bwd_add_bnred", ptr(dy), B, H, W, C, ptr(skip), ptr(dx), dt(dy),
+             *extra, stream())
+    return dx if bnred is None else (dx, part)
 
 
 def resize(x, B, Hi, Wi, Ho, Wo):
@@ -431,11 +466,17 @@ def resize(x, B, Hi, Wi, Ho, Wo):
     return y
 
 
-def resize_bwd(dy, B, Hi, Wi, Ho, Wo):
+def resize_bwd(dy, B, Hi, Wi, Ho, Wo, bnred=None):
+    """bnred: as avgpool2_bwd_add (returns (dx, part))."""
     C = dy.shape[-1]
     dx = like(B * Hi * Wi, C, dy)
-    call("nsm_resize_bwd", ptr(dy), B, Hi, Wi, C, ptr(dx), Ho, Wo, dt(dy), stream())
-    return dx
+    extra, part = _bnred(1, B, Hi, Wi, C, bnred, dy.device)
+    if extra is None:
+        call("nsm_resize_bwd", ptr(dy), B, Hi, Wi, C, ptr(dx), Ho, Wo, dt(dy), stream())
+    else:
+        call("nsm_resize_bwd_bnred", ptr(dy), B, Hi, Wi, C, ptr(dx), Ho, Wo, dt(dy), *extra,
+             stream())
+    return dx if bnred is None else (dx, part)
 
 
 def up2_resize(x, B, h, w, th, tw):
@@ -446,11 +487,17 @@ def up2_resize(x, B, h, w, th, tw):
     return y
 
 
-def up2_resize_bwd(dy, B, h, w, th, tw):
+def up2_resize_bwd(dy, B, h, w, th, tw, bnred=None):
+    """bnred: as avgpool2_bwd_add (returns (dx, part))."""
     C = dy.shape[-1]
     dx = like(B * h * w, C, dy)
-    call("nsm_up2_resize_bwd", ptr(dy), B, h, w, C, ptr(dx), th, tw, dt(dy), stream())
-    return dx
+    extra, part = _bnred(2, B, h, w, C, bnred, dy.device)
+    if extra is None:
+        call("nsm_up2_resize_bwd", ptr(dy), B, h, w, C, ptr(dx), th, tw, dt(dy), stream())
+    else:
+        call("nsm_up2_resize_bwd_bnred", ptr(dy), B, h, w, C, ptr(dx), th, tw, dt(dy), *extra,
+             stream())
+    return dx if bnred is None else (dx, part)
 
 
 # ---- boundary ----------------------------------------------------------------

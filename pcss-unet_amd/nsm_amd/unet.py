@@ -76,6 +76,11 @@ F32_MATERIALIZE_ACT = os.environ.get("NSM_F32_ACT", "1") != "0"
 # partials (the reduce pass's dA1 read is gone); 2 (default): per layer, see
 # bnb_mode.
 BNB_MODE = int(os.environ.get("NSM_BNB", "2"))
+# The output BN's backward reduction of blocks 2-8 rides in the kernel that
+# produces their gradient (resize / pooling backward: ops.avgpool2_bwd_add,
+# ops.resize_bwd, ops.up2_resize_bwd with bnred=); NSM_GRAD_BNRED=0 runs the
+# separate nsm_bn_bwd_reduce pass instead
+GRAD_BNRED = os.environ.get("NSM_GRAD_BNRED", "1") != "0"
 
 
 def bnb_mode(cip, cop, dtype):
@@ -468,14 +473,16 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None):
     return s
 
 
-def _block_bwd(blk, s, G, grads, need_dx, name=""):
-    """G: grad wrt the block output z = lrelu(bn2(Y2)) [M, cop]."""
+def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
+    """G: grad wrt the block output z = lrelu(bn2(Y2)) [M, cop]; gpart: the
+    BN-backward partials of G that its producer already wrote (ops.bn_bwd)."""
     c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
     ci, co = c0.in_channels, c4.out_channels
     B, H, W = s.B, s.H, s.W
     HW = H * W
     g = grads
-    dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias])
+    dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias],
+                     part=gpart)
     dtype = G.dtype
     w2d = s.pw.w2(ops.PACK_DGRAD)
     if s.A1 is not None:
@@ -636,15 +643,23 @@ class _UnetFn(torch.autograd.Function):
                              grads[mod.conv10.weight], grads[mod.conv10.bias])
         sb = ctx.saved_blocks
         skip_grad = {}
+        gpart = None
         for k in (9, 8, 7, 6):
             s = sb[k]
             with ops.stage(f"conv{k}.bwd"):
-                dX = _block_bwd(mod.block(k), s, G, grads, True, f"conv{k}")
+                dX = _block_bwd(mod.block(k), s, G, grads, True, f"conv{k}", gpart=gpart)
                 h, w, h2, w2, th, tw = ctx.ups[k]
+                # the x2 resize backward also reduces block k-1's output-BN
+                # backward (not the up9 composite: its gather kernel measured
+                # slower with the reduction than the separate pass, bf16 B=64
+                # conv9 stage 4.43 -> 4.70 ms)
                 if (th, tw) != (h2, w2):
-                    dprev = ops.up2_resize_bwd(dX, B, h, w, th, tw)
+                    dprev, gpart = ops.up2_resize_bwd(dX, B, h, w, th, tw), None
+                elif GRAD_BNRED:
+                    dprev, gpart = ops.resize_bwd(dX, B, h, w, h2, w2,
+                                                  bnred=(sb[k - 1].Y2, sb[k - 1].bn2))
                 else:
-                    dprev = ops.resize_bwd(dX, B, h, w, h2, w2)
+                    dprev, gpart = ops.resize_bwd(dX, B, h, w, h2, w2), None
             # the previous merge / c5 receives dprev; merge_{k-1} = conv + c_skip
             if k - 1 in SKIP_OF:
                 skip_grad[SKIP_OF[k - 1]] = dprev
@@ -657,7 +672,8 @@ class _UnetFn(torch.autograd.Function):
             s = sb[k]
             st = ops.stage(f"conv{k}.bwd")
             st.__enter__()
-            dX = _block_bwd(mod.block(k), s, G, grads, need_dx=(k > 2 or need_x), name=f"conv{k}")
+            dX = _block_bwd(mod.block(k), s, G, grads, need_dx=(k > 2 or need_x), name=f"conv{k}",
+                            gpart=gpart)
             if k == 5 and training and mod.emulate_checkpoint_bn:
                 # checkpoint recompute of conv5 (Unetmodel.py:114-116): 2nd BN update
                 blk = mod.block(5)
@@ -668,7 +684,11 @@ class _UnetFn(torch.autograd.Function):
                                       blk.conv[5].momentum, blk.conv[5].eps)
             if k > 2:
                 ph, pw = sb[k - 1].H, sb[k - 1].W
-                G = ops.avgpool2_bwd_add(dX, B, ph, pw, skip_grad.get(k - 1))
+                if GRAD_BNRED:
+                    G, gpart = ops.avgpool2_bwd_add(dX, B, ph, pw, skip_grad.get(k - 1),
+                                                    bnred=(sb[k - 1].Y2, sb[k - 1].bn2))
+                else:
+                    G = ops.avgpool2_bwd_add(dX, B, ph, pw, skip_grad.get(k - 1))
             else:
                 G = dX
             st.__exit__(None, None, None)

@@ -448,3 +448,50 @@ def test_adamw_clip(device):
         opt.step()
     for a, b in zip(dps, ref):
         assert (a.detach().cpu() - b.detach()).abs().max() <= 1e-6
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("kind,B,h,w,C", [("pool", 2, 16, 18, 64), ("pool", 3, 9, 7, 1024),
+                                          ("resize", 2, 8, 10, 128), ("resize", 1, 33, 20, 512),
+                                          ("up2", 2, 16, 16, 64), ("up2", 1, 67, 120, 32)])
+def test_grad_producer_bn_reduce(ops, device, kind, B, h, w, C, dtype):
+    """The pooling / resize backward with the next BN's backward reduction fused
+    (bnred=): the same gradient, and bn_bwd on its partials == bn_bwd with its
+    own reduce pass (values, dgamma, dbeta)."""
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    g = torch.Generator().manual_seed(h * w + C)
+    if kind == "pool":
+        dy = torch.randn(B * (h // 2) * (w // 2), C, generator=g)
+        skip = torch.randn(B * h * w, C, generator=g)
+    elif kind == "resize":
+        dy = torch.randn(B * (2 * h) * (2 * w), C, generator=g)
+    else:  # up2 composite to a skip size that is not 2h x 2w
+        th, tw = 2 * h - 1, 2 * w + 3
+        dy = torch.randn(B * th * tw, C, generator=g)
+    y2 = (torch.randn(B * h * w, C, generator=g) * 1.5 + 0.2).to(device=device, dtype=tdt)
+    bn = torch.nn.BatchNorm2d(C).to(device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    st = ops.bn_train(y2, bn, C, 0.1, 1e-5)
+    dyd = dy.to(device=device, dtype=tdt)
+
+    def produce(bnred):
+        if kind == "pool":
+            return ops.avgpool2_bwd_add(dyd, B, h, w, skip.to(device=device, dtype=tdt), bnred=bnred)
+        if kind == "resize":
+            return ops.resize_bwd(dyd, B, h, w, 2 * h, 2 * w, bnred=bnred)
+        return ops.up2_resize_bwd(dyd, B, h, w, th, tw, bnred=bnred)
+
+    G0 = produce(None)
+    G1, part = produce((y2, st))
+    assert part is not None
+    assert torch.equal(G0, G1)
+    outs = []
+    for p in (None, part):
+        dg, db, dbias = (torch.empty(C, device=device) for _ in range(3))
+        d = ops.bn_bwd(G1, y2, st, h * w, None, C, dg, db, dbias, part=p)
+        outs.append((d.float().cpu(), dg.cpu(), db.cpu()))
+    assert rel(outs[1][0], outs[0][0]) <= (4e-3 if dtype == "bf16" else 2e-6)
+    assert rel(outs[1][1], outs[0][1]) <= 1e-5
+    assert rel(outs[1][2], outs[0][2]) <= 1e-5
