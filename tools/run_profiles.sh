@@ -35,3 +35,7 @@ python3 tools/conv6_trace.py bf16 "$(f trace_bf16 run_kernel_trace.csv)" "profil
 python3 tools/pmc_traffic.py bf16 "$OUT/fetch_csv_bf16" "$OUT/write_csv_bf16" \
     "profiles/$R/traffic_conv6_fwd_bf16.json"
 cp -r "profiles/$R" "$OUT/profiles_copy"
+# one train step's launches in order, with per-family totals
+python3 tools/step_timeline.py "$(f trace_f32 run_kernel_trace.csv)" > "profiles/$R/step_timeline_b8_f32.txt"
+python3 tools/step_timeline.py "$(f trace_bf16 run_kernel_trace.csv)" > "profiles/$R/step_timeline_b64_bf16.txt"
+cp profiles/$R/step_timeline_* "$OUT/profiles_copy/"
