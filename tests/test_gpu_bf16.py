@@ -42,7 +42,10 @@ def bf_close(got, ref, ulps=2.0):
                                            # N = 128: 512x128 LDS-DMA tiles, two 256-row
                                            # BN partials per block (last block ragged)
                                            (4, 256, 256, 64, 128, 3), (4, 257, 255, 128, 128, 3),
-                                           (4, 256, 256, 512, 128, 1)])
+                                           (4, 256, 256, 512, 128, 1),
+                                           # 32-channel 3x3 on the 128x32 LDS-DMA tiles (BK 32),
+                                           # ragged last block
+                                           (2, 256, 256, 32, 32, 3), (3, 131, 167, 32, 32, 3)])
 def test_conv_fwd_bf16(ops, device, B, H, W, ci, co, k):
     g = torch.Generator().manual_seed(B * 1000 + H * 10 + ci + co + k)
     x = r(torch.randn(B, ci, H, W, generator=g))
@@ -91,7 +94,9 @@ def test_conv1x1_prologue_bf16(ops, device, B, H, W, ci, co):
                                            (2, 12, 12, 64, 128, 1),
                                            (4, 128, 128, 512, 64, 3), (2, 150, 147, 768, 64, 3),
                                            # 512x128 tiles (dx has 128 channels)
-                                           (4, 256, 256, 128, 64, 3)])
+                                           (4, 256, 256, 128, 64, 3),
+                                           # dx of a 32 -> 32 3x3: 128x32 LDS-DMA tiles
+                                           (2, 256, 256, 32, 32, 3)])
 def test_conv_dgrad_bf16(ops, device, B, H, W, ci, co, k):
     g = torch.Generator().manual_seed(11)
     x = torch.randn(B, ci, H, W, generator=g, requires_grad=True)
