@@ -120,8 +120,11 @@ def test_conv_dgrad_bf16(ops, device, B, H, W, ci, co, k):
                                                (2, 12, 10, 128, 512, 3, False),
                                                (2, 16, 16, 256, 256, 3, False),
                                                (3, 45, 43, 128, 128, 3, False),
-                                               # multi-tap N tiles (Cin 64: 4 taps, 128: 3 taps)
+                                               # multi-tap N tiles (Cin 64: 4 taps, 128: 3 taps,
+                                               # 32: 4 taps on 32x128 tiles)
                                                (2, 37, 41, 64, 64, 3, False),
+                                               (3, 37, 41, 32, 32, 3, False),
+                                               (2, 256, 256, 32, 32, 3, False),
                                                # prologue-free 1x1 on the DMA tiles
                                                (2, 16, 16, 128, 256, 1, False),
                                                (2, 20, 20, 512, 1024, 1, False)])
