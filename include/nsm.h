@@ -371,6 +371,21 @@ int nsm_conv1x1_dgrad_bnbwd(const void* dy2, int lddy2, int B, int H, int W, int
                             void* stream);
 int nsm_conv1x1_bnbwd_chunks(int B, int H, int W, int cip, int dtype);
 /* rows per BN-partial chunk of nsm_conv_fwd_bf16 (its M tile) */
+/* Eval-mode DoubleConv half in one pass (Unetmodel.py:21-28 with BatchNorm on
+ * its running statistics): y = lrelu(round(conv(x) + bias) * act_scale +
+ * act_shift, slope) (+ res: the decoder's additive skip, :125-137), round =
+ * the storage dtype's (the value the unfused conv -> bn_act pair stores in
+ * between); act_scale / act_shift from nsm_bn_finalize_eval. dtype NSM_F32 |
+ * NSM_BF16 (x, wpk, y, res in it). */
+int nsm_conv_fwd_act(const void* x, int ldx, int B, int H, int W, int cin_p, const void* wpk,
+                     const float* bias, int cout_p, int ksize, void* y, int ldy,
+                     const float* act_scale, const float* act_shift, float slope, const void* res,
+                     int ldres, int dtype, void* stream);
+/* nsm_wino_output with the same eval BN + LeakyReLU (+ skip) on the way out */
+int nsm_wino_output_act(const float* Mb, int B, int H, int W, int cout_p, int tile,
+                        const float* bias, float* y, int ldy, const float* act_scale,
+                        const float* act_shift, float slope, const float* res, int ldres,
+                        void* stream);
 int nsm_conv_stat_rows_bf16(int B, int H, int W, int cout_p);
 size_t nsm_conv_wgrad_bf16_ws(int B, int H, int W, int cin_p, int cout_p, int ksize);
 int nsm_conv_wgrad_bf16(const void* dy, int lddy, const void* x, int ldx, int B, int H, int W,

@@ -312,6 +312,13 @@ struct EpiStoreP {
   const float* bias;
   float* stats;  // optional BN partials [gridDim.x][2][N]: {sum, M2 about block mean}
   long long bstride;  // batched GEMM (Winograd): output offset per blockIdx.z
+  // optional eval-mode BN + LeakyReLU (+ skip) on the stored value:
+  // y = lrelu((acc + bias) * act_scale + act_shift, slope) (+ res)
+  const float* act_scale;
+  const float* act_shift;
+  float slope;
+  const float* res;
+  int ldres;
 };
 struct EpiStore {
   using P = EpiStoreP;
@@ -334,12 +341,20 @@ struct EpiStore {
     for (int tn = 0; tn < TN; ++tn) {
       int n = cx.nb + tn * 32 + col;
       if (n >= N) continue;
+      const float asc = e.act_scale ? e.act_scale[n] : 0.f;
+      const float ash = e.act_scale ? e.act_shift[n] : 0.f;
 #pragma unroll
       for (int tm = 0; tm < TM; ++tm) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           int m = cx.mb + tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (m < M) yb[(size_t)m * e.ldy + n] = acc[tm][tn][i];
+          if (m >= M) continue;
+          float v = acc[tm][tn][i];
+          if (e.act_scale) {
+            v = lrelu(v * asc + ash, e.slope);
+            if (e.res) v += e.res[(size_t)m * e.ldres + n];
+          }
+          yb[(size_t)m * e.ldy + n] = v;
         }
       }
     }
@@ -1011,6 +1026,10 @@ template <> struct WinoVec<6> {
   using T = float;
   static constexpr int W = 1;
 };
+__device__ __forceinline__ float vlrelu(float v, float s) { return lrelu(v, s); }
+__device__ __forceinline__ f32x4 vlrelu(f32x4 v, float s) {
+  return f32x4{lrelu(v.x, s), lrelu(v.y, s), lrelu(v.z, s), lrelu(v.w, s)};
+}
 __device__ __forceinline__ float vrelu(float v) { return fmaxf(v, 0.f); }
 __device__ __forceinline__ f32x4 vrelu(f32x4 v) {
   return f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
@@ -1166,12 +1185,24 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
 // tile's {count, mean, M2} into its own and writes partial[slot][3][N] =
 // {sum, M2 about the slot mean, count}, slot = (global thread id) / N4 (the
 // counted partial layout nsm_bn_finalize_train takes with rows_per_chunk 0).
-template <int MT, bool STATS>
+// ACT (eval, no STATS): y = lrelu((o + bias) * act_scale + act_shift) (+ res),
+// the following BatchNorm (running statistics) + LeakyReLU (+ skip) applied
+// on the way out (Unetmodel.py:22-23,27-28,125-137)
+struct WinoAct {
+  const float* scale;
+  const float* shift;
+  float slope;
+  const float* res;
+  int ldres;
+};
+
+template <int MT, bool STATS, bool ACT = false>
 __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
                                                           int W, int TH, int TW, long long T,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ y, int ldy,
-                                                          float* __restrict__ partial) {
+                                                          float* __restrict__ partial,
+                                                          WinoAct act = WinoAct{}) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int N4 = N / CW;
@@ -1195,6 +1226,11 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
       for (int e = 0; e < A; ++e) m[a][e] = *(const VT*)(in + (a * A + e) * plane);
     wmat2<CAt<MT>>(m, o);
     const VT bv = bias ? *(const VT*)(bias + c) : VT{};
+    VT asc{}, ash{};
+    if (ACT) {
+      asc = *(const VT*)(act.scale + c);
+      ash = *(const VT*)(act.shift + c);
+    }
     VT ts{};
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
@@ -1205,7 +1241,13 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
       for (int e = 0; e < MT; ++e)
         if (MT * tx + e < W) {
           o[a][e] = o[a][e] + bv;
-          *(VT*)(row + (size_t)e * ldy) = o[a][e];
+          VT v = o[a][e];
+          if (ACT) {
+            v = vlrelu(v * asc + ash, act.slope);
+            if (act.res)
+              v = v + *(const VT*)(act.res + ((size_t)(b * H + yy) * W + MT * tx + e) * act.ldres + c);
+          }
+          *(VT*)(row + (size_t)e * ldy) = v;
           if (STATS) ts = ts + o[a][e];
         }
     }
@@ -1509,9 +1551,38 @@ extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, 
   ap.slope = slope;
   int K = ksize * ksize * cin_p;
   RowsKP bp{wpk, K, cout_p, 0};
-  EpiStoreP ep{y, ldy, bias, stats, 0};
+  EpiStoreP ep{y, ldy, bias, stats, 0, nullptr, nullptr, 0.f, nullptr, 0};
   hipStream_t s = as_stream(stream);
   if (pro_scale) return dispatch_conv_fwd<true>(ap, bp, ep, (int)Ml, cout_p, K, s);
+  return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s);
+}
+
+static int conv_fwd_act_f32(const float* x, int ldx, int B, int H, int W, int cin_p,
+                            const float* wpk, const float* bias, int cout_p, int ksize, float* y,
+                            int ldy, const float* act_scale, const float* act_shift, float slope,
+                            const float* res, int ldres, hipStream_t s) {
+  NSM_CHECK_ARG(x && wpk && y && act_scale && act_shift, "conv_fwd_act: null pointer");
+  NSM_CHECK_ARG(B > 0 && H > 0 && W > 0 && cin_p % 32 == 0 && cout_p % 32 == 0,
+                "conv_fwd_act: bad shape");
+  NSM_CHECK_ARG(ldx >= cin_p && ldx % 4 == 0 && ldy >= cout_p && (!res || ldres >= cout_p),
+                "conv_fwd_act: bad leading dims");
+  NSM_CHECK_ARG(ksize == 1 || ksize == 3, "conv_fwd_act: ksize %d", ksize);
+  NSM_CHECK_ARG(((uintptr_t)x % 16) == 0 && ((uintptr_t)wpk % 16) == 0, "conv_fwd_act: 16B alignment");
+  const long long Ml = (long long)B * H * W;
+  NSM_CHECK_ARG(Ml < (1ll << 30), "conv_fwd_act: too many pixels");
+  ConvActP ap{};
+  ap.x = x;
+  ap.ld = ldx;
+  ap.cin = cin_p;
+  ap.H = H;
+  ap.W = W;
+  ap.M = (int)Ml;
+  ap.ksize = ksize;
+  ap.fdW = make_fastdiv(W);
+  ap.fdH = make_fastdiv(H);
+  const int K = ksize * ksize * cin_p;
+  RowsKP bp{wpk, K, cout_p, 0};
+  EpiStoreP ep{y, ldy, bias, nullptr, 0, act_scale, act_shift, slope, res, ldres};
   return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s);
 }
 
@@ -1655,7 +1726,7 @@ extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W
   hipStream_t s = as_stream(stream);
   RowsKP ap{V, cin_p, (int)g.T, g.T * cin_p};
   RowsKP bp{U, cin_p, cout_p, (long long)cout_p * cin_p};
-  EpiStoreP ep{Mb, cout_p, nullptr, nullptr, g.T * cout_p};
+  EpiStoreP ep{Mb, cout_p, nullptr, nullptr, g.T * cout_p, nullptr, nullptr, 0.f, nullptr, 0};
   const int M = (int)g.T, N = cout_p, K = cin_p, nb = g.alpha2;
   long long mb128 = ceil_div(M, 128);
   if (N >= 128)
@@ -1699,8 +1770,11 @@ extern "C" int nsm_wino_stat_slots(int B, int H, int W, int cout_p, int tile) {
 template <int MT>
 static void launch_wino_output(dim3 grid, hipStream_t s, const float* Mb, int cout_p, int H, int W,
                                const WinoGeom& g, const float* bias, float* y, int ldy,
-                               float* partial) {
-  if (partial)
+                               float* partial, const WinoAct* act = nullptr) {
+  if (act)
+    hipLaunchKernelGGL((wino_output_kernel<MT, false, true>), grid, dim3(256), 0, s, Mb, cout_p, H,
+                       W, g.TH, g.TW, g.T, bias, y, ldy, nullptr, *act);
+  else if (partial)
     hipLaunchKernelGGL((wino_output_kernel<MT, true>), grid, dim3(256), 0, s, Mb, cout_p, H, W,
                        g.TH, g.TW, g.T, bias, y, ldy, partial);
   else
@@ -1727,6 +1801,25 @@ extern "C" int nsm_wino_output_stats(const float* Mb, int B, int H, int W, int c
   else if (tile == 4) launch_wino_output<4>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
   else launch_wino_output<6>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
   NSM_LAUNCH_CHECK("wino_output");
+  return 0;
+}
+
+extern "C" int nsm_wino_output_act(const float* Mb, int B, int H, int W, int cout_p, int tile,
+                                   const float* bias, float* y, int ldy, const float* act_scale,
+                                   const float* act_shift, float slope, const float* res,
+                                   int ldres, void* stream) {
+  NSM_CHECK_ARG(Mb && y && act_scale && act_shift && cout_p % 32 == 0 && ldy % 4 == 0 &&
+                    (!res || (ldres % 4 == 0 && ldres >= cout_p)),
+                "wino_output_act: bad args");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_act: bad tile or shape");
+  const WinoAct act{act_scale, act_shift, slope, res, ldres};
+  dim3 grid(grid_1d(g.T * (cout_p / (tile == 6 ? 1 : 4))));
+  hipStream_t s = as_stream(stream);
+  if (tile == 2) launch_wino_output<2>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, nullptr, &act);
+  else if (tile == 4) launch_wino_output<4>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, nullptr, &act);
+  else launch_wino_output<6>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, nullptr, &act);
+  NSM_LAUNCH_CHECK("wino_output_act");
   return 0;
 }
 

@@ -50,6 +50,8 @@ _SIGS = {
     "nsm_bn_bwd_finalize": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
     "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
     "nsm_sum_rows": (I, [P, I, I, I, P, P]),
+    "nsm_conv_fwd_act": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, F, P, I, I, P]),
+    "nsm_wino_output_act": (I, [P, I, I, I, I, I, P, P, I, P, P, F, P, I, P]),
     "nsm_bnred_chunks": (I, [I, I, I, I, I]),
     "nsm_avgpool2_bwd_add_bnred": (I, [P, I, I, I, I, P, P, I, P, P, P, P, P, F, P, P]),
     "nsm_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P]),

@@ -136,6 +136,23 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
     return y, part
 
 
+def conv_fwd_act(x, B, H, W, wpk, bias, cout_p, ksize, st, res=None, slope=0.2, tag=None):
+    """Eval: lrelu(BN(conv(x) + bias)) (+ res) in one pass, BN from the
+    running statistics (st = bn_eval's BNState): the conv output itself is
+    never stored (nsm_conv_fwd_act)."""
+    M = x.shape[0]
+    y = like(M, cout_p, x)
+    if wpk.dtype != x.dtype or (res is not None and res.dtype != x.dtype):
+        raise TypeError("conv_fwd_act: activations, weights and skip must share a dtype")
+    ev = _probe(tag)
+    call("nsm_conv_fwd_act", ptr(x), x.stride(0), B, H, W, x.shape[1], ptr(wpk), ptr(bias),
+         cout_p, ksize, ptr(y), y.stride(0), ptr(st.scale), ptr(st.shift), slope, ptr(res),
+         res.stride(0) if res is not None else 0, dt(x), stream())
+    if ev is not None:
+        ev.record()
+    return y
+
+
 def wino_tiles(B, H, W, tile):
     return B * ((H + tile - 1) // tile) * ((W + tile - 1) // tile)
 
@@ -150,7 +167,7 @@ def wino_weight(w, n_p, k_p, flip, tile=4):
 
 
 def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, relu=False,
-                 stats=False, nslot=None, src_hw=None):
+                 stats=False, nslot=None, src_hw=None, act=None):
     """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(tile x tile, 3x3).
     keep_v=True also returns the transformed input V [(tile+2)^2][T][cin_p],
     reused by the Winograd weight gradient. stats=True returns (y, V|None,
@@ -158,7 +175,9 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     transform (counted layout, rpc 0), None where nsm_wino_stat_slots says the
     separate pass is faster (nslot: override the slot count, tests).
     src_hw=(hi, wi): x is [B*hi*wi, cin_p], convolved after a bilinear
-    align_corners resize to H x W that the input transform samples on the fly."""
+    align_corners resize to H x W that the input transform samples on the fly.
+    act=(BNState, res|None): eval BN + LeakyReLU (+ skip) applied by the output
+    transform (nsm_wino_output_act)."""
     from ._lib import lib
     cin_p = x.shape[1]
     M = B * H * W
@@ -177,6 +196,15 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     if ev is not None:
         ev.record()
     part = None
+    if act is not None:
+        assert not stats
+        ast, res = act
+        call("nsm_wino_output_act", ptr(Mb), B, H, W, cout_p, tile, ptr(bias), ptr(y),
+             y.stride(0), ptr(ast.scale), ptr(ast.shift), 0.2, ptr(res),
+             res.stride(0) if res is not None else 0, st)
+        if ev_all is not None:
+            ev_all.record()
+        return (y, V) if keep_v else y
     if not stats:
         nslot = 0
     elif nslot is None:

@@ -37,6 +37,9 @@ SLOPE = 0.2
 # forces one tile everywhere.
 WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "64"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
+# NSM_EVAL_FUSED=0: eval forward with separate BN-apply passes instead of the
+# BN + LeakyReLU (+ skip) in the conv epilogues (nsm_conv_fwd_act)
+EVAL_FUSED = os.environ.get("NSM_EVAL_FUSED", "1") != "0"
 # NSM_UP_WINO=0: materialise the decoder's x2-upsampled input of a Winograd
 # conv (nsm_resize_fwd) instead of sampling it inside the input transform
 UP_IN_WINO = os.environ.get("NSM_UP_WINO", "1") != "0"
@@ -397,7 +400,7 @@ def _masks_for(mod, B, device, training):
 
 class _BlockSaved:
     __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop", "V", "A1",
-                 "pw")
+                 "pw", "Z")
 
 
 def fuses_resize(blk, dtype):
@@ -407,11 +410,41 @@ def fuses_resize(blk, dtype):
             and ops.pad32(blk.conv[0].in_channels) >= WINOGRAD_MIN_CHANNELS)
 
 
-def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None):
+def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res):
+    """Eval: both convs with BN (running statistics) + LeakyReLU (+ the skip
+    add) in their epilogues — nothing but A1 and the block output is stored."""
+    c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
+    ci, co = c0.in_channels, c4.out_channels
+    cip, cop = ops.pad32(ci), ops.pad32(co)
+    dtype = xin.dtype
+    bn1 = ops.bn_eval(bn1m, cip, ci, bn1m.eps, xin.device, gamma=pw.vec("g1"), beta=pw.vec("be1"))
+    b1 = pw.vec("b1")
+    if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
+        tile = wino_tile(cip, H, W)
+        A1 = ops.conv3x3_wino(xin, B, H, W, pw.U1(tile, False), b1, cip, tile=tile,
+                              tag=name + ".conv.0.fwd", src_hw=src_hw, act=(bn1, None))
+    else:
+        assert src_hw is None
+        A1 = ops.conv_fwd_act(xin, B, H, W, pw.w1(ops.PACK_FWD), b1, cip, 3, bn1, slope=SLOPE,
+                              tag=name + ".conv.0.fwd")
+    bn2 = ops.bn_eval(bn2m, cop, co, bn2m.eps, xin.device, gamma=pw.vec("g2"), beta=pw.vec("be2"))
+    Z = ops.conv_fwd_act(A1, B, H, W, pw.w2(ops.PACK_FWD), pw.vec("b2"), cop, 1, bn2, res=res,
+                         slope=SLOPE, tag=name + ".conv.4.fwd")
+    s = _BlockSaved()
+    s.X = s.Y1 = s.Y2 = s.mask = s.V = s.A1 = None
+    s.bn1, s.bn2, s.pw, s.Z = bn1, bn2, pw, Z
+    s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
+    return s
+
+
+def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse_out=False,
+               res=None):
     """pw: the block's weight layouts (prep.StepWeights.block, all written by the
     step's single preparation launch), or None to build them here per call.
     src=(x_low, hi, wi): X is the bilinear resize of x_low to H x W, sampled
-    inside the Winograd input transform (X is None then; fuses_resize)."""
+    inside the Winograd input transform (X is None then; fuses_resize).
+    fuse_out (eval, EVAL_FUSED): the block output lrelu(bn2(Y2)) (+ res) is
+    produced by the convs' epilogues, returned as s.Z (Y1/Y2 not stored)."""
     c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
     ci, co = c0.in_channels, c4.out_channels
     cip, cop = ops.pad32(ci), ops.pad32(co)
@@ -422,6 +455,8 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None):
     dtype = xin.dtype
     if pw is None:
         pw = LazyBlockWeights(blk, dtype)
+    if fuse_out and not training and EVAL_FUSED:
+        return _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res)
     b1 = pw.vec("b1")
     V = None
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
@@ -470,6 +505,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None):
     s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
     s.V = V if training else None  # Winograd-domain input, reused by the weight gradient
     s.A1 = A1 if training else None  # activated 1x1 operand, reused by its weight gradient
+    s.Z = None
     return s
 
 
@@ -574,9 +610,9 @@ class _UnetFn(torch.autograd.Function):
         for k in ENCODER:
             with ops.stage(f"conv{k}.fwd"):
                 s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}",
-                               pw=sw.block(k) if sw else None)
+                               pw=sw.block(k) if sw else None, fuse_out=True)
                 saved[k], shapes[k] = s, (h, w)
-                c[k] = ops.bn_act(s.Y2, s.bn2, SLOPE)
+                c[k] = s.Z if s.Z is not None else ops.bn_act(s.Y2, s.bn2, SLOPE)
                 if k < 5:
                     inp = ops.avgpool2(c[k], B, h, w)
                     h, w = h // 2, w // 2
@@ -595,11 +631,11 @@ class _UnetFn(torch.autograd.Function):
                 else:                      # match is the identity (bitwise, as in ATen)
                     up = ops.resize(cur, B, h, w, h2, w2)
                 ups[k] = (h, w, h2, w2, th, tw)
-                s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}",
-                               pw=sw.block(k) if sw else None, src=src)
-                saved[k] = s
                 res = c[SKIP_OF[k]] if k in SKIP_OF else None
-                cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
+                s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}",
+                               pw=sw.block(k) if sw else None, src=src, fuse_out=True, res=res)
+                saved[k] = s
+                cur = s.Z if s.Z is not None else ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
                 h, w = th, tw
         z9 = cur
         with ops.stage("head.fwd"):
