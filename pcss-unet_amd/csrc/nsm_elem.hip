@@ -7,6 +7,8 @@
 // 32 in practice), so every lane moves float4 (16 B) and a wave moves 1 KiB
 // per instruction. Cross-block reductions are deterministic: each block writes
 // a partial row, a tiny finalize kernel merges rows in a fixed order (double).
+#include <algorithm>
+
 #include "nsm_common.h"
 
 namespace nsm {
@@ -763,8 +765,11 @@ __global__ void __launch_bounds__(256) up2_resize_fwd_rows_kernel(
 #pragma unroll
   for (int a = 0; a < 3; ++a) rows[a] = x + ((size_t)b * h + min(yb + a, h - 1)) * w * C;
   T* orow = y + ((size_t)b * th + oy) * tw * C;
+  // gridDim.y segments per row (small batches: enough blocks for the chip)
   const uint32_t items = (uint32_t)tw * (uint32_t)C8;
-  for (uint32_t it = threadIdx.x; it < items; it += blockDim.x) {
+  const uint32_t seg = (items + gridDim.y - 1) / gridDim.y;
+  const uint32_t i0 = blockIdx.y * seg, i1 = min(items, i0 + seg);
+  for (uint32_t it = i0 + threadIdx.x; it < i1; it += blockDim.x) {
     const int ox = (int)fdiv(it, fdC8);
     const int c = (int)(it - (uint32_t)ox * (uint32_t)C8) * 8;
     const int x0 = xb[ox];
@@ -1702,13 +1707,16 @@ extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, voi
   if (tw <= U2_MAXW && (long long)B * th < (1ll << 31) && th * 2 >= 2 * h - 1 && tw * 2 >= 2 * w - 1) {
     // second step downsizes (or keeps) the x2 grid: the 3-tap collapse holds
     const size_t lds = (size_t)tw * 4 * 4;
+    // row segments: >= ~2048 blocks when B * th is small (1080p inference: 135 rows)
+    const long long rows = (long long)B * th, per_row = (long long)tw * (C / 8);
+    long long segs = (2048 + rows - 1) / rows;
+    segs = std::max(1ll, std::min({segs, 16ll, (per_row + 1023) / 1024}));
+    const dim3 gr((unsigned)rows, (unsigned)segs);
 #define A_(T) NSM_CT(T, x), h, w, C / 8, f8, NSM_T(T, y), th, tw, a, b, c, d
     if (dtype == NSM_BF16)
-      hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<bf16_t>, dim3((unsigned)(B * th)), dim3(256),
-                         lds, s, A_(bf16_t));
+      hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<bf16_t>, gr, dim3(256), lds, s, A_(bf16_t));
     else
-      hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<float>, dim3((unsigned)(B * th)), dim3(256),
-                         lds, s, A_(float));
+      hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<float>, gr, dim3(256), lds, s, A_(float));
 #undef A_
   } else {
 #define A_(T) NSM_CT(T, x), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, y), th, tw, a, b, c, d
