@@ -319,6 +319,7 @@ struct EpiStoreP {
   float slope;
   const float* res;
   int ldres;
+  int vec;  // 16-B row stores staged through LDS (NSM_F32_EPI_VEC=0: 4-byte stores)
 };
 struct EpiStore {
   using P = EpiStoreP;
@@ -336,6 +337,42 @@ struct EpiStore {
       for (int tm = 0; tm < TM; ++tm)
 #pragma unroll
         for (int i = 0; i < 16; ++i) acc[tm][tn][i] += bv[tn];
+    }
+    if (e.vec && (e.ldy & 3) == 0 && (((uintptr_t)yb) & 15) == 0 &&
+        (!e.res || ((e.ldres & 3) == 0 && (((uintptr_t)e.res) & 15) == 0))) {
+      // each wave stages its tile as rows in LDS (stride WC + 4 floats: the two
+      // row halves of a store land on different banks) and writes 16-B chunks
+      constexpr int WR = TM * 32, WC = TN * 32, WCP = WC + 4, CPR = WC / 4;
+      float* reg = cx.lds + (cx.wm * WN + cx.wn) * (WR * WCP);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+        for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            reg[(tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * WCP + tn * 32 + col] = acc[tm][tn][i];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+      for (int it = 0; it < WR * CPR / 64; ++it) {
+        const int q = it * 64 + cx.lane, r = q / CPR, cc = q - r * CPR;
+        const int m = cx.mb + r, n = cx.nb + cc * 4;
+        if (m >= M || n >= N) continue;
+        f32x4 v = *(const f32x4*)&reg[r * WCP + cc * 4];
+        if (e.act_scale) {
+          const f32x4 a = *(const f32x4*)(e.act_scale + n), b = *(const f32x4*)(e.act_shift + n);
+          v = v * a + b;
+          v = f32x4{lrelu(v.x, e.slope), lrelu(v.y, e.slope), lrelu(v.z, e.slope),
+                    lrelu(v.w, e.slope)};
+          if (e.res) v += *(const f32x4*)(e.res + (size_t)m * e.ldres + n);
+        }
+        *(f32x4*)(yb + (size_t)m * e.ldy + n) = v;
+      }
+      if (!e.stats) return;
+      __syncthreads();  // stats_only reuses the LDS
+      stats_only<TM, TN, WM, WN>(e, acc, cx, M, N);
+      return;
     }
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {
@@ -1467,6 +1504,16 @@ static int grid_1d(long long work) {
 
 using namespace nsm;
 
+// NSM_F32_EPI_VEC=0: the fp32 store epilogue writes 4-byte elements directly
+static int f32_epi_vec() {
+  static int v = [] {
+    const char* e = getenv("NSM_F32_EPI_VEC");
+    return (!e || atoi(e) != 0) ? 1 : 0;
+  }();
+  return v;
+}
+
+
 extern "C" int nsm_pack_conv_weight(const float* w, int cout, int cin, int ksize, int cout_p,
                                     int cin_p, int mode, float* out, void* stream) {
   NSM_CHECK_ARG(w && out && cout > 0 && cin > 0 && cout_p >= cout && cin_p >= cin,
@@ -1551,7 +1598,7 @@ extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, 
   ap.slope = slope;
   int K = ksize * ksize * cin_p;
   RowsKP bp{wpk, K, cout_p, 0};
-  EpiStoreP ep{y, ldy, bias, stats, 0, nullptr, nullptr, 0.f, nullptr, 0};
+  EpiStoreP ep{y, ldy, bias, stats, 0, nullptr, nullptr, 0.f, nullptr, 0, f32_epi_vec()};
   hipStream_t s = as_stream(stream);
   if (pro_scale) return dispatch_conv_fwd<true>(ap, bp, ep, (int)Ml, cout_p, K, s);
   return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s);
@@ -1582,7 +1629,7 @@ static int conv_fwd_act_f32(const float* x, int ldx, int B, int H, int W, int ci
   ap.fdH = make_fastdiv(H);
   const int K = ksize * ksize * cin_p;
   RowsKP bp{wpk, K, cout_p, 0};
-  EpiStoreP ep{y, ldy, bias, nullptr, 0, act_scale, act_shift, slope, res, ldres};
+  EpiStoreP ep{y, ldy, bias, nullptr, 0, act_scale, act_shift, slope, res, ldres, f32_epi_vec()};
   return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s);
 }
 
@@ -1726,7 +1773,8 @@ extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W
   hipStream_t s = as_stream(stream);
   RowsKP ap{V, cin_p, (int)g.T, g.T * cin_p};
   RowsKP bp{U, cin_p, cout_p, (long long)cout_p * cin_p};
-  EpiStoreP ep{Mb, cout_p, nullptr, nullptr, g.T * cout_p, nullptr, nullptr, 0.f, nullptr, 0};
+  EpiStoreP ep{Mb, cout_p, nullptr, nullptr, g.T * cout_p, nullptr, nullptr, 0.f, nullptr, 0,
+               f32_epi_vec()};
   const int M = (int)g.T, N = cout_p, K = cin_p, nb = g.alpha2;
   long long mb128 = ceil_div(M, 128);
   if (N >= 128)
