@@ -603,6 +603,7 @@ struct EpiBnBwd {
 
 struct EpiSlabP {
   float* ws;
+  int vec;  // EpiSlabV: 16-B row stores staged through LDS
 };
 struct EpiSlab {
   using P = EpiSlabP;
@@ -624,6 +625,42 @@ struct EpiSlab {
           if (m < M) out[(size_t)m * N + n] = acc[tm][tn][i];
         }
       }
+    }
+  }
+};
+
+// EpiSlab with the LDS-staged 16-B row stores of EpiStore (fp32 weight-
+// gradient kernels only: their two K-major stages, 64 x (BM + BN + 8) floats,
+// hold the BM x BN tile unpadded — the +4 row pad of EpiStore would not fit at
+// 128x128; the bf16 kernels' LDS holds neither, they keep EpiSlab)
+struct EpiSlabV {
+  using P = EpiSlabP;
+  template <int TM, int TN, int WM, int WN>
+  __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
+                               int split) {
+    float* out = e.ws + (size_t)cx.zslab * M * N;
+    if (!e.vec || (N & 3) || (((uintptr_t)e.ws) & 15)) {
+      EpiSlab::apply<TM, TN, WM, WN>(e, acc, cx, M, N, split);
+      return;
+    }
+    const int col = cx.lane & 31, h = cx.lane >> 5;
+    constexpr int WR = TM * 32, WC = TN * 32, CPR = WC / 4;
+    float* reg = cx.lds + (cx.wm * WN + cx.wn) * (WR * WC);
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn)
+#pragma unroll
+      for (int tm = 0; tm < TM; ++tm)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)
+          reg[(tm * 32 + (i & 3) + 8 * (i >> 2) + 4 * h) * WC + tn * 32 + col] = acc[tm][tn][i];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int it = 0; it < WR * CPR / 64; ++it) {
+      const int q = it * 64 + cx.lane, r = q / CPR, cc = q - r * CPR;
+      const int m = cx.mb + r, n = cx.nb + cc * 4;
+      if (m < M && n < N) *(f32x4*)(out + (size_t)m * N + n) = *(const f32x4*)&reg[r * WC + cc * 4];
     }
   }
 };
@@ -794,7 +831,7 @@ static int launch_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& 
   using AL = PixRowsLoader<BM, NT, false, false>;
   using BL = PixRowsLoader<BN, NT, SHIFT, PRO>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), splits);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlab, PixRowsP, PixRowsP>), grid,
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlabV, PixRowsP, PixRowsP>), grid,
                      dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, splits);
   NSM_LAUNCH_CHECK("conv_wgrad");
   return 0;
@@ -1679,7 +1716,7 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
   bp.mask_ld = pro_mask ? cin_p : 0;
   bp.mask_on = pro_mask != nullptr;
   bp.slope = slope;
-  EpiSlabP ep{ws};
+  EpiSlabP ep{ws, f32_epi_vec()};
   hipStream_t s = as_stream(stream);
   int rc;
   if (ksize == 3)
@@ -1933,7 +1970,7 @@ static int launch_wino_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSl
   using AL = PixRowsLoader<BM, NT, false, false>;
   using BL = PixRowsLoader<BN, NT, false, false>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), nb * splits);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlab, PixRowsP, PixRowsP>), grid,
+  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlabV, PixRowsP, PixRowsP>), grid,
                      dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, splits);
   NSM_LAUNCH_CHECK("wino_wgrad_gemm");
   return 0;
@@ -1982,7 +2019,7 @@ extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V,
   bp.ld = cin_p;
   bp.ncols = cin_p;
   bp.bstride = g.T * cin_p;
-  EpiSlabP ep{slab};
+  EpiSlabP ep{slab, f32_epi_vec()};
   const int M = cout_p, N = cin_p, K = (int)g.T;
   int rc;
 #define NSM_WW(bm, bn, wm, wn) \
