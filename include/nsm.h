@@ -141,6 +141,15 @@ size_t nsm_wino_wgrad_ws(int B, int H, int W, int cin_p, int cout_p, int tile);
 int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int H, int W,
                            int cin_p, int cout_p, int cin, int cout, int tile, float* dw,
                            float* ws, size_t ws_floats, void* stream);
+/* Both Winograd transforms of a 3x3 conv's output gradient dy [B*H*W][c_p]
+ * from one read: V = the input transform for its input-gradient conv (as
+ * nsm_wino_input), dM = the transform nsm_conv3x3_wgrad_wino applies (each
+ * [(tile+2)^2][T][c_p]); then nsm_conv3x3_wgrad_wino_dm takes dM instead of dy. */
+int nsm_wino_dual_input(const float* dy, int lddy, int B, int H, int W, int c_p, int tile,
+                        float* V, float* dM, void* stream);
+int nsm_conv3x3_wgrad_wino_dm(const float* dM, const float* V, int B, int H, int W, int cin_p,
+                              int cout_p, int cin, int cout, int tile, float* dw, float* ws,
+                              size_t ws_floats, void* stream);
 
 /* nsm_conv_wgrad: dw[co][ci][kh][kw] (real cout x cin, reference layout) =
  *   sum_p dy[p][co] * pro(x[p+off(tap)][ci]); deterministic split-K over

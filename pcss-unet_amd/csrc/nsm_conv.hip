@@ -1390,6 +1390,64 @@ __global__ void __launch_bounds__(256) wino_dout_kernel(const float* __restrict_
   }
 }
 
+// Both Winograd transforms of one gradient dY (the input gradient of a 3x3
+// conv whose dgrad AND weight gradient run in the Winograd domain) from ONE
+// read of it: the (m+2)^2 patch of tile t gives V = B^T d B (the dgrad's input
+// transform, as wino_input) and its m x m interior gives dM = A^T-side
+// transform (as wino_dout). Saves a full read of dY per layer.
+template <int MT>
+__global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict__ dy, int ld, int H,
+                                                        int W, int C, int TH, int TW, long long T,
+                                                        float* __restrict__ V,
+                                                        float* __restrict__ dM) {
+  constexpr int A = MT + 2, CW = WinoVec<MT>::W;
+  using VT = typename WinoVec<MT>::T;
+  const int C4 = C / CW;
+  const long long total = T * C4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * CW;
+    const long long t = i / C4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    VT d[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const int yy = MT * ty - 1 + a;
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const int xx = MT * tx - 1 + e;
+        d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                      ? *(const VT*)(dy + ((size_t)(b * H + yy) * W + xx) * ld + c)
+                      : VT{};
+      }
+    }
+    const size_t plane = (size_t)T * C;
+    {
+      VT v[A][A];
+      wmat2<CBt<MT>>(d, v);
+      float* out = V + (size_t)t * C + c;
+#pragma unroll
+      for (int a = 0; a < A; ++a)
+#pragma unroll
+        for (int e = 0; e < A; ++e) *(VT*)(out + (a * A + e) * plane) = v[a][e];
+    }
+    VT g[MT][MT], sm[A][A];
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int e = 0; e < MT; ++e) g[a][e] = d[a + 1][e + 1];
+    wmat2<CA<MT>>(g, sm);
+    float* out = dM + (size_t)t * C + c;
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) *(VT*)(out + (a * A + e) * plane) = sm[a][e];
+  }
+}
+
 // dst[b][i] = sum_s src[b][s][i] (float4 lanes, fixed order): the split-K
 // partials of a batched GEMM, one batch entry per grid.y
 __global__ void __launch_bounds__(256) batched_splitsum_kernel(const float* __restrict__ src,
@@ -1976,10 +2034,51 @@ static int launch_wino_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSl
   return 0;
 }
 
+extern "C" int nsm_wino_dual_input(const float* dy, int lddy, int B, int H, int W, int c_p,
+                                   int tile, float* V, float* dM, void* stream) {
+  NSM_CHECK_ARG(dy && V && dM && c_p % 32 == 0 && lddy % 4 == 0 && lddy >= c_p,
+                "wino_dual_input: bad args");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_dual_input: bad tile or shape");
+  dim3 grid(grid_1d(g.T * c_p / (tile == 6 ? 1 : 4)));
+  hipStream_t s = as_stream(stream);
+  if (tile == 2)
+    hipLaunchKernelGGL(wino_dual_kernel<2>, grid, dim3(256), 0, s, dy, lddy, H, W, c_p, g.TH, g.TW,
+                       g.T, V, dM);
+  else if (tile == 4)
+    hipLaunchKernelGGL(wino_dual_kernel<4>, grid, dim3(256), 0, s, dy, lddy, H, W, c_p, g.TH, g.TW,
+                       g.T, V, dM);
+  else
+    hipLaunchKernelGGL(wino_dual_kernel<6>, grid, dim3(256), 0, s, dy, lddy, H, W, c_p, g.TH, g.TW,
+                       g.T, V, dM);
+  NSM_LAUNCH_CHECK("wino_dual_input");
+  return 0;
+}
+
+static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float* V, int B, int H,
+                      int W, int cin_p, int cout_p, int cin, int cout, int tile, float* dw,
+                      float* ws, size_t ws_floats, void* stream);
+
 extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int H,
                                       int W, int cin_p, int cout_p, int cin, int cout, int tile,
                                       float* dw, float* ws, size_t ws_floats, void* stream) {
-  NSM_CHECK_ARG(dy && V && dw && ws, "conv3x3_wgrad_wino: null pointer");
+  return wgrad_wino(dy, lddy, nullptr, V, B, H, W, cin_p, cout_p, cin, cout, tile, dw, ws,
+                    ws_floats, stream);
+}
+
+// the weight gradient from a dM nsm_wino_dual_input already wrote (no dY read)
+extern "C" int nsm_conv3x3_wgrad_wino_dm(const float* dM, const float* V, int B, int H, int W,
+                                         int cin_p, int cout_p, int cin, int cout, int tile,
+                                         float* dw, float* ws, size_t ws_floats, void* stream) {
+  NSM_CHECK_ARG(dM, "conv3x3_wgrad_wino_dm: null dM");
+  return wgrad_wino(nullptr, cout_p, dM, V, B, H, W, cin_p, cout_p, cin, cout, tile, dw, ws,
+                    ws_floats, stream);
+}
+
+static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float* V, int B, int H,
+                      int W, int cin_p, int cout_p, int cin, int cout, int tile, float* dw,
+                      float* ws, size_t ws_floats, void* stream) {
+  NSM_CHECK_ARG((dy || dM_in) && V && dw && ws, "conv3x3_wgrad_wino: null pointer");
   NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0 && lddy % 4 == 0 && cin <= cin_p &&
                     cout <= cout_p, "conv3x3_wgrad_wino: bad channels");
   WinoGeom g;
@@ -1992,7 +2091,9 @@ extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V,
   float* slab = ws;
   float* dM = ws + pl.slab_floats;
   dim3 g1(grid_1d(g.T * cout_p / (tile == 6 ? 1 : 4)));
-  if (tile == 2)
+  if (dM_in)
+    dM = (float*)dM_in;
+  else if (tile == 2)
     hipLaunchKernelGGL(wino_dout_kernel<2>, g1, dim3(256), 0, s, dy, lddy, H, W, cout_p, g.TH, g.TW,
                        g.T, dM);
   else if (tile == 4)

@@ -167,7 +167,7 @@ def wino_weight(w, n_p, k_p, flip, tile=4):
 
 
 def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, relu=False,
-                 stats=False, nslot=None, src_hw=None, act=None):
+                 stats=False, nslot=None, src_hw=None, act=None, v_in=None):
     """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(tile x tile, 3x3).
     keep_v=True also returns the transformed input V [(tile+2)^2][T][cin_p],
     reused by the Winograd weight gradient. stats=True returns (y, V|None,
@@ -177,20 +177,24 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     src_hw=(hi, wi): x is [B*hi*wi, cin_p], convolved after a bilinear
     align_corners resize to H x W that the input transform samples on the fly.
     act=(BNState, res|None): eval BN + LeakyReLU (+ skip) applied by the output
-    transform (nsm_wino_output_act)."""
+    transform (nsm_wino_output_act). v_in: x's input transform already made
+    (wino_dual_input); x is then not read."""
     from ._lib import lib
     cin_p = x.shape[1]
     M = B * H * W
     hi, wi = src_hw if src_hw is not None else (H, W)
     assert x.shape[0] == B * hi * wi, (x.shape, B, hi, wi)
     nb, T = (tile + 2) ** 2, wino_tiles(B, H, W, tile)
-    V = empty(nb * T * cin_p, device=x.device)    # kept alive for the wgrad
     Mb = empty(nb * T * cout_p, device=x.device)
     y = empty(M, cout_p, device=x.device)
     st = stream()
     ev_all = _probe(tag)  # the whole convolution: input transform + GEMM + output transform
-    call("nsm_wino_input_resize", ptr(x), x.stride(0), B, hi, wi, H, W, cin_p, tile, int(relu),
-         ptr(V), st)
+    if v_in is not None:
+        V = v_in
+    else:
+        V = empty(nb * T * cin_p, device=x.device)    # kept alive for the wgrad
+        call("nsm_wino_input_resize", ptr(x), x.stride(0), B, hi, wi, H, W, cin_p, tile,
+             int(relu), ptr(V), st)
     ev = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
     call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb), st)
     if ev is not None:
@@ -223,15 +227,33 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     return (y, V) if keep_v else y
 
 
-def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None):
-    """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino, same tile)."""
+def wino_dual_input(dy, B, H, W, tile=4):
+    """(Vd, dM) of the output gradient dy [B*H*W, C_p] from one read of it:
+    Vd feeds conv3x3_wino(v_in=Vd) (the input gradient), dM feeds
+    conv3x3_wgrad_wino(dM=dM) (the weight gradient)."""
+    c_p = dy.shape[1]
+    n = (tile + 2) ** 2 * wino_tiles(B, H, W, tile) * c_p
+    Vd = empty(n, device=dy.device)
+    dM = empty(n, device=dy.device)
+    call("nsm_wino_dual_input", ptr(dy), dy.stride(0), B, H, W, c_p, tile, ptr(Vd), ptr(dM),
+         stream())
+    return Vd, dM
+
+
+def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, dM=None):
+    """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino, same tile).
+    dM: dy's transform from wino_dual_input (dy is then not read)."""
     from ._lib import lib
     cout_p = dy.shape[1]
     n = int(lib.nsm_wino_wgrad_ws(B, H, W, cin_p, cout_p, tile))
     ws = empty(n, device=dy.device)
     ev = _probe(tag)
-    call("nsm_conv3x3_wgrad_wino", ptr(dy), dy.stride(0), ptr(V), B, H, W, cin_p, cout_p, cin, cout,
-         tile, ptr(dw), ptr(ws), n, stream())
+    if dM is None:
+        call("nsm_conv3x3_wgrad_wino", ptr(dy), dy.stride(0), ptr(V), B, H, W, cin_p, cout_p, cin,
+             cout, tile, ptr(dw), ptr(ws), n, stream())
+    else:
+        call("nsm_conv3x3_wgrad_wino_dm", ptr(dM), ptr(V), B, H, W, cin_p, cout_p, cin, cout,
+             tile, ptr(dw), ptr(ws), n, stream())
     if ev is not None:
         ev.record()
 

@@ -37,6 +37,9 @@ SLOPE = 0.2
 # forces one tile everywhere.
 WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "64"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
+# NSM_DUAL_WINO=0: the Winograd dgrad and wgrad transform the output gradient
+# in two separate reads of it instead of one (nsm_wino_dual_input)
+DUAL_TRANSFORM = os.environ.get("NSM_DUAL_WINO", "1") != "0"
 # NSM_EVAL_FUSED=0: eval forward with separate BN-apply passes instead of the
 # BN + LeakyReLU (+ skip) in the conv epilogues (nsm_conv_fwd_act)
 EVAL_FUSED = os.environ.get("NSM_EVAL_FUSED", "1") != "0"
@@ -536,10 +539,15 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
         dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias],
                          g[c0.bias])
+    Vd = None
     if s.V is not None:
-        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight],
-                               tile=wino_tile(s.cip, H, W),
-                               tag=name + ".conv.0.wgrad")
+        tile = wino_tile(s.cip, H, W)
+        dM = None
+        if need_dx and DUAL_TRANSFORM:
+            # dY1's two Winograd transforms (dgrad input, wgrad) from one read
+            Vd, dM = ops.wino_dual_input(dY1, B, H, W, tile=tile)
+        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=tile,
+                               tag=name + ".conv.0.wgrad", dM=dM)
         s.V = None
     else:
         ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
@@ -549,7 +557,7 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         tile = wino_tile(s.cip, H, W)
         U1d = s.pw.U1(tile, True)
         return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=tile,
-                                tag=name + ".conv.0.dgrad")
+                                tag=name + ".conv.0.dgrad", v_in=Vd)
     w1d = s.pw.w1(ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
 

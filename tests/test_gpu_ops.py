@@ -495,3 +495,26 @@ def test_grad_producer_bn_reduce(ops, device, kind, B, h, w, C, dtype):
     assert rel(outs[1][0], outs[0][0]) <= (4e-3 if dtype == "bf16" else 2e-6)
     assert rel(outs[1][1], outs[0][1]) <= 1e-5
     assert rel(outs[1][2], outs[0][2]) <= 1e-5
+
+
+@pytest.mark.parametrize("tile", [2, 4, 6])
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 9, 11, 32, 64), (1, 16, 16, 128, 128), (2, 37, 29, 64, 32)])
+def test_wino_dual_input(ops, device, B, H, W, ci, co, tile):
+    """nsm_wino_dual_input: both transforms of dy from one read == the separate
+    input transform (dgrad) and the weight gradient's own dy transform."""
+    g = torch.Generator().manual_seed(H * W + tile)
+    x = nhwc(torch.randn(B, ci, H, W, generator=g)).to(device)
+    dy = nhwc(torch.randn(B, co, H, W, generator=g)).to(device)
+    w = torch.randn(co, ci, 3, 3, generator=g) / (ci * 9) ** 0.5
+    U = ops.wino_weight(w.to(device), co, ci, flip=False, tile=tile)
+    Ud = ops.wino_weight(w.to(device), ci, co, flip=True, tile=tile)
+    _, V = ops.conv3x3_wino(x, B, H, W, U, None, co, tile=tile, keep_v=True)
+    Vd, dM = ops.wino_dual_input(dy, B, H, W, tile=tile)
+    dx0 = ops.conv3x3_wino(dy, B, H, W, Ud, None, ci, tile=tile)
+    dx1 = ops.conv3x3_wino(dy, B, H, W, Ud, None, ci, tile=tile, v_in=Vd)
+    assert torch.equal(dx0, dx1)
+    dw0 = torch.empty(co, ci, 3, 3, device=device)
+    dw1 = torch.empty(co, ci, 3, 3, device=device)
+    ops.conv3x3_wgrad_wino(dy, V, B, H, W, ci, ci, co, dw0, tile=tile)
+    ops.conv3x3_wgrad_wino(dy, V, B, H, W, ci, ci, co, dw1, tile=tile, dM=dM)
+    assert torch.equal(dw0, dw1)
