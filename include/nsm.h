@@ -228,6 +228,22 @@ int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, int H
 
 /* up x2 then resize to (th,tw) in one pass (Unetmodel.py:140-141: up9 then
  * _upsample_and_match back to the skip size); no 4x intermediate. */
+/* The decoder's upsample of a block output that is never written: the source
+ * taps are z = lrelu(y2*scale+shift) (+ res) (Unetmodel.py:27-28,125-137),
+ * rounded as nsm_bn_act stores them; y2 = that block's second BN input, res
+ * its skip [B*Hi*Wi][C] or NULL. nsm_up2_resize_fwd_act needs the row-blocked
+ * composite (target width <= 2048, second step not upsizing). */
+int nsm_resize_fwd_act(const void* y2, int B, int Hi, int Wi, int C, void* out, int Ho, int Wo,
+                       const float* scale, const float* shift, float slope, const void* res,
+                       int dtype, void* stream);
+int nsm_up2_resize_fwd_act(const void* y2, int B, int h, int w, int C, void* out, int th, int tw,
+                           const float* scale, const float* shift, float slope, const void* res,
+                           int dtype, void* stream);
+/* encoder block output z = lrelu(y*scale+shift) and AvgPool2d(2)(z) from one
+ * read of y (Unetmodel.py:27-28,105,108,111) */
+int nsm_bn_act_pool(const void* y, int B, int H, int W, int C, const float* scale,
+                    const float* shift, float slope, void* z, void* pooled, int dtype,
+                    void* stream);
 int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, void* y, int th, int tw,
                        int dtype, void* stream);
 int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th, int tw,

@@ -450,6 +450,50 @@ __global__ void __launch_bounds__(256) avgpool2_fwd_kernel(const T* __restrict__
   }
 }
 
+// The encoder block output z = lrelu(bn2(Y2)) (Unetmodel.py:27-28) and its
+// AvgPool2d(2) (:105,108,111) from one read of Y2: each thread takes a 2x2
+// pixel quad (ceil grid, so odd rows / columns still get their z) of one
+// 8-channel group, writes the quad's z (the skip tensor) and, inside the floor
+// grid, their mean from the stored values (as avgpool2_fwd would read them).
+template <typename T>
+__global__ void __launch_bounds__(256) bn_act_pool_kernel(const T* __restrict__ y, int B, int H,
+                                                          int W, int C8, FastDiv fdC8,
+                                                          FastDiv fdWc, FastDiv fdHc,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          float slope, T* __restrict__ z,
+                                                          T* __restrict__ pooled) {
+  const int Hc = (H + 1) / 2, Wc = (W + 1) / 2, Ho = H / 2, Wo = W / 2, C = C8 * 8;
+  const uint32_t total = (uint32_t)B * Hc * Wc * C8;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t p = fdiv(i, fdC8);
+    const int c = (int)(i - p * (uint32_t)C8) * 8;
+    const uint32_t t = fdiv(p, fdWc);
+    const int cx = (int)(p - t * Wc);
+    const uint32_t b = fdiv(t, fdHc);
+    const int cy = (int)(t - b * Hc);
+    const F8 sc = ldf8(scale + c), sh = ldf8(shift + c);
+    F8 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int yy = 2 * cy + (k >> 1), xx = 2 * cx + (k & 1);
+      q[k] = f8zero();
+      if (yy < H && xx < W) {
+        const size_t off = (((size_t)b * H + yy) * W + xx) * C + c;
+        q[k] = as_stored8<T>(lrelu8(ld8(y + off) * sc + sh, slope));
+        st8(z + off, q[k]);
+      }
+    }
+    if (cy < Ho && cx < Wo) {
+      F8 sum = q[0];
+      sum += q[1];
+      sum += q[2];
+      sum += q[3];
+      st8(pooled + (((size_t)b * Ho + cy) * Wo + cx) * C + c, 0.25f * sum);
+    }
+  }
+}
+
 template <typename T, bool RED>
 __global__ void __launch_bounds__(256) avgpool2_bwd_add_kernel(const T* __restrict__ dy, int B,
                                                                int H, int W, int C8, FastDiv fdC8,
@@ -511,12 +555,34 @@ __device__ __forceinline__ uint32_t xcd_block() {
 
 // 8 channels (one 16-B bf16 vector / two fp32 vectors) per lane: the model's
 // activations (C % 8 == 0)
-template <typename T>
+// ACT ("act on load"): the source is not materialised — every tap is the
+// decoder block output z = lrelu(Y2*scale+shift) (+ skip), rounded as bn_act
+// stores it (Unetmodel.py:27-28,125-137 then :122-141's upsample), so z is
+// never written or re-read. ActSrc carries Y2's BN vectors and the skip.
+struct ActSrc {
+  const float* scale;
+  const float* shift;
+  const void* res;
+  float slope;
+};
+template <typename T, bool ACT>
+__device__ __forceinline__ F8 src8(const T* x, size_t off, const ActSrc& a, int c) {
+  if constexpr (!ACT) {
+    return ld8(x + off);
+  } else {
+    F8 o = lrelu8(ld8(x + off) * ldf8(a.scale + c) + ldf8(a.shift + c), a.slope);
+    if (a.res) o += ld8((const T*)a.res + off);
+    return as_stored8<T>(o);
+  }
+}
+
+template <typename T, bool ACT = false>
 __global__ void __launch_bounds__(256) resize_fwd8_kernel(const T* __restrict__ x, int Hi, int Wi,
                                                           int C8, uint32_t total, FastDiv fdC8,
                                                           FastDiv fdWo, FastDiv fdHo,
                                                           T* __restrict__ y, int Ho, int Wo,
-                                                          float sh, float sw) {
+                                                          float sh, float sw,
+                                                          ActSrc act = ActSrc{}) {
   const int C = C8 * 8;
   for (uint32_t i = xcd_block() * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     uint32_t p;
@@ -526,10 +592,11 @@ __global__ void __launch_bounds__(256) resize_fwd8_kernel(const T* __restrict__ 
     lin_idx(sh, q.y, Hi, y0, y1, ly0, ly1);
     lin_idx(sw, q.x, Wi, x0, x1, lx0, lx1);
     const size_t rb = (size_t)q.b * Hi;
-    const T* r0 = x + (rb + y0) * Wi * C + q.c;
-    const T* r1 = x + (rb + y1) * Wi * C + q.c;
-    const F8 v = ly0 * (lx0 * ld8(r0 + x0 * C) + lx1 * ld8(r0 + x1 * C)) +
-                 ly1 * (lx0 * ld8(r1 + x0 * C) + lx1 * ld8(r1 + x1 * C));
+    const size_t r0 = (rb + y0) * Wi * C + q.c, r1 = (rb + y1) * Wi * C + q.c;
+    const F8 v = ly0 * (lx0 * src8<T, ACT>(x, r0 + x0 * C, act, q.c) +
+                        lx1 * src8<T, ACT>(x, r0 + x1 * C, act, q.c)) +
+                 ly1 * (lx0 * src8<T, ACT>(x, r1 + x0 * C, act, q.c) +
+                        lx1 * src8<T, ACT>(x, r1 + x1 * C, act, q.c));
     st8(y + (size_t)p * C + q.c, v);
   }
 }
@@ -748,10 +815,10 @@ __device__ __forceinline__ int comb3(float s2, int o, int n2, float s1, int n1, 
   return i00;
 }
 
-template <typename T>
+template <typename T, bool ACT = false>
 __global__ void __launch_bounds__(256) up2_resize_fwd_rows_kernel(
     const T* __restrict__ x, int h, int w, int C8, FastDiv fdC8, T* __restrict__ y, int th, int tw,
-    float s1h, float s1w, float s2h, float s2w) {
+    float s1h, float s1w, float s2h, float s2w, ActSrc act = ActSrc{}) {
   extern __shared__ float u2f_tables[];  // [tw][3] weights, [tw] first tap
   float* xw = u2f_tables;
   int* xb = (int*)(u2f_tables + (size_t)tw * 3);
@@ -761,9 +828,9 @@ __global__ void __launch_bounds__(256) up2_resize_fwd_rows_kernel(
   float wy[3];
   const int yb = comb3(s2h, oy, 2 * h, s1h, h, wy);
   __syncthreads();
-  const T* rows[3];
+  size_t rows[3];
 #pragma unroll
-  for (int a = 0; a < 3; ++a) rows[a] = x + ((size_t)b * h + min(yb + a, h - 1)) * w * C;
+  for (int a = 0; a < 3; ++a) rows[a] = ((size_t)b * h + min(yb + a, h - 1)) * w * C;
   T* orow = y + ((size_t)b * th + oy) * tw * C;
   // gridDim.y segments per row (small batches: enough blocks for the chip)
   const uint32_t items = (uint32_t)tw * (uint32_t)C8;
@@ -778,9 +845,9 @@ __global__ void __launch_bounds__(256) up2_resize_fwd_rows_kernel(
     F8 v[9];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
-      v[3 * a] = ld8(rows[a] + c0);
-      v[3 * a + 1] = ld8(rows[a] + c1);
-      v[3 * a + 2] = ld8(rows[a] + c2);
+      v[3 * a] = src8<T, ACT>(x, rows[a] + c0, act, c);
+      v[3 * a + 1] = src8<T, ACT>(x, rows[a] + c1, act, c);
+      v[3 * a + 2] = src8<T, ACT>(x, rows[a] + c2, act, c);
     }
     F8 acc = f8zero();
 #pragma unroll
@@ -1561,6 +1628,28 @@ extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, 
   return 0;
 }
 
+extern "C" int nsm_bn_act_pool(const void* y, int B, int H, int W, int C, const float* scale,
+                               const float* shift, float slope, void* z, void* pooled, int dtype,
+                               void* stream) {
+  NSM_CHECK_ARG(y && z && pooled && scale && shift && C % 8 == 0 && H >= 2 && W >= 2,
+                "bn_act_pool: bad args");
+  const long long work = (long long)B * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
+  NSM_CHECK_ARG(work < (1ll << 31), "bn_act_pool: too large");
+  dim3 g(grid_for(work));
+  const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv((W + 1) / 2),
+                fh = make_fastdiv((H + 1) / 2);
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL(bn_act_pool_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(bf16_t, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,
+                       NSM_T(bf16_t, z), NSM_T(bf16_t, pooled));
+  else
+    hipLaunchKernelGGL(bn_act_pool_kernel<float>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(float, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,
+                       NSM_T(float, z), NSM_T(float, pooled));
+  NSM_LAUNCH_CHECK("bn_act_pool");
+  return 0;
+}
+
 extern "C" int nsm_avgpool2_fwd(const void* x, int B, int H, int W, int C, void* y, int dtype,
                                 void* stream) {
   NSM_CHECK_ARG(x && y && C % 8 == 0 && H >= 2 && W >= 2, "avgpool2_fwd: bad args");
@@ -1691,6 +1780,62 @@ static int resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, in
 extern "C" int nsm_resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho, int Wo,
                               int dtype, void* stream) {
   return resize_bwd(dy, B, Hi, Wi, C, dx, Ho, Wo, dtype, nullptr, stream);
+}
+
+// ---- upsample of a decoder block output that is never materialised ---------
+extern "C" int nsm_resize_fwd_act(const void* y2, int B, int Hi, int Wi, int C, void* out, int Ho,
+                                  int Wo, const float* scale, const float* shift, float slope,
+                                  const void* res, int dtype, void* stream) {
+  NSM_CHECK_ARG(y2 && out && scale && shift && B > 0 && Hi > 0 && Wi > 0 && Ho > 0 && Wo > 0 &&
+                    C % 8 == 0, "resize_fwd_act: bad args");
+  const long long tot8 = (long long)B * Ho * Wo * (C / 8);
+  NSM_CHECK_ARG(tot8 < (1ll << 31), "resize_fwd_act: too large");
+  const float sh = ac_scale(Hi, Ho), sw = ac_scale(Wi, Wo);
+  hipStream_t s = as_stream(stream);
+  dim3 g(xcd_grid(tot8));
+  const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(Wo), fh = make_fastdiv(Ho);
+  const ActSrc act{scale, shift, res, slope};
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL((resize_fwd8_kernel<bf16_t, true>), g, dim3(256), 0, s,
+                       NSM_CT(bf16_t, y2), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh,
+                       NSM_T(bf16_t, out), Ho, Wo, sh, sw, act);
+  else
+    hipLaunchKernelGGL((resize_fwd8_kernel<float, true>), g, dim3(256), 0, s, NSM_CT(float, y2),
+                       Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(float, out), Ho, Wo, sh,
+                       sw, act);
+  NSM_LAUNCH_CHECK("resize_fwd_act");
+  return 0;
+}
+
+extern "C" int nsm_up2_resize_fwd_act(const void* y2, int B, int h, int w, int C, void* out,
+                                      int th, int tw, const float* scale, const float* shift,
+                                      float slope, const void* res, int dtype, void* stream) {
+  NSM_CHECK_ARG(y2 && out && scale && shift && B > 0 && h > 0 && w > 0 && th > 0 && tw > 0 &&
+                    C % 8 == 0, "up2_resize_fwd_act: bad args");
+  const long long tot8 = (long long)B * th * tw * (C / 8);
+  NSM_CHECK_ARG(tot8 < (1ll << 31), "up2_resize_fwd_act: too large");
+  NSM_CHECK_ARG(tw <= U2_MAXW && (long long)B * th < (1ll << 31) && th * 2 >= 2 * h - 1 &&
+                    tw * 2 >= 2 * w - 1, "up2_resize_fwd_act: needs the row-blocked kernel");
+  hipStream_t s = as_stream(stream);
+  const float a = ac_scale(h, 2 * h), b = ac_scale(w, 2 * w), c = ac_scale(2 * h, th),
+              d = ac_scale(2 * w, tw);
+  const FastDiv f8 = make_fastdiv(C / 8);
+  const size_t lds = (size_t)tw * 4 * 4;
+  const long long rows = (long long)B * th, per_row = (long long)tw * (C / 8);
+  long long segs = (2048 + rows - 1) / rows;
+  segs = std::max(1ll, std::min({segs, 16ll, (per_row + 1023) / 1024}));
+  const dim3 gr((unsigned)rows, (unsigned)segs);
+  const ActSrc act{scale, shift, res, slope};
+  if (dtype == NSM_BF16)
+    hipLaunchKernelGGL((up2_resize_fwd_rows_kernel<bf16_t, true>), gr, dim3(256), lds, s,
+                       NSM_CT(bf16_t, y2), h, w, C / 8, f8, NSM_T(bf16_t, out), th, tw, a, b, c,
+                       d, act);
+  else
+    hipLaunchKernelGGL((up2_resize_fwd_rows_kernel<float, true>), gr, dim3(256), lds, s,
+                       NSM_CT(float, y2), h, w, C / 8, f8, NSM_T(float, out), th, tw, a, b, c, d,
+                       act);
+  NSM_LAUNCH_CHECK("up2_resize_fwd_act");
+  return 0;
 }
 
 extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, void* y, int th,

@@ -529,6 +529,49 @@ def resize_bwd(dy, B, Hi, Wi, Ho, Wo, bnred=None):
     return dx if bnred is None else (dx, part)
 
 
+class Lazy:
+    """A decoder block output z = lrelu(bn2(Y2)) (+ res) that is not
+    materialised: the next upsample computes it on load (resize_act)."""
+    __slots__ = ("y2", "st", "res")
+
+    def __init__(self, y2, st, res):
+        self.y2, self.st, self.res = y2, st, res
+
+    def materialise(self, slope=0.2):
+        return bn_act(self.y2, self.st, slope, res=self.res)
+
+
+def resize_act(z, B, Hi, Wi, Ho, Wo, slope=0.2):
+    """resize of a Lazy block output (nsm_resize_fwd_act)."""
+    C = z.y2.shape[-1]
+    y = like(B * Ho * Wo, C, z.y2)
+    call("nsm_resize_fwd_act", ptr(z.y2), B, Hi, Wi, C, ptr(y), Ho, Wo, ptr(z.st.scale),
+         ptr(z.st.shift), slope, ptr(z.res), dt(z.y2), stream())
+    return y
+
+
+def up2_resize_act(z, B, h, w, th, tw, slope=0.2):
+    """up x2 + resize of a Lazy block output (nsm_up2_resize_fwd_act), or None
+    when the row-blocked kernel does not take this geometry."""
+    if not (tw <= 2048 and th * 2 >= 2 * h - 1 and tw * 2 >= 2 * w - 1):
+        return None
+    C = z.y2.shape[-1]
+    y = like(B * th * tw, C, z.y2)
+    call("nsm_up2_resize_fwd_act", ptr(z.y2), B, h, w, C, ptr(y), th, tw, ptr(z.st.scale),
+         ptr(z.st.shift), slope, ptr(z.res), dt(z.y2), stream())
+    return y
+
+
+def bn_act_pool(y, st, B, H, W, slope=0.2):
+    """(z, avgpool2(z)) with z = lrelu(y*scale+shift), one read of y."""
+    C = y.shape[-1]
+    z = like(B * H * W, C, y)
+    pooled = like(B * (H // 2) * (W // 2), C, y)
+    call("nsm_bn_act_pool", ptr(y), B, H, W, C, ptr(st.scale), ptr(st.shift), slope, ptr(z),
+         ptr(pooled), dt(y), stream())
+    return z, pooled
+
+
 def up2_resize(x, B, h, w, th, tw):
     """bilinear x2 (align_corners) then resize to (th, tw), one pass."""
     C = x.shape[-1]

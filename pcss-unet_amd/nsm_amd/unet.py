@@ -37,6 +37,14 @@ SLOPE = 0.2
 # forces one tile everywhere.
 WINOGRAD_MIN_CHANNELS = (int(os.environ.get("NSM_WINO_MIN", "64"))
                          if os.environ.get("NSM_WINOGRAD", "1") != "0" else 1 << 30)
+# NSM_ACT_POOL=0: the encoder block output and its AvgPool2d as two passes
+# (bn_act, avgpool2) instead of one (ops.bn_act_pool)
+ACT_POOL = os.environ.get("NSM_ACT_POOL", "1") != "0"
+# NSM_LAZY_DECODER=1 (bf16): compute the decoder block outputs c5, merge6-8
+# inside the next block's upsample (ops.Lazy) instead of materialising them.
+# Off by default: B=64 bf16 A/B 1214 -> 1189 frames/s (the act-on-load upsample
+# reads Y2 and the residual at every bilinear tap; conv9 stage +0.9 ms).
+LAZY_DECODER = os.environ.get("NSM_LAZY_DECODER", "0") != "0"
 # NSM_DUAL_WINO=0: the Winograd dgrad and wgrad transform the output gradient
 # in two separate reads of it instead of one (nsm_wino_dual_input)
 DUAL_TRANSFORM = os.environ.get("NSM_DUAL_WINO", "1") != "0"
@@ -620,9 +628,19 @@ class _UnetFn(torch.autograd.Function):
                 s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}",
                                pw=sw.block(k) if sw else None, fuse_out=True)
                 saved[k], shapes[k] = s, (h, w)
-                c[k] = s.Z if s.Z is not None else ops.bn_act(s.Y2, s.bn2, SLOPE)
+                if s.Z is not None:
+                    c[k] = s.Z
+                    if k < 5:
+                        inp = ops.avgpool2(c[k], B, h, w)
+                elif k < 5 and ACT_POOL:   # z and its pooling from one read of Y2
+                    c[k], inp = ops.bn_act_pool(s.Y2, s.bn2, B, h, w, SLOPE)
+                elif k == 5 and LAZY_DECODER and cdt == torch.bfloat16:
+                    c[k] = ops.Lazy(s.Y2, s.bn2, None)   # sampled by conv6's upsample
+                else:
+                    c[k] = ops.bn_act(s.Y2, s.bn2, SLOPE)
+                    if k < 5:
+                        inp = ops.avgpool2(c[k], B, h, w)
                 if k < 5:
-                    inp = ops.avgpool2(c[k], B, h, w)
                     h, w = h // 2, w // 2
         skip_shape = {6: shapes[4], 7: shapes[3], 8: shapes[2], 9: (Rh, Rw)}
         cur, (h, w) = c[5], shapes[5]
@@ -632,10 +650,17 @@ class _UnetFn(torch.autograd.Function):
                 h2, w2 = 2 * h, 2 * w
                 th, tw = skip_shape[k]
                 src = None
+                lazy = isinstance(cur, ops.Lazy)
                 if (th, tw) != (h2, w2):   # up x2 then _upsample_and_match, fused
-                    up = ops.up2_resize(cur, B, h, w, th, tw)
+                    up = ops.up2_resize_act(cur, B, h, w, th, tw, SLOPE) if lazy else None
+                    if up is None:
+                        cur = cur.materialise(SLOPE) if lazy else cur
+                        up = ops.up2_resize(cur, B, h, w, th, tw)
                 elif fuses_resize(mod.block(k), cdt):  # sampled by the Winograd input transform
+                    cur = cur.materialise(SLOPE) if lazy else cur
                     up, src = None, (cur, h, w)
+                elif lazy:                 # the previous block output computed on load
+                    up = ops.resize_act(cur, B, h, w, h2, w2, SLOPE)
                 else:                      # match is the identity (bitwise, as in ATen)
                     up = ops.resize(cur, B, h, w, h2, w2)
                 ups[k] = (h, w, h2, w2, th, tw)
@@ -643,7 +668,12 @@ class _UnetFn(torch.autograd.Function):
                 s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}",
                                pw=sw.block(k) if sw else None, src=src, fuse_out=True, res=res)
                 saved[k] = s
-                cur = s.Z if s.Z is not None else ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
+                if s.Z is not None:
+                    cur = s.Z
+                elif k != 9 and LAZY_DECODER and cdt == torch.bfloat16:
+                    cur = ops.Lazy(s.Y2, s.bn2, res)     # only the next upsample reads it
+                else:
+                    cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
                 h, w = th, tw
         z9 = cur
         with ops.stage("head.fwd"):

@@ -518,3 +518,28 @@ def test_wino_dual_input(ops, device, B, H, W, ci, co, tile):
     ops.conv3x3_wgrad_wino(dy, V, B, H, W, ci, ci, co, dw0, tile=tile)
     ops.conv3x3_wgrad_wino(dy, V, B, H, W, ci, ci, co, dw1, tile=tile, dM=dM)
     assert torch.equal(dw0, dw1)
+
+
+@pytest.mark.parametrize("dtype", ["f32", "bf16"])
+@pytest.mark.parametrize("B,H,W,C", [(2, 16, 18, 64), (1, 9, 7, 128), (2, 5, 9, 512)])
+def test_bn_act_pool_and_lazy_resize(ops, device, B, H, W, C, dtype):
+    """bn_act_pool == bn_act then avgpool2 (bitwise); resize / up2_resize of a
+    Lazy block output == bn_act(+res) then the resize (bitwise)."""
+    tdt = torch.bfloat16 if dtype == "bf16" else torch.float32
+    g = torch.Generator().manual_seed(H * W + C)
+    y = (torch.randn(B * H * W, C, generator=g) * 2).to(device=device, dtype=tdt)
+    res = torch.randn(B * H * W, C, generator=g).to(device=device, dtype=tdt)
+    st = ops.BNState(C, device)
+    st.scale.copy_(torch.rand(C, generator=g) + 0.5)
+    st.shift.copy_(torch.randn(C, generator=g))
+    z0 = ops.bn_act(y, st, 0.2)
+    p0 = ops.avgpool2(z0, B, H, W)
+    z1, p1 = ops.bn_act_pool(y, st, B, H, W, 0.2)
+    assert torch.equal(z0, z1) and torch.equal(p0, p1)
+    zr = ops.bn_act(y, st, 0.2, res=res)
+    lazy = ops.Lazy(y, st, res)
+    assert torch.equal(ops.resize(zr, B, H, W, 2 * H, 2 * W),
+                       ops.resize_act(lazy, B, H, W, 2 * H, 2 * W, 0.2))
+    th, tw = 2 * H - 1, 2 * W - 1
+    a = ops.up2_resize_act(lazy, B, H, W, th, tw, 0.2)
+    assert a is not None and torch.equal(ops.up2_resize(zr, B, H, W, th, tw), a)
