@@ -122,6 +122,15 @@ int nsm_wino_input_resize(const float* x, int ldx, int B, int hi, int wi, int H,
                           int tile, int relu, float* V, void* stream);
 int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
                   int tile, float* Mb, void* stream);
+/* fp32 GEMM arithmetic of the Winograd layers (the batched GEMMs of
+ * nsm_wino_gemm / nsm_conv3x3_wino and the weight gradient of
+ * nsm_conv3x3_wgrad_wino): 1 (default, env NSM_F32_SPLIT) = each fp32 operand
+ * split exactly into three bf16 terms, the six products above fp32 rounding
+ * on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (fp32 accuracy, 2.67x
+ * fewer MFMA cycles); 0 = v_mfma_f32_32x32x2_f32. Returns the previous mode.
+ * Replaces no reference interface (the reference runs cuDNN fp32 convs,
+ * Unetmodel.py:16-27); host-wide setting, not per stream. */
+int nsm_set_f32_split(int mode);
 int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, int tile, const float* bias,
                     float* y, int ldy, void* stream);
 /* nsm_wino_output that also emits the BatchNorm batch statistics of y

@@ -779,6 +779,8 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
   EP::template apply<TM, TN, WM, WN>(ep, acc, cx, M, N, split);
 }
 
+#include "nsm_conv_split.inc"
+
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
@@ -789,8 +791,7 @@ static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const typename 
   using AL = ConvActLoader<BM, NT, PRO>;
   using BL = RowsKLoader<BN, NT>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 1);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EP, ConvActP, RowsKP>), grid,
-                     dim3(NT), 0, s, ap, bp, ep, M, N, K, K, 1);
+  launch_f32_gemm<BM, BN, WM, WN, AL, BL, EP, ConvActP, RowsKP>(grid, s, ap, bp, ep, M, N, K, K, 1);
   NSM_LAUNCH_CHECK("conv_fwd");
   return 0;
 }
@@ -831,8 +832,8 @@ static int launch_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& 
   using AL = PixRowsLoader<BM, NT, false, false>;
   using BL = PixRowsLoader<BN, NT, SHIFT, PRO>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), splits);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlabV, PixRowsP, PixRowsP>), grid,
-                     dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, splits);
+  launch_f32_gemm<BM, BN, WM, WN, AL, BL, EpiSlabV, PixRowsP, PixRowsP>(grid, s, ap, bp, ep, M, N, K,
+                                                                        kchunk, splits);
   NSM_LAUNCH_CHECK("conv_wgrad");
   return 0;
 }
@@ -1583,8 +1584,7 @@ static int launch_wino_gemm(const RowsKP& ap, const RowsKP& bp, const EpiStoreP&
   using AL = RowsKLoader<BM, NT>;
   using BL = RowsKLoader<BN, NT>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), nb);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiStore, RowsKP, RowsKP>), grid,
-                     dim3(NT), 0, s, ap, bp, ep, M, N, K, K, 1);
+  launch_f32_gemm<BM, BN, WM, WN, AL, BL, EpiStore, RowsKP, RowsKP>(grid, s, ap, bp, ep, M, N, K, K, 1);
   NSM_LAUNCH_CHECK("wino_gemm");
   return 0;
 }
@@ -1872,8 +1872,10 @@ extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W
                f32_epi_vec()};
   const int M = (int)g.T, N = cout_p, K = cin_p, nb = g.alpha2;
   long long mb128 = ceil_div(M, 128);
+  // the split kernel runs two blocks per CU (one stage of LDS): 128x128 from
+  // two dispatch rounds on
   if (N >= 128)
-    return (mb128 * ceil_div(N, 128) * nb >= 1024)
+    return (mb128 * ceil_div(N, 128) * nb >= (f32_split() ? 512 : 1024))
                ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s)
                : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s);
   if (N >= 64) return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, nb, s);
@@ -2028,8 +2030,8 @@ static int launch_wino_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSl
   using AL = PixRowsLoader<BM, NT, false, false>;
   using BL = PixRowsLoader<BN, NT, false, false>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), nb * splits);
-  hipLaunchKernelGGL((gemm_f32_kernel<BM, BN, WM, WN, AL, BL, EpiSlabV, PixRowsP, PixRowsP>), grid,
-                     dim3(NT), 0, s, ap, bp, ep, M, N, K, kchunk, splits);
+  launch_f32_gemm<BM, BN, WM, WN, AL, BL, EpiSlabV, PixRowsP, PixRowsP>(grid, s, ap, bp, ep, M, N, K,
+                                                                        kchunk, splits);
   NSM_LAUNCH_CHECK("wino_wgrad_gemm");
   return 0;
 }
@@ -2167,3 +2169,11 @@ static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float
 
 namespace nsm {
 #include "nsm_conv_bf16.inc"
+
+// 1: fp32 GEMMs on the bf16 matrix cores by the exact split (default), 0: on
+// v_mfma_f32_32x32x2_f32; returns the previous mode
+extern "C" int nsm_set_f32_split(int mode) {
+  const int prev = f32_split() ? 1 : 0;
+  g_f32_split = mode ? 1 : 0;
+  return prev;
+}

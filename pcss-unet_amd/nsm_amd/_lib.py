@@ -34,6 +34,7 @@ _SIGS = {
     "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, I, I, P, I, P, Z, P]),
     "nsm_wino_input": (I, [P, I, I, I, I, I, I, I, P, P]),
     "nsm_wino_gemm": (I, [P, P, I, I, I, I, I, I, P, P]),
+    "nsm_set_f32_split": (I, [I]),
     "nsm_wino_output": (I, [P, I, I, I, I, I, P, P, I, P]),
     "nsm_wino_wgrad_ws": (Z, [I, I, I, I, I, I]),
     "nsm_conv3x3_wgrad_wino": (I, [P, I, P, I, I, I, I, I, I, I, I, P, P, Z, P]),

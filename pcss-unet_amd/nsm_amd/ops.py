@@ -35,6 +35,14 @@ def empty(*shape, device):
     return torch.empty(*shape, dtype=F32, device=device)
 
 
+def set_f32_split(mode):
+    """fp32 GEMMs on the bf16 matrix cores by the exact three-way split (1,
+    the default; fp32 accuracy, csrc/nsm_conv_split.inc) or on the fp32 MFMA
+    (0). Returns the previous mode."""
+    from ._lib import lib
+    return int(lib.nsm_set_f32_split(int(mode)))
+
+
 # ---- parameters ------------------------------------------------------------
 def pack_conv_weight(w, cout_p, cin_p, mode, dtype=F32):
     """MFMA operand layout of a conv weight, in the activations' dtype."""
