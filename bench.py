@@ -206,6 +206,13 @@ def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
     achieved = alg_flops / (conv_ms * 1e-3) / 1e12
     ex = ex_flops / (conv_ms * 1e-3) / 1e12
     gx = ex_flops / (gemm_ms * 1e-3) / 1e12
+    split = os.environ.get("NSM_F32_SPLIT", "1") != "0"
+    arith = {"f32_gemm": "exact 3-way bf16 split, 6 products on v_mfma_f32_32x32x16_bf16, fp32 "
+                         "accumulate (csrc/nsm_conv_split.inc)" if split else
+                         "v_mfma_f32_32x32x2_f32",
+             # the matrix-core work the split issues: 6 bf16 products per fp32 product
+             "bf16_mfma_flops_per_launch": 6 * ex_flops if split else None,
+             "gemm_bf16_mfma_frac": round(6 * gx / BF16_PEAK_TFLOPS, 4) if split else None}
     return {"kernel": f"conv6.conv.0.fwd 3x3 1024->1024 at {h6}x{w6}, B={B}: Winograd F({m}x{m},3x3) "
                       f"= nsm_wino_input + nsm_wino_gemm ({nb} x M={T6} N=1024 K=1024) + "
                       "nsm_wino_output",
@@ -218,7 +225,7 @@ def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
             "executed_flops_per_launch": ex_flops,
             "gemm": {"avg_launch_ms": round(gemm_ms, 4), "executed_tflops": round(gx, 2),
                      "executed_frac": round(gx / FP32_PEAK_TFLOPS, 4),
-                     "bytes_per_launch": gemm_bytes}}
+                     "bytes_per_launch": gemm_bytes, **arith}}
 
 
 def direct_roofline(B, H, W, kern_ms, launches):

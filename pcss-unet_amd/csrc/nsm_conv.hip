@@ -327,7 +327,7 @@ struct EpiStore {
   __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
                                int) {
     const int col = cx.lane & 31, h = cx.lane >> 5;
-    float* yb = e.y + (size_t)blockIdx.z * e.bstride;  // store paths run with zsplit == 1
+    float* yb = e.y + (size_t)cx.zslab * e.bstride;  // store paths run with zsplit == 1
     float bv[TN];
 #pragma unroll
     for (int tn = 0; tn < TN; ++tn) {

@@ -63,3 +63,65 @@ def test_split_matches_fp32_accuracy(ops, device, B, H, W, ci, co, tile):
         # the Winograd transforms dominate both; the GEMM arithmetic must not add error
         assert r1 <= 1.25 * r0 + 1e-9, (name, r0, r1)
         assert m1 <= 1.5 * m0 + 1e-8, (name, m0, m1)
+
+
+@pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 16, 16, 32, 64, 3), (2, 24, 20, 64, 128, 1),
+                                           (1, 33, 35, 128, 128, 3), (2, 64, 64, 32, 32, 3)])
+def test_split_direct_convs(ops, device, B, H, W, ci, co, k):
+    """Direct implicit-GEMM forward, input gradient and split-K weight gradient
+    (the non-Winograd fp32 GEMMs) in both modes against float64."""
+    g = torch.Generator().manual_seed(B * 100 + ci + co + k)
+    x = torch.randn(B, ci, H, W, generator=g, dtype=torch.float64, requires_grad=True)
+    w = (torch.randn(co, ci, k, k, generator=g, dtype=torch.float64) / (ci * k * k) ** 0.5).requires_grad_(True)
+    dy = torch.randn(B, co, H, W, generator=g, dtype=torch.float64)
+    ref = F.conv2d(x, w, padding=k // 2)
+    ref.backward(dy)
+    xs, ws, dys = x.detach().float(), w.detach().float(), dy.float()
+    res = {}
+    for mode in (0, 1):
+        ops.set_f32_split(mode)
+        wp = ops.pack_conv_weight(ws.to(device), co, ci, ops.PACK_FWD)
+        y = ops.conv_fwd(nhwc(xs).to(device), B, H, W, wp, None, co, k)
+        wd = ops.pack_conv_weight(ws.to(device), co, ci, ops.PACK_DGRAD)
+        dx = ops.conv_fwd(nhwc(dys).to(device), B, H, W, wd, None, ci, k)
+        dw = torch.empty(co, ci, k, k, device=device)
+        ops.conv_wgrad(nhwc(dys).to(device), nhwc(xs).to(device), B, H, W, k, ci, co, dw)
+        res[mode] = (_errs(nchw(y.cpu(), B, H, W), ref.detach()), _errs(nchw(dx.cpu(), B, H, W), x.grad),
+                     _errs(dw.cpu(), w.grad))
+    ops.set_f32_split(1)
+    for i, name in enumerate(("fwd", "dgrad", "wgrad")):
+        (m0, r0), (m1, r1) = res[0][i], res[1][i]
+        print(f"direct k{k} {name}: fp32-MFMA max {m0:.2e} rms {r0:.2e} | split max {m1:.2e} rms {r1:.2e}")
+        assert r1 <= 1.5 * r0 + 1e-9, (name, r0, r1)
+        assert m1 <= 2.0 * m0 + 1e-8, (name, m0, m1)
+
+
+def test_split_train_step_vs_oracle(ops, device):
+    """Model level: a 1x7x256x256 train step with the split GEMMs stays as close
+    to the CPU fp32 oracle as the fp32-MFMA path does (output, loss, grads)."""
+    from oracle import unet_ref as O
+    from oracle.weights import make_state, synthetic_batch
+    from nsm_amd import CustomLoss, Unet
+    np_sd = make_state(7, 42)
+    x_np, y_np = synthetic_batch(1, 7, 256, 256)
+    sd = O.torch_state(np_sd, requires_grad=True)
+    xo = torch.from_numpy(x_np).requires_grad_(True)
+    oo, _ = O.forward(sd, xo, True, None, 0.0)
+    O.custom_loss(oo, torch.from_numpy(y_np), 0.9).backward()
+    errs = {}
+    for mode in (0, 1):
+        ops.set_f32_split(mode)
+        m = Unet(in_ch=7, dropout_rate=0.0)
+        m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in np_sd.items()})
+        m = m.to(device).train()
+        x = torch.from_numpy(x_np).to(device).requires_grad_(True)
+        out = m(x)
+        CustomLoss(device, 0.9)(out, torch.from_numpy(y_np).to(device)).backward()
+        ge = max(((p.grad.cpu().double() - sd[k].grad.double()).norm() / sd[k].grad.double().norm()).item()
+                 for k, p in m.named_parameters() if not k.endswith("bias"))
+        errs[mode] = ((out.detach().cpu() - oo.detach()).abs().max().item(), ge)
+    ops.set_f32_split(1)
+    print(f"train step vs oracle: fp32-MFMA out {errs[0][0]:.2e} grad {errs[0][1]:.2e} | "
+          f"split out {errs[1][0]:.2e} grad {errs[1][1]:.2e}")
+    assert errs[1][0] <= 2.0 * errs[0][0] + 1e-6
+    assert errs[1][1] <= 2.0 * errs[0][1] + 1e-6
