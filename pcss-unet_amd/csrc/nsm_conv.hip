@@ -1210,21 +1210,50 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
 #pragma unroll
       for (int e = 0; e < A; ++e)
         lin_idx(sw, min(max(MT * tx - 1 + e, 0), W - 1), wi, x0[e], x1[e], lx0[e], lx1[e]);
+      // Separable: a patch row is ly0 * h(y0) + ly1 * h(y1), h(y) the
+      // x-interpolated source row y. The (m+2) patch rows of a x2 upsample
+      // touch only ~m/2 + 2 source rows, so h(y) is computed once per source
+      // row and kept while consecutive patch rows reuse it (4 loads per
+      // element -> ~1.5). The reuse tests depend on the tile only, which is
+      // uniform over a wave whenever C / CW >= 64 (the decoder layers).
+      VT h0[A], h1[A];
+      int ya = -1, yb = -1;  // source rows held in h0, h1
 #pragma unroll
       for (int a = 0; a < A; ++a) {
         const int yy = MT * ty - 1 + a;
         int y0, y1;
         float ly0, ly1;
         lin_idx(sh, min(max(yy, 0), H - 1), hi, y0, y1, ly0, ly1);
-        const float* r0 = x + ((size_t)b * hi + y0) * wi * ld + c;
-        const float* r1 = x + ((size_t)b * hi + y1) * wi * ld + c;
+        if (y0 != ya) {
+          if (y0 == yb) {
+#pragma unroll
+            for (int e = 0; e < A; ++e) h0[e] = h1[e];
+          } else {
+            const float* r0 = x + ((size_t)b * hi + y0) * wi * ld + c;
+#pragma unroll
+            for (int e = 0; e < A; ++e)
+              h0[e] = lx0[e] * *(const VT*)(r0 + (size_t)x0[e] * ld) +
+                      lx1[e] * *(const VT*)(r0 + (size_t)x1[e] * ld);
+          }
+          ya = y0;
+        }
+        if (y1 != yb) {
+          if (y1 == ya) {
+#pragma unroll
+            for (int e = 0; e < A; ++e) h1[e] = h0[e];
+          } else {
+            const float* r1 = x + ((size_t)b * hi + y1) * wi * ld + c;
+#pragma unroll
+            for (int e = 0; e < A; ++e)
+              h1[e] = lx0[e] * *(const VT*)(r1 + (size_t)x0[e] * ld) +
+                      lx1[e] * *(const VT*)(r1 + (size_t)x1[e] * ld);
+          }
+          yb = y1;
+        }
 #pragma unroll
         for (int e = 0; e < A; ++e) {
           const int xx = MT * tx - 1 + e;
-          const VT v = ly0 * (lx0[e] * *(const VT*)(r0 + (size_t)x0[e] * ld) +
-                              lx1[e] * *(const VT*)(r0 + (size_t)x1[e] * ld)) +
-                       ly1 * (lx0[e] * *(const VT*)(r1 + (size_t)x0[e] * ld) +
-                              lx1[e] * *(const VT*)(r1 + (size_t)x1[e] * ld));
+          const VT v = ly0 * h0[e] + ly1 * h1[e];
           d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) ? v : VT{};
         }
       }
@@ -1896,13 +1925,37 @@ static int wino_stat_step(int cout_p, int tile) {
   }
   return 256 / a;
 }
+// blocks of the statistics kernel resident at once on the device (every block
+// does the same grid-stride work, so a grid past one round leaves a tail:
+// F(6x6)'s 138 VGPRs hold 3 blocks per CU, i.e. 768 of a 1024-block grid)
+static int wino_stat_resident(int tile) {
+  static int cache[7] = {0, 0, 0, 0, 0, 0, 0};
+  if (tile < 0 || tile > 6) return 1024;
+  if (cache[tile]) return cache[tile];
+  int per = 0, dev = 0, cus = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) {
+    const void* k = tile == 6   ? (const void*)wino_output_kernel<6, true>
+                    : tile == 4 ? (const void*)wino_output_kernel<4, true>
+                                : (const void*)wino_output_kernel<2, true>;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, 0);
+  }
+  cache[tile] = (e == hipSuccess && per > 0 && cus > 0) ? per * cus : 1024;
+  return cache[tile];
+}
 static long long wino_stat_slots(long long T, int cout_p, int tile) {
   const int N4 = cout_p / (tile == 6 ? 1 : 4), step = wino_stat_step(cout_p, tile);
+  // the policy (stats form where a thread covers >= 2 tiles) is judged on
+  // ~1024 blocks; the grid itself is one resident round
   long long ns = (1024ll * 256) / N4;
   if (ns < 512) ns = 512;
   ns = ns / step * step;
   if (ns < step) ns = step;
   if (T < 2 * ns) return 0;
+  long long nr = ((long long)wino_stat_resident(tile) * 256) / N4;
+  nr = nr / step * step;
+  if (nr >= step && nr < ns) ns = nr;
   return ns;
 }
 

@@ -23,7 +23,7 @@ B8_CONV6 = 8 * 64 * 64
 KINDS = {
     "f32": dict(
         match=lambda n: n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n
-        and "gemm_f32_kernel" in n,
+        and ("gemm_f32_kernel" in n or "gemm_f32s_kernel" in n),
         grid=(8 * 8 * 64 * 256, 16 * 8 * 36 * 256), triple=True,
         alg=(2 * B8_CONV6 * 1024 + 9 * 1024 * 1024 + 1024) * 4,
         desc="conv6.conv.0 fwd (+ dgrad twin), B=8: wino_input + gemm_f32_kernel<128,128,2,2,"
