@@ -99,36 +99,47 @@ __device__ __forceinline__ double wave_sum_d(double v) {
   return v;
 }
 
+// fixed-order double sum over a 256-thread block (red: 4 doubles of LDS)
+__device__ __forceinline__ double block_sum_d(double v, double* red) {
+  v = wave_sum_d(v);
+  __syncthreads();  // red may still be read from a previous call
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// One 256-thread block per channel: every partial row of a pass is loaded by
+// one lane in one round (the per-wave form took ~nchunk/256 dependent rounds).
 __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
     const float* __restrict__ partial, int nchunk, int rpc, int M, int C, int c_real,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* run_mean,
     float* run_var, int64_t* num_batches, float momentum, float eps, int n_updates, float* mean_o,
     float* invstd_o, float* scale_o, float* shift_o) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0 && num_batches) *num_batches += n_updates;
-  if (c >= C) return;
+  __shared__ double red[4];
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x;
+  if (blockIdx.x == 0 && tid == 0 && num_batches) *num_batches += n_updates;
   // rpc == 0: counted partials [nchunk][3][C] = {sum, M2, count} (the Winograd
   // output transform's slots); else {sum, M2} of rpc-row chunks
   const size_t st = (size_t)(rpc ? 2 : 3) * C;
   double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-  int k = lane;
-  for (; k + 192 < nchunk; k += 256) {
+  int k = tid;
+  for (; k + 768 < nchunk; k += 1024) {
     s0 += partial[k * st + c];
-    s1 += partial[(k + 64) * st + c];
-    s2 += partial[(k + 128) * st + c];
-    s3 += partial[(k + 192) * st + c];
+    s1 += partial[(k + 256) * st + c];
+    s2 += partial[(k + 512) * st + c];
+    s3 += partial[(k + 768) * st + c];
   }
-  for (; k < nchunk; k += 64) s0 += partial[k * st + c];
-  const double mean = wave_sum_d((s0 + s1) + (s2 + s3)) / M;
+  for (; k < nchunk; k += 256) s0 += partial[k * st + c];
+  const double mean = block_sum_d((s0 + s1) + (s2 + s3), red) / M;
   double q0 = 0.0, q1 = 0.0;
-  for (k = lane; k < nchunk; k += 128) {
+  for (k = tid; k < nchunk; k += 512) {
     int n0 = rpc ? min(M, k * rpc + rpc) - k * rpc : (int)partial[k * st + 2 * C + c];
     if (n0 > 0) {
       double d = partial[k * st + c] / n0 - mean;
       q0 += partial[k * st + C + c] + n0 * d * d;
     }
-    int k1 = k + 64;
+    int k1 = k + 256;
     if (k1 < nchunk) {
       int n1 = rpc ? min(M, k1 * rpc + rpc) - k1 * rpc : (int)partial[k1 * st + 2 * C + c];
       if (n1 > 0) {
@@ -137,8 +148,8 @@ __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
       }
     }
   }
-  const double m2 = wave_sum_d(q0 + q1);
-  if (lane != 0) return;
+  const double m2 = block_sum_d(q0 + q1, red);
+  if (tid != 0) return;
   const float var_b = (float)(m2 / M);
   const float var_u = M > 1 ? (float)(m2 / (M - 1)) : var_b;
   const float mf = (float)mean;
@@ -306,24 +317,24 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
     const float* __restrict__ partial, int nchunk, int M, int C, int c_real,
     const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma,
     float* dbeta, float* dbias_prev, float* coef) {
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (c >= C) return;
+  __shared__ double red[4];
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x;  // one block per channel (see bn_finalize_train_kernel)
   const size_t st = (size_t)2 * C;
   double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
-  int k = lane;
-  for (; k + 64 < nchunk; k += 128) {
+  int k = tid;
+  for (; k + 256 < nchunk; k += 512) {
     a0 += partial[k * st + c];
     b0 += partial[k * st + C + c];
-    a1 += partial[(k + 64) * st + c];
-    b1 += partial[(k + 64) * st + C + c];
+    a1 += partial[(k + 256) * st + c];
+    b1 += partial[(k + 256) * st + C + c];
   }
-  for (; k < nchunk; k += 64) {
+  for (; k < nchunk; k += 256) {
     a0 += partial[k * st + c];
     b0 += partial[k * st + C + c];
   }
-  const double S1 = wave_sum_d(a0 + a1), S2 = wave_sum_d(b0 + b1);
-  if (lane != 0) return;
+  const double S1 = block_sum_d(a0 + a1, red), S2 = block_sum_d(b0 + b1, red);
+  if (tid != 0) return;
   const float gm = gamma[c], is = invstd[c];
   const double mdz = S1 / M, mdzx = S2 / M;
   const float k1 = gm * is;
@@ -1496,7 +1507,7 @@ extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_
   NSM_CHECK_ARG(nchunk >= 1 && (rows_per_chunk == 0 ||
                                 (rows_per_chunk >= 1 && (long long)nchunk * rows_per_chunk >= M)),
                 "bn_finalize: chunks do not cover M");
-  hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(ceil_div(C, 4)), dim3(256), 0,
+  hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(C), dim3(256), 0,
                      as_stream(stream), partial, nchunk, rows_per_chunk, M, C, c_real, gamma, beta,
                      run_mean,
                      run_var, num_batches, momentum, eps, n_updates, mean, invstd, scale, shift);
@@ -1597,7 +1608,7 @@ extern "C" int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int 
                                    const float* gamma, const float* invstd, float* dgamma,
                                    float* dbeta, float* dbias_prev, float* coef, void* stream) {
   NSM_CHECK_ARG(partial && gamma && invstd && coef, "bn_bwd_finalize: bad args");
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(ceil_div(C, 4)), dim3(256), 0,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0,
                      as_stream(stream), partial, nchunk, M, C, c_real, gamma, invstd, dgamma, dbeta,
                      dbias_prev, coef);
   NSM_LAUNCH_CHECK("bn_bwd_finalize");
