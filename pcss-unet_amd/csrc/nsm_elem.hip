@@ -432,6 +432,23 @@ struct BnRedAcc {
       st8(pr + C + tc * 8, red[tc]);
     }
   }
+  // a block covering channels [c0, c0 + 8 G) of a C-channel tensor (group =
+  // tid % G): its slice of partial row `row`
+  __device__ void write_slice(const BnRedP& r, int G, int c0, int C, int row) {
+    __shared__ F8 red[256];
+    const int tid = threadIdx.x, rl = 256 / G, tc = tid % G;
+    red[tid] = s1;
+    col_tree_reduce(red, G, rl, tid);
+    const F8 t1 = red[tc];
+    __syncthreads();
+    red[tid] = s2;
+    col_tree_reduce(red, G, rl, tid);
+    if (tid < G) {
+      float* pr = r.partial + (size_t)row * 2 * C + c0;
+      st8(pr + tc * 8, t1);
+      st8(pr + C + tc * 8, red[tc]);
+    }
+  }
 };
 
 // ---------------------------------------------------------------------------
@@ -868,6 +885,56 @@ __global__ void __launch_bounds__(256) up2_resize_fwd_rows_kernel(
   }
 }
 
+// Separable form of the row-blocked composite forward: grid = (output row,
+// channel slice). Phase 1 combines the row's 3 source rows with the y weights
+// into an fp32 LDS row [w][cb] (each source element loaded once per block);
+// phase 2 takes the 3 x taps of every output column from LDS: 3 global vector
+// loads per output instead of 9.
+template <typename T, bool ACT = false>
+__global__ void __launch_bounds__(256) up2_resize_fwd_sep_kernel(
+    const T* __restrict__ x, int h, int w, int C, int lcb8, T* __restrict__ y, int th, int tw,
+    float s1h, float s1w, float s2h, float s2w, ActSrc act = ActSrc{}) {
+  extern __shared__ float u2s_lds[];  // [w][cb] column sums, [tw][3] x weights, [tw] first taps
+  const int cb8 = 1 << lcb8, cb = cb8 * 8;
+  float* vcol = u2s_lds;
+  float* xw = vcol + (size_t)w * cb;
+  int* xb = (int*)(xw + (size_t)tw * 3);
+  const int tid = threadIdx.x;
+  const int b = blockIdx.x / th, oy = blockIdx.x - b * th;
+  const int c0 = blockIdx.y * cb;
+  for (int ox = tid; ox < tw; ox += blockDim.x) xb[ox] = comb3(s2w, ox, 2 * w, s1w, w, xw + ox * 3);
+  float wy[3];
+  const int yb = comb3(s2h, oy, 2 * h, s1h, h, wy);
+  size_t rows[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) rows[a] = ((size_t)b * h + min(yb + a, h - 1)) * w * C + c0;
+  const uint32_t items1 = (uint32_t)w << lcb8;
+  for (uint32_t it = tid; it < items1; it += blockDim.x) {
+    const int xi = (int)(it >> lcb8), c = (int)(it & (cb8 - 1)) * 8;
+    const size_t o = (size_t)xi * C + c;
+    const F8 v0 = src8<T, ACT>(x, rows[0] + o, act, c0 + c);
+    const F8 v1 = src8<T, ACT>(x, rows[1] + o, act, c0 + c);
+    const F8 v2 = src8<T, ACT>(x, rows[2] + o, act, c0 + c);
+    F8 acc = wy[0] * v0;
+    acc += wy[1] * v1;
+    acc += wy[2] * v2;
+    *(f32x4*)&vcol[xi * cb + c] = acc.a;
+    *(f32x4*)&vcol[xi * cb + c + 4] = acc.b;
+  }
+  __syncthreads();
+  T* orow = y + ((size_t)b * th + oy) * tw * C + c0;
+  const uint32_t items2 = (uint32_t)tw << lcb8;
+  for (uint32_t it = tid; it < items2; it += blockDim.x) {
+    const int ox = (int)(it >> lcb8), c = (int)(it & (cb8 - 1)) * 8;
+    const int x0 = xb[ox];
+    const float wx0 = xw[ox * 3], wx1 = xw[ox * 3 + 1], wx2 = xw[ox * 3 + 2];
+    F8 acc = wx0 * ld8(&vcol[x0 * cb + c]);
+    acc += wx1 * ld8(&vcol[min(x0 + 1, w - 1) * cb + c]);
+    acc += wx2 * ld8(&vcol[min(x0 + 2, w - 1) * cb + c]);
+    st8(orow + (size_t)ox * C + c, acc);
+  }
+}
+
 // combined 1-D weight of final output index o on input index i
 __device__ __forceinline__ float comb_w(float s2, int o, int n2, float s1, int n1, int i) {
   int m0, m1;
@@ -1091,6 +1158,225 @@ __global__ void __launch_bounds__(256) resize_bwd_rows_kernel(
     if (RED) ra.add<T>(rp, as_stored8<T>(acc), ((size_t)b * h + iy) * w + ix, C, c);
   }
   if (RED) ra.write(rp, C8);
+}
+
+// Separable row-blocked backward of a bilinear upsample: the single resize
+// (COMP false: nn.Upsample x2, Unetmodel.py:122-134) or the x2 + match
+// composite (COMP true: up9, :140-141). Grid = (input row, channel slice).
+// Phase 1 sums the block's dY rows (its y window) with their weights into an
+// fp32 LDS row [tw][cb] — every dY element is loaded once per block with
+// 16-B vector loads; phase 2 gathers each input column's x window from LDS.
+// The 2-D gather form issued RS_W x-taps per dY row per output (~24 vector
+// loads per output) and was load-issue bound at 2.2-2.9 TB/s.
+__device__ __forceinline__ void comp_window(float s1, float s2, int i, int n1, int out, int& lo,
+                                            int& hi) {
+  int mlo, mhi, lo2, hi2;
+  cand_range(s1, i, 2 * n1, mlo, mhi);
+  cand_range(s2, mlo, out, lo, hi2);
+  cand_range(s2, mhi, out, lo2, hi);
+  lo = min(lo, lo2);
+  hi = max(hi, hi2);
+}
+
+template <bool COMP>
+__device__ __forceinline__ float sep_w(float s1, float s2, int o, int n1, int i) {
+  if constexpr (COMP) return comb_w(s2, o, 2 * n1, s1, n1, i);
+  return lin_w(s1, o, n1, i);
+}
+
+template <bool COMP>
+__device__ __forceinline__ void sep_window(float s1, float s2, int i, int n1, int out, int& lo,
+                                           int& hi) {
+  if constexpr (COMP) comp_window(s1, s2, i, n1, out, lo, hi);
+  else cand_range(s1, i, out, lo, hi);
+  trim_range(lo, hi, [&](int o) { return sep_w<COMP>(s1, s2, o, n1, i); });
+}
+
+constexpr int SEP_YW = 32;  // union-window y weights kept per row (wider: computed per use)
+
+// R consecutive input rows per block share one pass over the dY rows of
+// their union window: each dY row is loaded once per block (a x2 upsample
+// spreads a dY row over 2 input rows, the composite over ~3, so one row per
+// block re-read dY 2-3x) and accumulated into R LDS rows.
+template <typename T, bool RED, bool COMP, int R>
+__global__ void __launch_bounds__(256) resize_bwd_sep_kernel(
+    const T* __restrict__ dy, int h, int w, int C, int lcb8, T* __restrict__ dx, int th, int tw,
+    float s1h, float s1w, float s2h, float s2w, BnRedP rp) {
+  // [R][tw][cb] row sums, [w][RS_W] x weights, [w] window starts, [w] widths
+  extern __shared__ float sep_lds[];
+  __shared__ float yw[R][SEP_YW];
+  __shared__ int ywin[2];
+  const int cb8 = 1 << lcb8, cb = cb8 * 8;
+  float* vrow = sep_lds;
+  float* xw = sep_lds + (size_t)R * tw * cb;
+  int* xlo = (int*)(xw + (size_t)w * RS_W);
+  int* xn = xlo + w;
+  const int tid = threadIdx.x;
+  const int hb = (h + R - 1) / R;
+  const int b = blockIdx.x / hb, iy0 = (blockIdx.x - b * hb) * R;
+  const int nr = min(R, h - iy0);
+  const int c0 = blockIdx.y * cb;
+  for (int ix = tid; ix < w; ix += blockDim.x) {
+    int lo, hi;
+    sep_window<COMP>(s1w, s2w, ix, w, tw, lo, hi);
+    xlo[ix] = lo;
+    xn[ix] = hi - lo + 1;
+#pragma unroll
+    for (int k = 0; k < RS_W; ++k)
+      xw[ix * RS_W + k] = lo + k <= hi ? sep_w<COMP>(s1w, s2w, lo + k, w, ix) : 0.f;
+  }
+  if (tid == 0) {
+    int lo, hi, lo2, hi2;
+    sep_window<COMP>(s1h, s2h, iy0, h, th, lo, hi);
+    sep_window<COMP>(s1h, s2h, iy0 + nr - 1, h, th, lo2, hi2);
+    ywin[0] = min(lo, lo2);
+    ywin[1] = max(hi, hi2);
+  }
+  __syncthreads();
+  const int olo = ywin[0], ny = ywin[1] - ywin[0] + 1;
+  // weight of union-window row k on input row iy0 + r (0 outside its window)
+  if (tid < R * SEP_YW) {
+    const int r = tid / SEP_YW, k = tid % SEP_YW;
+    yw[r][k] = (r < nr && k < ny) ? sep_w<COMP>(s1h, s2h, olo + k, h, iy0 + r) : 0.f;
+  }
+  __syncthreads();
+  // phase 1: vrow[r][ox][c] = sum_oy wy(oy, iy0 + r) dY[b][oy][ox][c0 + c]
+  const T* base = dy + (size_t)b * th * tw * C + c0;
+  const size_t rstride = (size_t)tw * C;
+  const uint32_t items1 = (uint32_t)tw << lcb8;
+  for (uint32_t it = tid; it < items1; it += blockDim.x) {
+    const int ox = (int)(it >> lcb8), c = (int)(it & (cb8 - 1)) * 8;
+    const T* p = base + (size_t)olo * rstride + (size_t)ox * C + c;
+    F8 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = f8zero();
+    auto add = [&](const F8& v, int k) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const float wk = k < SEP_YW ? yw[r][k]
+                                    : (r < nr ? sep_w<COMP>(s1h, s2h, olo + k, h, iy0 + r) : 0.f);
+        const F8 t = acc[r] + wk * v;  // a zero weight must not pass an Inf / NaN on
+        acc[r].a = wk != 0.f ? t.a : acc[r].a;
+        acc[r].b = wk != 0.f ? t.b : acc[r].b;
+      }
+    };
+    int k = 0;
+    for (; k + 1 < ny; k += 2) {  // two rows' loads in flight
+      const F8 v0 = ld8(p + (size_t)k * rstride), v1 = ld8(p + (size_t)(k + 1) * rstride);
+      add(v0, k);
+      add(v1, k + 1);
+    }
+    if (k < ny) add(ld8(p + (size_t)k * rstride), k);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      float* q = &vrow[((size_t)r * tw + ox) * cb + c];
+      *(f32x4*)q = acc[r].a;
+      *(f32x4*)(q + 4) = acc[r].b;
+    }
+  }
+  __syncthreads();
+  // phase 2: dx[b][iy0 + r][ix][c0 + c] = sum_k wx(ix, k) vrow[r][xlo + k][c]
+  const uint32_t items2 = (uint32_t)w << lcb8;
+  for (int r = 0; r < nr; ++r) {
+    const int iy = iy0 + r;
+    T* orow = dx + ((size_t)b * h + iy) * w * C + c0;
+    const float* vr = vrow + (size_t)r * tw * cb;
+    BnRedAcc ra;
+    if (RED) ra.init(rp, c0 + (tid & (cb8 - 1)) * 8);
+    for (uint32_t it = tid; it < items2; it += blockDim.x) {
+      const int ix = (int)(it >> lcb8), c = (int)(it & (cb8 - 1)) * 8;
+      const int lo = xlo[ix], n = xn[ix];
+      F8 acc = f8zero();
+      if (n <= RS_W) {
+#pragma unroll
+        for (int k = 0; k < RS_W; ++k)
+          if (k < n) acc += xw[ix * RS_W + k] * ld8(&vr[(lo + k) * cb + c]);
+      } else {
+        for (int k = 0; k < n; ++k)
+          acc += sep_w<COMP>(s1w, s2w, lo + k, w, ix) * ld8(&vr[(lo + k) * cb + c]);
+      }
+      st8(orow + (size_t)ix * C + c, acc);
+      if (RED) ra.add<T>(rp, as_stored8<T>(acc), ((size_t)b * h + iy) * w + ix, C, c0 + c);
+    }
+    // partial row b * h + iy (the B * h rows nsm_bnred_chunks reports)
+    if (RED) ra.write_slice(rp, cb8, c0, C, b * h + iy);
+  }
+}
+
+// channel slice of the separable kernels: the widest power-of-two multiple
+// of 8 channels dividing C (at most 256 groups) whose fp32 LDS rows (rows x
+// width x cb) fit `budget` bytes; -1 if 8 channels do not fit
+static int sep_lcb8(int C, int width, int rows = 1, size_t budget = 32768) {
+  int l = 0;
+  while ((8 << (l + 1)) <= C && C % (8 << (l + 1)) == 0 &&
+         (size_t)rows * width * (8 << (l + 1)) * 4 <= budget && (1 << (l + 1)) <= 256)
+    ++l;
+  if ((size_t)rows * width * (8 << l) * 4 > budget) return -1;
+  return l;
+}
+// the backward's rows per block and channel slice: 4 rows where a 32-channel
+// (fp32 128-B) slice still fits 48 KiB, else 2, else 1
+struct SepPlan {
+  int R, lcb8;
+};
+static int sep_rmax() {  // NSM_SEP_RMAX: cap on the rows per block (A/B)
+  static int v = [] {
+    const char* e = getenv("NSM_SEP_RMAX");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+static SepPlan sep_bwd_plan(int C, int tw) {
+  for (int R : {4, 2}) {
+    if (R > sep_rmax()) continue;
+    const int l = sep_lcb8(C, tw, R, 65536);
+    if (l >= 2 || (l >= 0 && (8 << l) == C)) return SepPlan{R, l};
+  }
+  return SepPlan{1, sep_lcb8(C, tw, 1, 65536)};
+}
+// dynamic LDS above the default 64 KiB (gfx950: 160 KiB per workgroup)
+template <typename K>
+static void allow_big_lds(K kernel) {
+  static const bool once = [&] {
+    (void)hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              120 * 1024);
+    return true;
+  }();
+  (void)once;
+}
+template <typename T, bool RED, bool COMP, int R>
+static void launch_sep_bwd(dim3 g, size_t lds, hipStream_t s, const void* dy, int h, int w, int C,
+                           int lcb8, void* dx, int th, int tw, float s1h, float s1w, float s2h,
+                           float s2w, const BnRedP& rp) {
+  auto k = resize_bwd_sep_kernel<T, RED, COMP, R>;
+  allow_big_lds(k);
+  hipLaunchKernelGGL(k, g, dim3(256), lds, s, (const T*)dy, h, w, C, lcb8, (T*)dx, th, tw, s1h,
+                     s1w, s2h, s2w, rp);
+}
+template <bool COMP>
+static void dispatch_sep_bwd(const SepPlan& pl, int B, size_t lds, hipStream_t s, const void* dy,
+                             int h, int w, int C, void* dx, int th, int tw, float s1h, float s1w,
+                             float s2h, float s2w, const BnRedP* rp, int dtype) {
+  const dim3 g((unsigned)(B * ((h + pl.R - 1) / pl.R)), (unsigned)(C >> (pl.lcb8 + 3)));
+  const BnRedP r = rp ? *rp : BnRedP{};
+#define NSM_SEP(T, RED, R)                                                                      \
+  launch_sep_bwd<T, RED, COMP, R>(g, lds, s, dy, h, w, C, pl.lcb8, dx, th, tw, s1h, s1w, s2h, s2w, r)
+#define NSM_SEP_R(T, RED) \
+  (pl.R == 4 ? NSM_SEP(T, RED, 4) : pl.R == 2 ? NSM_SEP(T, RED, 2) : NSM_SEP(T, RED, 1))
+  if (dtype == NSM_BF16) {
+    if (rp) NSM_SEP_R(bf16_t, true); else NSM_SEP_R(bf16_t, false);
+  } else {
+    if (rp) NSM_SEP_R(float, true); else NSM_SEP_R(float, false);
+  }
+#undef NSM_SEP_R
+#undef NSM_SEP
+}
+static bool sep_resize() {
+  static bool v = [] {
+    const char* e = getenv("NSM_RESIZE_SEP");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
 }
 
 // ---------------------------------------------------------------------------
@@ -1758,7 +2044,14 @@ static int resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, in
   if (C % 8 == 0 && tot8 < (1ll << 31)) {
     dim3 g(xcd_grid(tot8));
     const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(Wi), fh = make_fastdiv(Hi);
-    if (Wi <= U2_MAXW && (long long)B * Hi < (1ll << 31) && rows_resize()) {
+    const SepPlan pl = sep_bwd_plan(C, Wo);
+    const size_t slds = pl.lcb8 < 0 ? 0
+                                    : (size_t)pl.R * Wo * (8 << pl.lcb8) * 4 +
+                                          (size_t)Wi * (RS_W + 2) * 4;
+    if (sep_resize() && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * Hi < (1ll << 31)) {
+      dispatch_sep_bwd<false>(pl, B, slds, s, dy, Hi, Wi, C, dx, Ho, Wo, sh, sw, 0.f, 0.f, rp,
+                              dtype);
+    } else if (Wi <= U2_MAXW && (long long)B * Hi < (1ll << 31) && rows_resize()) {
       NSM_CHECK_ARG(!rp || 256 % (C / 8) == 0, "resize_bwd: fused BN reduction needs C/8 | 256");
       const size_t lds = (size_t)Wi * (RS_W + 2) * 4;
       const dim3 gr((unsigned)(B * Hi));
@@ -1837,7 +2130,19 @@ extern "C" int nsm_up2_resize_fwd_act(const void* y2, int B, int h, int w, int C
   segs = std::max(1ll, std::min({segs, 16ll, (per_row + 1023) / 1024}));
   const dim3 gr((unsigned)rows, (unsigned)segs);
   const ActSrc act{scale, shift, res, slope};
-  if (dtype == NSM_BF16)
+  const int lcb8 = sep_lcb8(C, w);
+  const size_t slds = lcb8 < 0 ? 0 : (size_t)w * (8 << lcb8) * 4 + (size_t)tw * 16;
+  if (sep_resize() && lcb8 >= 0 && slds <= 65536) {
+    const dim3 gs((unsigned)rows, (unsigned)(C / (8 << lcb8)));
+    if (dtype == NSM_BF16)
+      hipLaunchKernelGGL((up2_resize_fwd_sep_kernel<bf16_t, true>), gs, dim3(256), slds, s,
+                         NSM_CT(bf16_t, y2), h, w, C, lcb8, NSM_T(bf16_t, out), th, tw, a, b, c,
+                         d, act);
+    else
+      hipLaunchKernelGGL((up2_resize_fwd_sep_kernel<float, true>), gs, dim3(256), slds, s,
+                         NSM_CT(float, y2), h, w, C, lcb8, NSM_T(float, out), th, tw, a, b, c, d,
+                         act);
+  } else if (dtype == NSM_BF16)
     hipLaunchKernelGGL((up2_resize_fwd_rows_kernel<bf16_t, true>), gr, dim3(256), lds, s,
                        NSM_CT(bf16_t, y2), h, w, C / 8, f8, NSM_T(bf16_t, out), th, tw, a, b, c,
                        d, act);
@@ -1868,12 +2173,24 @@ extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, voi
     long long segs = (2048 + rows - 1) / rows;
     segs = std::max(1ll, std::min({segs, 16ll, (per_row + 1023) / 1024}));
     const dim3 gr((unsigned)rows, (unsigned)segs);
+    const int lcb8 = sep_lcb8(C, w);
+    const size_t slds = lcb8 < 0 ? 0 : (size_t)w * (8 << lcb8) * 4 + (size_t)tw * 16;
+    if (sep_resize() && lcb8 >= 0 && slds <= 65536) {
+      const dim3 gs((unsigned)rows, (unsigned)(C / (8 << lcb8)));
+#define A_(T) NSM_CT(T, x), h, w, C, lcb8, NSM_T(T, y), th, tw, a, b, c, d
+      if (dtype == NSM_BF16)
+        hipLaunchKernelGGL(up2_resize_fwd_sep_kernel<bf16_t>, gs, dim3(256), slds, s, A_(bf16_t));
+      else
+        hipLaunchKernelGGL(up2_resize_fwd_sep_kernel<float>, gs, dim3(256), slds, s, A_(float));
+#undef A_
+    } else {
 #define A_(T) NSM_CT(T, x), h, w, C / 8, f8, NSM_T(T, y), th, tw, a, b, c, d
     if (dtype == NSM_BF16)
       hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<bf16_t>, gr, dim3(256), lds, s, A_(bf16_t));
     else
       hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<float>, gr, dim3(256), lds, s, A_(float));
 #undef A_
+    }
   } else {
 #define A_(T) NSM_CT(T, x), h, w, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(T, y), th, tw, a, b, c, d
     NSM_DT(up2_resize_fwd8_kernel, A_);
@@ -1895,7 +2212,13 @@ static int up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, 
               d = ac_scale(2 * w, tw);
   const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(w), fh = make_fastdiv(h);
   const BnRedP r = rp ? *rp : BnRedP{};
-  if (w <= U2_MAXW && (long long)B * h < (1ll << 31)) {
+  const SepPlan pl = sep_bwd_plan(C, tw);
+  const size_t slds = pl.lcb8 < 0 ? 0
+                                  : (size_t)pl.R * tw * (8 << pl.lcb8) * 4 +
+                                        (size_t)w * (RS_W + 2) * 4;
+  if (sep_resize() && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * h < (1ll << 31)) {
+    dispatch_sep_bwd<true>(pl, B, slds, s, dy, h, w, C, dx, th, tw, a, b, c, d, rp, dtype);
+  } else if (w <= U2_MAXW && (long long)B * h < (1ll << 31)) {
     NSM_CHECK_ARG(!rp || 256 % (C / 8) == 0, "up2_resize_bwd: fused BN reduction needs C/8 | 256");
     const size_t lds = (size_t)w * (RS_W + 2) * 4;
     const dim3 gr((unsigned)(B * h));

@@ -363,6 +363,36 @@ def test_up2_resize_composite(ops, device, h, w, th, tw):
     assert (nchw(dx.cpu(), B, h, w) - x.grad).abs().max() <= 2e-5 * max(1, x.grad.abs().max().item())
 
 
+@pytest.mark.parametrize("kind,B,h,w,C", [("resize", 2, 32, 32, 128), ("resize", 1, 16, 24, 512),
+                                          ("resize", 1, 8, 8, 1024), ("up2", 2, 64, 64, 64),
+                                          ("up2", 1, 67, 120, 32), ("resize", 1, 270, 480, 16)])
+def test_resize_bwd_channel_slices(ops, device, kind, B, h, w, C):
+    """The separable backward (and the composite's separable forward) at the
+    decoder's channel counts (several channel slices per row, x windows from
+    LDS) against PyTorch-CPU fp32 autograd of the reference upsample (+ match
+    for the composite); fp32 like the reference, whose source-index rounding
+    the kernels reproduce."""
+    g = torch.Generator().manual_seed(h * C + w)
+    x = torch.randn(B, C, h, w, generator=g, requires_grad=True)
+    if kind == "resize":
+        th, tw = 2 * h, 2 * w
+        ref = F.interpolate(x, size=(th, tw), mode="bilinear", align_corners=True)
+    else:
+        th, tw = 2 * h - 1, 2 * w + 3
+        ref = F.interpolate(F.interpolate(x, size=(2 * h, 2 * w), mode="bilinear", align_corners=True),
+                            size=(th, tw), mode="bilinear", align_corners=True)
+    gy = torch.randn(B, C, th, tw, generator=g)
+    ref.backward(gy)
+    xd = nhwc(x.detach()).to(device)
+    y = ops.resize(xd, B, h, w, th, tw) if kind == "resize" else ops.up2_resize(xd, B, h, w, th, tw)
+    assert (nchw(y.cpu(), B, th, tw) - ref.detach()).abs().max().item() <= 1e-5
+    dyd = nhwc(gy).to(device)
+    dx = (ops.resize_bwd(dyd, B, h, w, th, tw) if kind == "resize"
+          else ops.up2_resize_bwd(dyd, B, h, w, th, tw))
+    err = (nchw(dx.cpu(), B, h, w) - x.grad).abs().max().item()
+    assert err <= 2e-5 * max(1.0, x.grad.abs().max().item()), err
+
+
 def test_resize_identity_bitwise(ops, device):
     x = torch.randn(3 * 7 * 9, 16, device=device)
     y = ops.resize(x, 3, 7, 9, 7, 9)
