@@ -1319,10 +1319,14 @@ static int sep_lcb8(int C, int width, int rows = 1, size_t budget = 32768) {
 struct SepPlan {
   int R, lcb8;
 };
-static int sep_rmax() {  // NSM_SEP_RMAX: cap on the rows per block (A/B)
+// NSM_SEP_RMAX: cap on the rows per block. 2 by measurement (tools/
+// elem_bench_f32.py, B=8 fp32): R = 2 vs 1 cuts the x2 backward 126 -> 110 us
+// (C=512), and R = 4 is no faster without the fused BN reduction and slower
+// with it (124 -> 145 us: four partial-row reductions per block)
+static int sep_rmax() {
   static int v = [] {
     const char* e = getenv("NSM_SEP_RMAX");
-    return e ? atoi(e) : 4;
+    return e ? atoi(e) : 2;
   }();
   return v;
 }
