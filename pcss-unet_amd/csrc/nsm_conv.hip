@@ -917,9 +917,18 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   for (int i = threadIdx.x; i < 64 * taps; i += 256) {
     int tap = i / 64, cl = i % 64;
     float s = 0.f;
-    if (cl < nci) {
+    if (cl < nci) {  // four splits' loads in flight (fixed order: deterministic)
       const float* src = ws + (size_t)co * N + tap * cin_p + ci0 + cl;
-      for (int k = 0; k < splits; ++k) s += src[k * MN];
+      float s1 = 0.f, s2 = 0.f, s3 = 0.f;
+      int k = 0;
+      for (; k + 3 < splits; k += 4) {
+        s += src[k * MN];
+        s1 += src[(k + 1) * MN];
+        s2 += src[(k + 2) * MN];
+        s3 += src[(k + 3) * MN];
+      }
+      for (; k < splits; ++k) s += src[k * MN];
+      s = (s + s1) + (s2 + s3);
     }
     tile[cl * taps + tap] = s;
   }

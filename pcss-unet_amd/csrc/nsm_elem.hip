@@ -208,9 +208,14 @@ __global__ void sum_rows_kernel(const float* __restrict__ part, int nrows, int w
   const int j = blockIdx.x * blockDim.x + threadIdx.x, g = blockIdx.y;
   if (j >= width) return;
   const int k0 = g * G, k1 = min(nrows, k0 + G);
-  double s = 0.0;
-  for (int k = k0; k < k1; ++k) s += part[(size_t)k * width + j];
-  out[(size_t)g * width + j] = (float)s;
+  double s = 0.0, s1 = 0.0;  // two rows' loads in flight, fixed order
+  int k = k0;
+  for (; k + 1 < k1; k += 2) {
+    s += part[(size_t)k * width + j];
+    s1 += part[(size_t)(k + 1) * width + j];
+  }
+  if (k < k1) s += part[(size_t)k * width + j];
+  out[(size_t)g * width + j] = (float)(s + s1);
 }
 
 __global__ void bn_finalize_eval_kernel(const float* __restrict__ rm, const float* __restrict__ rv,
