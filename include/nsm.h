@@ -156,6 +156,14 @@ int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int
  * [(tile+2)^2][T][c_p]); then nsm_conv3x3_wgrad_wino_dm takes dM instead of dy. */
 int nsm_wino_dual_input(const float* dy, int lddy, int B, int H, int W, int c_p, int tile,
                         float* V, float* dM, void* stream);
+/* As nsm_wino_dual_input, with dy not materialised: each element is the
+ * first BatchNorm's backward of g (grad wrt its LeakyReLU(+Dropout2d) output)
+ * and y (its input), exactly what nsm_bn_bwd_apply(g, y, ..., coef) would
+ * store (Unetmodel.py:21-24). */
+int nsm_wino_dual_input_bn(const float* g, int ldg, const float* y, int ldy, int B, int H, int W,
+                           int c_p, int tile, const float* scale, const float* shift, float slope,
+                           const float* mask, const float* mean, const float* coef, float* V,
+                           float* dM, void* stream);
 int nsm_conv3x3_wgrad_wino_dm(const float* dM, const float* V, int B, int H, int W, int cin_p,
                               int cout_p, int cin, int cout, int tile, float* dw, float* ws,
                               size_t ws_floats, void* stream);

@@ -1434,11 +1434,31 @@ __global__ void __launch_bounds__(256) wino_dout_kernel(const float* __restrict_
 // read of it: the (m+2)^2 patch of tile t gives V = B^T d B (the dgrad's input
 // transform, as wino_input) and its m x m interior gives dM = A^T-side
 // transform (as wino_dout). Saves a full read of dY per layer.
-template <int MT>
+// BN: dy is not materialised — each patch element is the first BatchNorm's
+// backward (Unetmodel.py:21-24) computed from its inputs, exactly as
+// nsm_bn_bwd_apply would have stored it: dz = g * lrelu'(y*scale+shift) *
+// mask[b][c], dy = k1*dz + k2*(y - mean) + k3 (coef of nsm_bn_bwd_finalize);
+// zero outside the image (the dgrad's padding). Saves writing dY1 and
+// reading it back (it has no other consumer on the Winograd path).
+struct WinoBnSrc {
+  const float* y;
+  int ldy;
+  const float* scale;
+  const float* shift;
+  const float* mean;
+  const float* coef;
+  const float* mask;  // [B][C] or null
+  float slope;
+};
+__device__ __forceinline__ float vlrelu_grad(float z, float s) { return lrelu_grad(z, s); }
+__device__ __forceinline__ f32x4 vlrelu_grad(f32x4 z, float s) { return lrelu_grad_v4(z, s); }
+
+template <int MT, bool BN = false>
 __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict__ dy, int ld, int H,
                                                         int W, int C, int TH, int TW, long long T,
                                                         float* __restrict__ V,
-                                                        float* __restrict__ dM) {
+                                                        float* __restrict__ dM,
+                                                        WinoBnSrc bn = WinoBnSrc{}) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int C4 = C / CW;
@@ -1452,15 +1472,37 @@ __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict_
     const int ty = (int)(r % TH);
     const long long b = r / TH;
     VT d[A][A];
+    VT sc{}, sh{}, mu{}, k1{}, k2{}, k3{}, mk{};
+    if constexpr (BN) {
+      sc = *(const VT*)(bn.scale + c);
+      sh = *(const VT*)(bn.shift + c);
+      mu = *(const VT*)(bn.mean + c);
+      k1 = *(const VT*)(bn.coef + c);
+      k2 = *(const VT*)(bn.coef + C + c);
+      k3 = *(const VT*)(bn.coef + 2 * C + c);
+      if (bn.mask) mk = *(const VT*)(bn.mask + (size_t)b * C + c);
+    }
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       const int yy = MT * ty - 1 + a;
 #pragma unroll
       for (int e = 0; e < A; ++e) {
         const int xx = MT * tx - 1 + e;
-        d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
-                      ? *(const VT*)(dy + ((size_t)(b * H + yy) * W + xx) * ld + c)
-                      : VT{};
+        const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const size_t p = (size_t)(b * H + yy) * W + xx;
+        if constexpr (BN) {
+          VT v{};
+          if (in) {
+            const VT gv = *(const VT*)(dy + p * ld + c);
+            const VT yv = *(const VT*)(bn.y + p * bn.ldy + c);
+            VT dz = gv * vlrelu_grad(yv * sc + sh, bn.slope);
+            if (bn.mask) dz = dz * mk;
+            v = k1 * dz + k2 * (yv - mu) + k3;
+          }
+          d[a][e] = v;
+        } else {
+          d[a][e] = in ? *(const VT*)(dy + p * ld + c) : VT{};
+        }
       }
     }
     const size_t plane = (size_t)T * C;
@@ -2119,6 +2161,28 @@ extern "C" int nsm_wino_dual_input(const float* dy, int lddy, int B, int H, int 
     hipLaunchKernelGGL(wino_dual_kernel<6>, grid, dim3(256), 0, s, dy, lddy, H, W, c_p, g.TH, g.TW,
                        g.T, V, dM);
   NSM_LAUNCH_CHECK("wino_dual_input");
+  return 0;
+}
+
+extern "C" int nsm_wino_dual_input_bn(const float* g, int ldg, const float* y, int ldy, int B,
+                                      int H, int W, int c_p, int tile, const float* scale,
+                                      const float* shift, float slope, const float* mask,
+                                      const float* mean, const float* coef, float* V, float* dM,
+                                      void* stream) {
+  NSM_CHECK_ARG(g && y && V && dM && scale && shift && mean && coef && c_p % 32 == 0 &&
+                    ldg % 4 == 0 && ldg >= c_p && ldy % 4 == 0 && ldy >= c_p,
+                "wino_dual_input_bn: bad args");
+  WinoGeom geo;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, geo), "wino_dual_input_bn: bad tile or shape");
+  dim3 grid(grid_1d(geo.T * c_p / (tile == 6 ? 1 : 4)));
+  hipStream_t s = as_stream(stream);
+  const WinoBnSrc bn{y, ldy, scale, shift, mean, coef, mask, slope};
+#define A_ g, ldg, H, W, c_p, geo.TH, geo.TW, geo.T, V, dM, bn
+  if (tile == 2) hipLaunchKernelGGL((wino_dual_kernel<2, true>), grid, dim3(256), 0, s, A_);
+  else if (tile == 4) hipLaunchKernelGGL((wino_dual_kernel<4, true>), grid, dim3(256), 0, s, A_);
+  else hipLaunchKernelGGL((wino_dual_kernel<6, true>), grid, dim3(256), 0, s, A_);
+#undef A_
+  NSM_LAUNCH_CHECK("wino_dual_input_bn");
   return 0;
 }
 

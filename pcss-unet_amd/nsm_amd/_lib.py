@@ -55,6 +55,7 @@ _SIGS = {
     "nsm_up2_resize_fwd_act": (I, [P, I, I, I, I, P, I, I, P, P, F, P, I, P]),
     "nsm_bn_act_pool": (I, [P, I, I, I, I, P, P, F, P, P, I, P]),
     "nsm_wino_dual_input": (I, [P, I, I, I, I, I, I, P, P, P]),
+    "nsm_wino_dual_input_bn": (I, [P, I, P, I, I, I, I, I, I, P, P, F, P, P, P, P, P, P]),
     "nsm_conv3x3_wgrad_wino_dm": (I, [P, P, I, I, I, I, I, I, I, I, P, P, Z, P]),
     "nsm_conv_fwd_act": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, F, P, I, I, P]),
     "nsm_wino_output_act": (I, [P, I, I, I, I, I, P, P, I, P, P, F, P, I, P]),

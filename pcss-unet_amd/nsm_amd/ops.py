@@ -248,6 +248,30 @@ def wino_dual_input(dy, B, H, W, tile=4):
     return Vd, dM
 
 
+class DeferredBnBwd:
+    """dY of a train-mode BN backward whose last pass (nsm_bn_bwd_apply) was
+    not run: g (grad wrt lrelu(BN(y))*mask) and the finalize coefficients.
+    Consumed by wino_dual_input_bn, which forms dY per element on the fly."""
+    __slots__ = ("g", "coef", "shape", "device", "dtype")
+
+    def __init__(self, g, coef):
+        self.g, self.coef = g, coef
+        self.shape, self.device, self.dtype = g.shape, g.device, g.dtype
+
+
+def wino_dual_input_bn(d, y, st, mask, B, H, W, tile=4, slope=0.2):
+    """wino_dual_input of the BN backward d = DeferredBnBwd(g, coef) of BN
+    input y (state st, Dropout2d mask [B][C] or None): dY is never stored."""
+    c_p = y.shape[1]
+    n = (tile + 2) ** 2 * wino_tiles(B, H, W, tile) * c_p
+    Vd = empty(n, device=y.device)
+    dM = empty(n, device=y.device)
+    call("nsm_wino_dual_input_bn", ptr(d.g), d.g.stride(0), ptr(y), y.stride(0), B, H, W, c_p,
+         tile, ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(d.coef),
+         ptr(Vd), ptr(dM), stream())
+    return Vd, dM
+
+
 def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, dM=None):
     """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino, same tile).
     dM: dy's transform from wino_dual_input (dy is then not read)."""
@@ -398,11 +422,13 @@ def bn_act(y, st, slope=0.2, res=None, out=None, mask=None, HW=0):
     return o
 
 
-def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, part=None):
+def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, part=None,
+           defer=False):
     """Backward through lrelu(.)*mask after a train-mode BN: returns dy
     (grad wrt the BN input) and writes dgamma/dbeta/dbias_prev (real chans).
     part=(partial, nchunk): the {sum dz, sum dz*xhat} partials already written
-    by g's producer (GradPart), so the reduce pass is skipped."""
+    by g's producer (GradPart), so the reduce pass is skipped. defer=True:
+    DeferredBnBwd(g, coef) instead of dy (its consumer forms dy itself)."""
     M, C = y.shape
     assert g.dtype == y.dtype
     if part is None:
@@ -422,6 +448,8 @@ def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, par
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
          ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
+    if defer:
+        return DeferredBnBwd(g, coef)
     dy = like(M, C, y)
     call("nsm_bn_bwd_apply", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
          ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy), dy.stride(0), dt(y),
@@ -433,14 +461,15 @@ SUM_ROWS_ABOVE = 512  # BN-backward partial rows beyond which nsm_sum_rows merge
 
 
 def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
-                         recompute, slope=0.2, tag=None):
+                         recompute, slope=0.2, tag=None, defer=False):
     """dY1 of a DoubleConv's first BN from dY2 (grad wrt the 1x1 conv output):
     the 1x1 input gradient dA1 = dY2 W2 with the BN + LeakyReLU + Dropout2d
     backward in its epilogue (nsm_conv1x1_dgrad_bnbwd) — the same values as
     bn_bwd(conv_fwd(dY2, w2d, ...), y, ...) without the separate reduce pass.
     recompute=True: a partials-only GEMM pass, then the GEMM again writing dY1
     (dA1 never stored); False: one pass storing dA1 + partials, then
-    nsm_bn_bwd_apply."""
+    nsm_bn_bwd_apply. defer=True (with recompute=False): DeferredBnBwd(dA1,
+    coef) instead of dy, the apply pass left to the consumer."""
     from ._lib import lib
     M, cop = dY2.shape
     C = y.shape[1]
@@ -464,6 +493,10 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
          ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
+    if defer and not recompute:
+        if ev is not None:
+            ev.record()
+        return DeferredBnBwd(dA1, coef)
     dy = like(M, C, y)
     if recompute:
         call("nsm_conv1x1_dgrad_bnbwd", *args, 2, None, ptr(coef), ptr(dy), dy.stride(0), dtc,

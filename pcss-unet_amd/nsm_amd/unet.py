@@ -48,6 +48,13 @@ LAZY_DECODER = os.environ.get("NSM_LAZY_DECODER", "0") != "0"
 # NSM_DUAL_WINO=0: the Winograd dgrad and wgrad transform the output gradient
 # in two separate reads of it instead of one (nsm_wino_dual_input)
 DUAL_TRANSFORM = os.environ.get("NSM_DUAL_WINO", "1") != "0"
+# NSM_LAZY_DY1=1: the dual transform forms dY1 per element from dA1 and Y1
+# (nsm_wino_dual_input_bn) instead of reading the dY1 nsm_bn_bwd_apply stored.
+# Off: it saves the dY1 round trip but the F(6x6) kernel then issues 128
+# loads per thread (two tensors over the overlapping 8x8 patches) and became
+# issue-bound — conv7 apply 152 + dual 250 us -> fused 484 us, conv6 210 ->
+# 260 us (only conv3 gained, 56 -> 48 us).
+LAZY_DY1 = os.environ.get("NSM_LAZY_DY1", "0") != "0"
 # NSM_EVAL_FUSED=0: eval forward with separate BN-apply passes instead of the
 # BN + LeakyReLU (+ skip) in the conv epilogues (nsm_conv_fwd_act)
 EVAL_FUSED = os.environ.get("NSM_EVAL_FUSED", "1") != "0"
@@ -539,21 +546,27 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
                        pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
     mode = bnb_mode(s.cip, s.cop, dtype)
+    # dY1 is consumed only by its two Winograd transforms: leave the BN apply
+    # to the dual transform kernel, dY1 is never stored
+    lazy = s.V is not None and need_dx and DUAL_TRANSFORM and LAZY_DY1
     if mode:
         dY1 = ops.conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
                                        g[bn1m.bias], g[c0.bias], mode == 2,
-                                       tag=name + ".conv.4.dgrad")
+                                       tag=name + ".conv.4.dgrad", defer=lazy)
     else:
         dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
         dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias],
-                         g[c0.bias])
+                         g[c0.bias], defer=lazy)
     Vd = None
     if s.V is not None:
         tile = wino_tile(s.cip, H, W)
         dM = None
         if need_dx and DUAL_TRANSFORM:
             # dY1's two Winograd transforms (dgrad input, wgrad) from one read
-            Vd, dM = ops.wino_dual_input(dY1, B, H, W, tile=tile)
+            if isinstance(dY1, ops.DeferredBnBwd):
+                Vd, dM = ops.wino_dual_input_bn(dY1, s.Y1, s.bn1, s.mask, B, H, W, tile=tile)
+            else:
+                Vd, dM = ops.wino_dual_input(dY1, B, H, W, tile=tile)
         ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=tile,
                                tag=name + ".conv.0.wgrad", dM=dM)
         s.V = None

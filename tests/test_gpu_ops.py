@@ -528,6 +528,35 @@ def test_grad_producer_bn_reduce(ops, device, kind, B, h, w, C, dtype):
 
 
 @pytest.mark.parametrize("tile", [2, 4, 6])
+@pytest.mark.parametrize("B,H,W,C,drop", [(2, 9, 11, 32, True), (1, 16, 16, 128, False),
+                                         (2, 37, 29, 64, True)])
+def test_wino_dual_input_bn(ops, device, B, H, W, C, drop, tile):
+    """nsm_wino_dual_input_bn (the first BN's backward formed per element
+    inside the dual transform, dY1 never stored) == bn_bwd then
+    wino_dual_input, and dgamma / dbeta / dbias identical."""
+    g = torch.Generator().manual_seed(H * W + C + tile)
+    y = (torch.randn(B * H * W, C, generator=g) * 1.3 + 0.4).to(device)
+    gr = torch.randn(B * H * W, C, generator=g).to(device)
+    mask = ((torch.rand(B, C, generator=g) > 0.2).float() / 0.8).to(device) if drop else None
+    bn = torch.nn.BatchNorm2d(C).to(device)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.2, 0.2)
+    st = ops.bn_train(y, bn, C, 0.1, 1e-5)
+    outs = []
+    for defer in (False, True):
+        dg, db, dbias = (torch.empty(C, device=device) for _ in range(3))
+        d = ops.bn_bwd(gr, y, st, H * W, mask, C, dg, db, dbias, defer=defer)
+        Vd, dM = (ops.wino_dual_input_bn(d, y, st, mask, B, H, W, tile=tile) if defer
+                  else ops.wino_dual_input(d, B, H, W, tile=tile))
+        outs.append((Vd.cpu(), dM.cpu(), dg.cpu(), db.cpu(), dbias.cpu()))
+    for a, b in zip(outs[0][:2], outs[1][:2]):
+        assert rel(b, a) <= 1e-6
+    for a, b in zip(outs[0][2:], outs[1][2:]):
+        assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("tile", [2, 4, 6])
 @pytest.mark.parametrize("B,H,W,ci,co", [(2, 9, 11, 32, 64), (1, 16, 16, 128, 128), (2, 37, 29, 64, 32)])
 def test_wino_dual_input(ops, device, B, H, W, ci, co, tile):
     """nsm_wino_dual_input: both transforms of dy from one read == the separate
