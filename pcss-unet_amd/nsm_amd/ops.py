@@ -4,6 +4,8 @@ Activations are NHWC fp32 2-D views `[pixels, channels_padded]`; every
 wrapper allocates its outputs with the PyTorch caching allocator and launches
 on the current HIP stream. No host synchronisation anywhere.
 """
+import os
+
 import torch
 
 from ._lib import call, ptr, stream
@@ -347,7 +349,7 @@ def bn_partials(y):
     return part
 
 
-MERGE_ABOVE = 1024  # partial chunks beyond which a parallel first-level merge runs
+MERGE_ABOVE = int(os.environ.get("NSM_MERGE_ABOVE", "1024"))  # partial chunks beyond which a parallel first-level merge runs
 
 
 def merged(part, M, C):
@@ -457,7 +459,7 @@ def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, par
     return dy
 
 
-SUM_ROWS_ABOVE = 512  # BN-backward partial rows beyond which nsm_sum_rows merges them first
+SUM_ROWS_ABOVE = int(os.environ.get("NSM_SUM_ROWS_ABOVE", "512"))  # BN-backward partial rows beyond which nsm_sum_rows merges them first
 
 
 def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
