@@ -797,11 +797,26 @@ static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const typename 
 }
 
 // BM chosen by dispatch_conv_fwd (rows per BN-stat partial)
+// 256-row tiles (4 waves of 64x32: 0.75 fragment reads per MFMA instead of
+// 1) for the 32-channel fp32 convs with >= 2048 of them (conv2 at 256^2):
+// conv2.0 fwd 127 -> 112 us, its dgrad 117 -> 101 us (NSM_N32_BM256=0: 128)
+static bool n32_bm256() {
+  static bool v = [] {
+    const char* e = getenv("NSM_N32_BM256");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
 static int conv_fwd_bm(long long M, int N) {
   long long mb128 = ceil_div(M, 128);
   if (N >= 128) return mb128 * ceil_div(N, 128) >= 512 ? 128 : 64;
   if (N >= 64) return mb128 * ceil_div(N, 64) >= 512 ? 128 : 64;
   return mb128 >= 512 ? 128 : 64;
+}
+// rows per BN-partial row of the fp32 direct-conv dispatch (dispatch_conv_fwd)
+static int conv_fwd_bm_f(long long M, int N) {
+  if (N < 64 && n32_bm256() && ceil_div(M, 128) >= 4096) return 256;
+  return conv_fwd_bm(M, N);
 }
 
 template <bool PRO, class EP = EpiStore>
@@ -821,6 +836,8 @@ static int dispatch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const typenam
       return launch_conv_fwd<128, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
     return launch_conv_fwd<64, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
   }
+  if (n32_bm256() && mb128 >= 4096)
+    return launch_conv_fwd<256, 32, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
   if (mb128 >= 512) return launch_conv_fwd<128, 32, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
   return launch_conv_fwd<64, 32, 2, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
 }
@@ -1742,7 +1759,7 @@ extern "C" int nsm_conv_fwd(const float* x, int ldx, int B, int H, int W, int ci
 
 extern "C" int nsm_conv_stat_rows(int B, int H, int W, int cout_p) {
   long long M = (long long)B * H * W;
-  return conv_fwd_bm(M, cout_p);
+  return conv_fwd_bm_f(M, cout_p);
 }
 
 extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, int cin_p,
