@@ -807,6 +807,16 @@ static bool n32_bm256() {
   }();
   return v;
 }
+// 256x64 tiles (4 waves of 64x64) for the 64-channel fp32 convs with >= 2048
+// of them (conv2.4, conv8.4 at 256^2 and their input gradients): 118.5 ->
+// 101.9, 78 -> 66-70, 59 -> 55 us per launch (NSM_N64_BM256=0: 128x64)
+static bool n64_bm256() {
+  static bool v = [] {
+    const char* e = getenv("NSM_N64_BM256");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
 static int conv_fwd_bm(long long M, int N) {
   long long mb128 = ceil_div(M, 128);
   if (N >= 128) return mb128 * ceil_div(N, 128) >= 512 ? 128 : 64;
@@ -816,6 +826,7 @@ static int conv_fwd_bm(long long M, int N) {
 // rows per BN-partial row of the fp32 direct-conv dispatch (dispatch_conv_fwd)
 static int conv_fwd_bm_f(long long M, int N) {
   if (N < 64 && n32_bm256() && ceil_div(M, 128) >= 4096) return 256;
+  if (N == 64 && n64_bm256() && ceil_div(M, 128) >= 4096) return 256;
   return conv_fwd_bm(M, N);
 }
 
@@ -832,6 +843,8 @@ static int dispatch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const typenam
     return launch_conv_fwd<64, 128, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
   }
   if (N >= 64) {
+    if (n64_bm256() && mb128 >= 4096 && N == 64)
+      return launch_conv_fwd<256, 64, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
     if (mb128 * ceil_div(N, 64) >= 512)
       return launch_conv_fwd<128, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
     return launch_conv_fwd<64, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
