@@ -1973,6 +1973,16 @@ extern "C" int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int 
   return nsm_wino_input_resize(x, ldx, B, H, W, H, W, cin_p, tile, relu, V, stream);
 }
 
+// 256x64 tiles for the 64-channel Winograd GEMMs (conv9 at 256^2: fwd 122 ->
+// 109 us, dgrad 116 -> 105 us); NSM_WINO_N64_BM256=0: 128x64
+static bool wino_n64_bm256() {
+  static bool v = [] {
+    const char* e = getenv("NSM_WINO_N64_BM256");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p,
                              int cout_p, int tile, float* Mb, void* stream) {
   NSM_CHECK_ARG(V && U && Mb && cin_p % 32 == 0 && cout_p % 32 == 0, "wino_gemm: bad args");
@@ -1991,7 +2001,12 @@ extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W
     return (mb128 * ceil_div(N, 128) * nb >= (f32_split() ? 512 : 1024))
                ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s)
                : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s);
-  if (N >= 64) return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, nb, s);
+  if (N >= 64) {
+    // 256x64 (4 waves of 64x64) where the batched grid still has >= 2048 blocks
+    if (N == 64 && wino_n64_bm256() && f32_split() && ceil_div(M, 256) * nb >= 2048)
+      return launch_wino_gemm<256, 64, 4, 1>(ap, bp, ep, M, N, K, nb, s);
+    return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, nb, s);
+  }
   return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, nb, s);
 }
 
