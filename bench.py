@@ -114,32 +114,61 @@ def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=128, tile=4, passes=3):
     return out
 
 
-def stage_table(work, times_ms, peak=FP32_PEAK_TFLOPS):
+STAGE_COLS = ["stage", "ms", "alg_tflops", "mfma_frac", "hbm_frac", "meas_gbs", "meas_hbm_frac",
+              "meas_over_alg", "mfma_busy", "meas_mfma_frac"]
+
+
+def stage_table(work, times_ms, pipe_mult, peak, measured=None):
+    """Per-stage rows (STAGE_COLS): live time (HIP events), algorithmic
+    (direct-conv) TFLOP/s, `mfma_frac` = the matrix-core work the stage issues
+    on the pipe that runs it (fp32 split: pipe_mult = 6 bf16 products per fp32
+    product) / time / that pipe's dense peak, `hbm_frac` = algorithmic bytes /
+    time / 8 TB/s; with a committed PMC summary (tools/stage_pmc.py) of the same
+    configuration: measured HBM bytes (TCC fabric requests + WRITE_SIZE) / live
+    time, their ratio to the algorithmic bytes, MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES
+    per SIMD-cycle at the held clock) and the counted MFMA work (512 x
+    SQ_INSTS_VALU_MFMA_MOPS_*) / live time / peak."""
     rows = []
+    ms_ = (measured or {}).get("stages", {})
     for st in STAGES:
         if st not in times_ms:
             continue
-        t_ms = times_ms[st]
+        t = times_ms[st] * 1e-3
         fl, ex, by = work[st]
-        tf = fl / (t_ms * 1e-3) / 1e12
-        mf = ex / (t_ms * 1e-3) / 1e12
-        gbs = by / (t_ms * 1e-3) / 1e9
-        ai = ex / by
-        rows.append({"stage": st, "ms": round(float(t_ms), 3), "tflops": round(tf, 2),
-                     "mfma_tflops": round(mf, 2),
-                     "mfma_frac": round(mf / peak, 3), "gbs": round(gbs, 1),
-                     "hbm_frac": round(gbs / HBM_PEAK_GBS, 3), "flop_per_byte": round(ai, 1),
-                     "bound": "mfma" if ai > peak * 1e12 / (HBM_PEAK_GBS * 1e9) else "hbm"})
+        m = ms_.get(st, {})
+        mb = m.get("hbm_bytes")
+        mf = None
+        if "bf16_mfma_flops" in m:
+            mf = (m["bf16_mfma_flops"] / (BF16_PEAK_TFLOPS * 1e12)
+                  + m.get("f32_mfma_flops", 0.0) / (FP32_PEAK_TFLOPS * 1e12)) / t
+        rows.append([st, round(t * 1e3, 3), round(fl / t / 1e12, 1),
+                     round(pipe_mult * ex / t / (peak * 1e12), 3),
+                     round(by / t / (HBM_PEAK_GBS * 1e9), 3),
+                     round(mb / t / 1e9) if mb else None,
+                     round(mb / t / (HBM_PEAK_GBS * 1e9), 3) if mb else None,
+                     round(mb / by, 2) if mb else None,
+                     m.get("mfma_busy"), round(mf, 3) if mf is not None else None])
     return rows
+
+
+def load_stage_pmc(tag):
+    """The newest committed per-stage PMC summary of this configuration."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"stage_pmc_{tag}.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        return json.load(f), os.path.relpath(files[-1], ROOT)
 
 
 def mean_ms(evs):
     return float(np.mean([a.elapsed_time(b) for a, b in evs])) if evs else float("nan")
 
 
-def load_traffic(name="traffic_wino_gemm_conv6.json"):
+def load_traffic(name):
     """HBM bytes per launch of the dominant kernel from the committed rocprofv3
-    PMC summary (FETCH_SIZE x2 per the gfx950 calibration + WRITE_SIZE)."""
+    PMC summary (tools/pmc_traffic.py: sized TCC fabric read requests +
+    WRITE_SIZE)."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)))
     if not files:
@@ -149,14 +178,19 @@ def load_traffic(name="traffic_wino_gemm_conv6.json"):
     return t.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
 
 
-def cpu_baseline(in_ch, H, W, frames=4, reps=5, train=True):
-    """Oracle restatement (same ATen ops as the reference) fp32 on the host
-    cores: frames/s of the train step (fwd+L1+bwd) or of the eval forward
-    (infer.py's per-frame work), on a bounded sample (`frames` x `reps`)."""
+def cpu_baseline(in_ch, H, W, frames=8, reps=3, train=True, bf16_autocast=False):
+    """The reference's CPU path timed on this box's host cores: the oracle
+    restatement (same ATen ops as Unetmodel.py) on a bounded sample (`frames`
+    frames, median of `reps` after one warmup). train: fwd + 0.9*L1 + bwd at
+    the headline batch (B=8); else the eval forward under inference_mode, with
+    bf16_autocast = infer.py's CPU mode (`torch.amp.autocast('cpu',
+    dtype=torch.bfloat16)`, infer.py:63-65).
+    Threads: the CPU share the GPU box grants this job (OMP_NUM_THREADS = 16
+    per GPU); os.sched_getaffinity lists the whole host's cores there
+    (`affinity_cores`), which other jobs' GPUs share."""
     from oracle import unet_ref as O
     from oracle.weights import make_state, synthetic_batch
     cores = len(os.sched_getaffinity(0))
-    # the box grants this job a CPU share (OMP_NUM_THREADS, 16 per GPU); use it
     share = int(os.environ.get("OMP_NUM_THREADS", cores))
     torch.set_num_threads(max(1, min(cores, share)))
     sd = O.torch_state(make_state(in_ch, 42), requires_grad=train)
@@ -169,7 +203,8 @@ def cpu_baseline(in_ch, H, W, frames=4, reps=5, train=True):
             out, _ = O.forward(sd, x, True, None, 0.0)
             O.custom_loss(out, y, 0.9).backward()
         else:
-            with torch.no_grad():
+            with torch.inference_mode(), torch.amp.autocast("cpu", dtype=torch.bfloat16,
+                                                            enabled=bf16_autocast):
                 O.forward(sd, torch.from_numpy(x_np), False)
 
     step()
@@ -179,22 +214,28 @@ def cpu_baseline(in_ch, H, W, frames=4, reps=5, train=True):
         step()
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
-    what = "train step (fwd+L1+bwd)" if train else "eval forward (no_grad)"
-    return {"value": frames / t, "unit": "frames/s", "cores": torch.get_num_threads(),
+    what = ("train step (fwd+0.9*L1+bwd) fp32" if train else
+            "eval forward, inference_mode + bf16 autocast (infer.py:63-65 CPU mode)"
+            if bf16_autocast else "eval forward, inference_mode, fp32")
+    return {"value": round(frames / t, 4), "unit": "frames/s", "cores": torch.get_num_threads(),
             "affinity_cores": cores, "kind": "port",
-            "sample": f"{frames} frame(s) {in_ch}x{H}x{W} fp32 {what}, "
-                      f"oracle/unet_ref.py on PyTorch CPU, median of {reps} after 1 warmup, "
-                      f"{ts and round(sum(ts), 2)} s timed"}
+            "cores_policy": "the box's CPU share per GPU (OMP_NUM_THREADS); affinity spans the "
+                            "whole shared host",
+            "sample": f"{frames} frame(s) {in_ch}x{H}x{W} {what}, oracle/unet_ref.py on PyTorch "
+                      f"CPU, median of {reps} after 1 warmup, {round(sum(ts), 2)} s timed"}
 
 
 def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
-    """Roofline object of conv6.conv.0's forward, the largest convolution of the
-    step, timed as a whole (Winograd input transform + batched MFMA GEMM +
-    output transform, HIP events on the launch stream). `achieved`/`frac` are
-    on SURVEY.md §8(d)'s algorithmic basis (direct-convolution FLOPs
-    2*B*h*w*Cin*Cout*9): F(4x4,3x3) issues 4x fewer MFMA products, so frac can
-    exceed 1. `executed_frac` prices the MFMA work actually issued (36 GEMMs of
-    T x 1024 x 1024) against the fp32 MFMA peak; `gemm` is the GEMM launch alone."""
+    """Roofline object of the step's dominant kernel: conv6.conv.0's forward
+    Winograd batched GEMM (nsm_wino_gemm, (m+2)^2 GEMMs of T x 1024 x 1024),
+    timed per launch with HIP events on its stream. Priced on the pipe that
+    runs it: with the exact 3-way split (default) every fp32 product is 6 bf16
+    MFMA products, so achieved = 6 x 2*(m+2)^2*T*1024^2 / launch time against
+    the dense bf16 peak (frac <= 1); NSM_F32_SPLIT=0 runs the fp32 MFMA (one
+    product each, fp32 peak). `whole_conv` adds the two Winograd transforms
+    (input + output): its time, the same work / that time, and SURVEY.md
+    §8(d)'s direct-convolution FLOPs / that time (`direct_equiv_tflops`, a
+    rate, not a roofline position: Winograd issues 5x fewer products)."""
     Rh, Rw = H // 2, W // 2
     m, nb = wino_tile, (wino_tile + 2) ** 2
     h6, w6 = Rh // 4, Rw // 4                     # conv6 runs at (H/8, W/8)
@@ -203,29 +244,27 @@ def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
     alg_bytes = (2 * B * h6 * w6 * 1024 + 9 * 1024 * 1024 + 1024) * 4
     ex_flops = nb * 2.0 * T6 * 1024 * 1024
     gemm_bytes = nb * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
-    achieved = alg_flops / (conv_ms * 1e-3) / 1e12
-    ex = ex_flops / (conv_ms * 1e-3) / 1e12
-    gx = ex_flops / (gemm_ms * 1e-3) / 1e12
     split = os.environ.get("NSM_F32_SPLIT", "1") != "0"
-    arith = {"f32_gemm": "exact 3-way bf16 split, 6 products on v_mfma_f32_32x32x16_bf16, fp32 "
-                         "accumulate (csrc/nsm_conv_split.inc)" if split else
-                         "v_mfma_f32_32x32x2_f32",
-             # the matrix-core work the split issues: 6 bf16 products per fp32 product
-             "bf16_mfma_flops_per_launch": 6 * ex_flops if split else None,
-             "gemm_bf16_mfma_frac": round(6 * gx / BF16_PEAK_TFLOPS, 4) if split else None}
-    return {"kernel": f"conv6.conv.0.fwd 3x3 1024->1024 at {h6}x{w6}, B={B}: Winograd F({m}x{m},3x3) "
-                      f"= nsm_wino_input + nsm_wino_gemm ({nb} x M={T6} N=1024 K=1024) + "
-                      "nsm_wino_output",
-            "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(achieved / FP32_PEAK_TFLOPS, 4),
-            "basis": "SURVEY.md §8(d) algorithmic (direct-conv) FLOPs per launch / whole-conv time",
-            "executed_tflops": round(ex, 2), "executed_frac": round(ex / FP32_PEAK_TFLOPS, 4),
-            "avg_launch_ms": round(conv_ms, 4), "launches": launches,
-            "algorithmic_flops_per_launch": alg_flops, "algorithmic_bytes_per_launch": alg_bytes,
-            "executed_flops_per_launch": ex_flops,
-            "gemm": {"avg_launch_ms": round(gemm_ms, 4), "executed_tflops": round(gx, 2),
-                     "executed_frac": round(gx / FP32_PEAK_TFLOPS, 4),
-                     "bytes_per_launch": gemm_bytes, **arith}}
+    mult, peak = (6, BF16_PEAK_TFLOPS) if split else (1, FP32_PEAK_TFLOPS)
+    work = mult * ex_flops
+    achieved = work / (gemm_ms * 1e-3) / 1e12
+    return {"kernel": f"conv6.conv.0.fwd Winograd F({m}x{m},3x3) batched GEMM nsm_wino_gemm "
+                      f"({nb} x M={T6} N=1024 K=1024), B={B} at {h6}x{w6}: "
+                      + ("gemm_f32s_kernel (fp32 via the exact 3-way bf16 split, 6 products on "
+                         "v_mfma_f32_32x32x16_bf16)" if split else "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)"),
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4),
+            "basis": (f"matrix-core work issued per launch on the pipe that runs it ({mult} x "
+                      f"{ex_flops / 1e9:.1f} GFLOP of fp32 products) / launch time / that pipe's "
+                      "dense peak"),
+            "avg_launch_ms": round(gemm_ms, 4), "launches": launches,
+            "flops_per_launch": work, "fp32_product_flops_per_launch": ex_flops,
+            "algorithmic_bytes_per_launch": gemm_bytes,
+            "whole_conv": {"what": "nsm_wino_input + nsm_wino_gemm + nsm_wino_output",
+                           "avg_ms": round(conv_ms, 4),
+                           "pipe_frac": round(work / (conv_ms * 1e-3) / 1e12 / peak, 4),
+                           "direct_equiv_tflops": round(alg_flops / (conv_ms * 1e-3) / 1e12, 1),
+                           "direct_conv_flops": alg_flops, "direct_conv_bytes": alg_bytes}}
 
 
 def direct_roofline(B, H, W, kern_ms, launches):
@@ -302,12 +341,25 @@ def run_dry(args):
     for _ in range(args.warmup):
         step()
     elapsed = timed(step, args.steps, world, dev)
+    # the workloads a real run at this N measures (train: headline + secondary)
+    plan = [{"config": "configs[1]", "role": "headline", "batch_per_gpu": args.batch,
+             "global_batch": world * args.batch, "dtype": args.dtype}]
+    if not args.no_secondary:
+        plan.append({"config": "configs[3]" if world > 1 else "configs[2] (= configs[3] at N=1)",
+                     "role": "secondary", "batch_per_gpu": 64, "global_batch": world * 64,
+                     "dtype": "bf16"})
+        if world == 1:
+            plan += [{"config": "configs[4]", "role": "secondary", "batch_per_gpu": 1,
+                      "dtype": d} for d in ("bf16", "f32")]
+            plan.append({"config": "configs[0]", "role": "secondary", "batch_per_gpu": 1,
+                         "dtype": "f32"})
     if rank == 0:
         print(json.dumps({"metric": "dry-run (launcher check, not a measurement)", "value": 0.0,
                           "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
                           "dry_run": True, "world_size": world,
-                          "backend": dist.get_backend() if world > 1 else None}), flush=True)
+                          "backend": dist.get_backend() if world > 1 else None,
+                          "workloads": plan}), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -316,50 +368,79 @@ def run_dry(args):
 def run_train(args):
     world, rank, dev = init_dist(args)
     res = train_measure(args, world, rank, dev)
-    if rank == 0 and world == 1 and not args.no_secondary:
-        res["secondary"] = secondary_configs(args, world, rank, dev)
+    if not args.no_secondary:
+        sec = secondary_configs(args, world, rank, dev)
+        if rank == 0:
+            res["secondary"] = sec
     C, H, W = args.in_ch, args.res, args.res
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(C, H, W)
+        res["cpu_baseline"] = cpu_baseline(C, H, W, frames=args.batch)
         if args.dtype == "bf16":
             res["cpu_baseline"]["sample"] += " (fp32: the reference's CPU path)"
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res, args)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
 
 
+def emit(res, args):
+    """The ONE JSON line (compact: the driver keeps its last 2000 characters,
+    so the secondary configs and the CPU baseline come last) and, with
+    --detail PATH, the full record as a file."""
+    if args.detail:
+        with open(args.detail, "w") as f:
+            json.dump(res, f, indent=1)
+    out = {k: v for k, v in res.items() if k not in ("secondary", "cpu_baseline", "_full")}
+    if "secondary" in res:
+        out["secondary"] = res["secondary"]
+    if "cpu_baseline" in res:
+        out["cpu_baseline"] = res["cpu_baseline"]
+    print(json.dumps(out, separators=(",", ":")), flush=True)
+
+
 def _summary(r):
-    """The fields of a secondary measurement kept in the headline JSON line."""
+    """A secondary measurement as kept in the headline JSON line."""
     roof = r["roofline"]
-    return {"metric": r["metric"], "value": r["value"], "unit": r["unit"],
-            "ms_per_step": r["ms_per_step"], "steps": r["steps"], "warmup": r["warmup"],
-            "dtype": r["dtype"], "config": r["config"],
-            "model_tflops_per_s": r["model_tflops_per_s"],
-            "roofline": {k: roof.get(k) for k in ("kernel", "bound", "achieved", "peak", "unit",
-                                                  "frac", "executed_frac", "avg_launch_ms",
-                                                  "traffic", "traffic_source")},
-            "stages": r["stages"]}
+    out = {"config": r["config"]["workload"].split(":")[0], "dtype": r["dtype"],
+           "global_batch": r["config"]["global_batch"], "value": r["value"], "unit": r["unit"],
+           "ms_per_step": r["ms_per_step"], "steps": r["steps"],
+           "roofline": {k: roof.get(k) for k in ("achieved", "frac", "avg_launch_ms", "traffic")}}
+    if "dp" in r:
+        out["dp"] = r["dp"]
+    if r["config"]["workload"].startswith(("configs[2]", "configs[3]")):
+        out["stages"] = r["stages"]
+    if "cpu_baseline" in r:
+        out["cpu_baseline"] = r["cpu_baseline"]
+    return out
 
 
 def secondary_configs(args, world, rank, dev):
     """The other BASELINE.json configs measured in the same run (so the
-    driver's record carries them): configs[2] (B=64 bf16 train step, the
-    per-GPU share of configs[3]'s batch 512 on 8 GPUs), configs[4] (1080p
-    hipGraph inference, fp32 and bf16) and configs[0] (1x7x256x256 eval)."""
+    driver's record carries them). Every N: configs[3]'s per-GPU work (B=64
+    bf16 train step per GPU: global batch 512 at N=8; at N=1 this is
+    configs[2]). N=1 also: configs[4] (1080p hipGraph inference, bf16 and fp32,
+    each beside the reference's CPU infer.py timing of the same mode) and
+    configs[0] (1x7x256x256 eval)."""
     import argparse as _ap
     out = []
     base = dict(vars(args))
-    for kw in (dict(workload="train", dtype="bf16", batch=64, steps=max(10, args.steps // 5),
-                    warmup=3),
-               dict(workload="infer1080", dtype="bf16", batch=1, steps=100, warmup=5),
-               dict(workload="infer1080", dtype="f32", batch=1, steps=50, warmup=5),
-               dict(workload="infer256", dtype="f32", batch=1, steps=100, warmup=5)):
+    kws = [dict(workload="train", dtype="bf16", batch=64, steps=max(10, args.steps // 5),
+                warmup=3)]
+    if world == 1:
+        kws += [dict(workload="infer1080", dtype="bf16", batch=1, steps=100, warmup=5),
+                dict(workload="infer1080", dtype="f32", batch=1, steps=50, warmup=5),
+                dict(workload="infer256", dtype="f32", batch=1, steps=100, warmup=5)]
+    for kw in kws:
         a = _ap.Namespace(**{**base, **kw, "vgg": False})
         torch.cuda.empty_cache()
-        r = train_measure(a, world, rank, dev) if a.workload == "train" else \
-            infer_measure(a, world, rank, dev)
+        if a.workload == "train":
+            r = train_measure(a, world, rank, dev)
+        else:
+            r = infer_measure(a, world, rank, dev)
+            if a.workload == "infer1080" and rank == 0 and not args.no_cpu_baseline:
+                r["cpu_baseline"] = cpu_baseline(a.in_ch, 1080, 1920, frames=1, reps=3,
+                                                 train=False, bf16_autocast=a.dtype == "bf16")
         out.append(_summary(r))
     torch.cuda.empty_cache()
     return out
@@ -398,7 +479,10 @@ def train_measure(args, world, rank, dev):
         loss = crit(out, y, x)
         loss.backward()
         if world > 1:
-            nsm_amd.allreduce_grads(model.parameters())
+            # the exposed part of the overlapped all-reduce: how long the compute
+            # stream waits for RCCL after the backward (HIP events)
+            with nops.stage("dp.allreduce_wait"):
+                nsm_amd.allreduce_grads(model.parameters())
         opt.step()
         opt.zero_grad()
         # the reference's batch is a fresh tensor every step (setdata.py:325-326),
@@ -417,7 +501,11 @@ def train_measure(args, world, rank, dev):
         nops.PROBES[st + ".fwd"] = []
         nops.PROBES[st + ".bwd"] = []
     nops.PROBES["vgg.fwd"] = []
+    dp_tags = ("dp.bn_broadcast", "dp.allreduce_wait")
+    for t in dp_tags:
+        nops.PROBES[t] = []
     elapsed = timed(step, args.steps, world, dev)
+    dp_ms = {t: mean_ms(nops.PROBES.pop(t)) for t in dp_tags}
     evs = nops.PROBES.pop(probe_tag)
     kern_ms = mean_ms(evs)
     gemm_ms = mean_ms(nops.PROBES.pop(probe_tag + ".gemm"))
@@ -427,17 +515,23 @@ def train_measure(args, world, rank, dev):
         fw, bw = nops.PROBES.pop(st + ".fwd"), nops.PROBES.pop(st + ".bwd")
         if fw and bw:
             times[st] = mean_ms(fw) + mean_ms(bw)
+    split = os.environ.get("NSM_F32_SPLIT", "1") != "0"
+    full = (H, W, C) == (512, 512, 7)
     if bf16:
         work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30)
         roof = direct_roofline(B, H, W, kern_ms, len(evs))
-        traffic, traffic_src = (load_traffic("traffic_conv6_fwd_bf16.json") if B == 64
+        traffic, traffic_src = (load_traffic("traffic_conv6_fwd_bf16.json") if B == 64 and full
                                 else (None, None))
-        roof.update({"traffic": traffic, "traffic_source": traffic_src})
+        pipe_mult, peak, tag = 1, BF16_PEAK_TFLOPS, f"b{B}_bf16"
     else:
         work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=wino_tile)
-        traffic, traffic_src = load_traffic("traffic_conv6_fwd_f32.json")
+        traffic, traffic_src = (load_traffic("traffic_conv6_fwd_gemm_f32.json") if B == 8 and full
+                                else (None, None))
         roof = dominant_roofline(B, H, W, kern_ms, gemm_ms, len(evs), wino_tile(1024, H // 8, W // 8))
-        roof.update({"traffic": traffic, "traffic_source": traffic_src})
+        pipe_mult, peak = (6, BF16_PEAK_TFLOPS) if split else (1, FP32_PEAK_TFLOPS)
+        tag = f"b{B}_f32"
+    roof.update({"traffic": traffic, "traffic_source": traffic_src})
+    measured, measured_src = load_stage_pmc(tag) if full else (None, None)
 
     frames = world * B * args.steps
     step_flops = 3 * unet_fwd_flops(C, H, W) * B
@@ -463,9 +557,20 @@ def train_measure(args, world, rank, dev):
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"dp{world}"},
         "model_tflops_per_s": round(step_flops * args.steps / elapsed / 1e12 / world, 2),
+        "world_size": dist.get_world_size() if world > 1 else 1,
+        "backend": dist.get_backend() if world > 1 else None,
+        "stage_cols": STAGE_COLS,
+        "stages": stage_table(work, times, pipe_mult, peak, measured),
+        "stage_pmc_source": measured_src,
         "roofline": roof,
-        "stages": stage_table(work, times, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS),
     }
+    if world > 1:
+        res["dp"] = {"bn_broadcast_ms": round(dp_ms["dp.bn_broadcast"], 4),
+                     "allreduce_wait_ms": round(dp_ms["dp.allreduce_wait"], 4),
+                     "grad_bytes": 4 * sum(p.numel() for p in model.parameters()),
+                     "note": "HIP-event time the compute stream spends in the rank-0 BN "
+                             "buffer broadcast at each forward and waiting for the overlapped "
+                             "gradient all-reduce after the backward"}
     if vgg_evs:
         vfl = 2 * B * vgg_fwd_flops(H, W)
         vms = mean_ms(vgg_evs)
@@ -483,7 +588,7 @@ def run_infer(args):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.in_ch, H, W, frames=1, reps=3, train=False)
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        emit(res, args)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
@@ -523,6 +628,9 @@ def infer_measure(args, world, rank, dev):
     evs = nops.PROBES.pop(probe_tag)
     gevs = nops.PROBES.pop(probe_tag + ".gemm", [])
     times = {st: mean_ms(nops.PROBES.pop(st + ".fwd")) for st in STAGES}
+    split = os.environ.get("NSM_F32_SPLIT", "1") != "0"
+    pipe_mult, peak = (6, BF16_PEAK_TFLOPS) if (split and not bf16) else \
+        (1, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS)
     if bf16:
         work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30, passes=1)
         roof = direct_roofline(B, H, W, mean_ms(evs), len(evs))
@@ -550,8 +658,9 @@ def infer_measure(args, world, rank, dev):
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"replicas{world}"},
         "model_tflops_per_s": round(unet_fwd_flops(C, H, W) * frames / elapsed / 1e12 / world, 2),
+        "stage_cols": STAGE_COLS,
+        "stages": stage_table(work, times, pipe_mult, peak),
         "roofline": roof,
-        "stages": stage_table(work, times, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS),
     }
     return res
 
@@ -596,6 +705,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--vgg", action="store_true",
                     help="train: include CustomLoss's VGG19 perceptual term (customLoss.py:7-90)")
+    ap.add_argument("--detail", default=None,
+                    help="also write the full record (all stage rows of every config) to this file")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo launcher check with a stand-in step (no GPU, not a measurement)")
     args = ap.parse_args()

@@ -122,6 +122,17 @@ int nsm_wino_input_resize(const float* x, int ldx, int B, int hi, int wi, int H,
                           int tile, int relu, float* V, void* stream);
 int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
                   int tile, float* Mb, void* stream);
+/* nsm_wino_gemm with the operands' absolute maxima: amax (device) = bits of
+ * max|V|, max|U| (fp32 bit patterns compare as unsigned). With the fp32 split
+ * on, the GEMM then runs the f16x2 split (power-of-two scaled operands, two
+ * fp16 terms, three f16 MFMA products; nsm_conv_split16.inc) instead of the
+ * bf16 three-way split; amax NULL = nsm_wino_gemm. */
+int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
+                    int tile, float* Mb, const uint32_t* amax, void* stream);
+/* atomic max of |x[i]| (as fp32 bits) into *out over n floats; *out must be
+ * zeroed first. NaN counts above +Inf. The maxima a GEMM operand needs when
+ * its producer does not record them. */
+int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
 /* fp32 GEMM arithmetic of the Winograd layers (the batched GEMMs of
  * nsm_wino_gemm / nsm_conv3x3_wino and the weight gradient of
  * nsm_conv3x3_wgrad_wino): 1 (default, env NSM_F32_SPLIT) = each fp32 operand
@@ -339,14 +350,15 @@ int nsm_adamw_step(float* p, const float* g, float* m, float* v, int64_t n, floa
  *   NaN/Inf census; any parameter > 20 % invalid -> skip (main.py:295-317);
  *   else repair NaN -> mean + randn*std*0.1, Inf -> sign*max|valid|*10
  *   (:320-354; randn from `noise` if non-NULL, else a counter-based generator
- *   keyed by seed and the step count); per-parameter clip to 1000*scale
+ *   keyed by seed and the tail-call count step[1]); per-parameter clip to 1000*scale
  *   (:361-365); unscale by 1/scale (:368); per-parameter skip above 1e5,
  *   rescale to 1e3 above 1e3 (:383-397); clip_grad_norm_(max_norm) (:405);
  *   skip if a clipped norm > 10 (:408-418).
  *   Writes seg_coef[nseg][4] (pre-clip x unscale, 1e3 rescale, clip coef,
  *   zeroed), stat[4] (total norm, clip coef, max_norm, max clipped norm),
  *   flags[8] (skip, repaired, severe, nonfinite, huge, postclip, n_rescaled,
- *   n_zeroed), and step[0] += !skip. workspace: nsm_tail_ws_bytes().
+ *   n_zeroed), step[0] += !skip (AdamW steps taken) and step[1] += 1 (tail
+ *   calls; `step` holds two ints). workspace: nsm_tail_ws_bytes().
  * nsm_adamw_tail: torch.optim.AdamW step (main.py:421, hyper-parameters
  *   main.py:955) with g scaled by seg_coef; a no-op when flags[0] is set; the
  *   bias corrections use the device step count. */
@@ -380,6 +392,12 @@ int nsm_range_flag(const float* o, int64_t n, float lo, float hi, int* flag, voi
  * c < c_j and 0 for c_j <= c < cp_j, u ~ U[0,1) from a counter-based hash of
  * (seed, j, b, c). desc (device) = njobs x {off, c, cp, keep as float bits}. */
 int nsm_dropout_masks(const int* desc, int njobs, int B, uint64_t seed, float* out, void* stream);
+/* Profiling marker: an empty kernel of (code + 1) workgroups of 64 lanes.
+ * With NSM_STAGE_MARKS=1 the host brackets each encoder/decoder stage
+ * (Unetmodel.py:104-148) with markers (code = stage id, 0 = stage end), so a
+ * rocprofv3 PMC pass can attribute every dispatch to its stage
+ * (tools/stage_pmc.py); never launched otherwise. */
+int nsm_stage_mark(int code, void* stream);
 
 /* ---- bf16 convolutions (BASELINE config 3) ---------------------------------
  * Same contracts as nsm_pack_conv_weight / nsm_conv_fwd_stats / nsm_conv_wgrad

@@ -1692,12 +1692,13 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
 
 template <int BM, int BN, int WM, int WN>
 static int launch_wino_gemm(const RowsKP& ap, const RowsKP& bp, const EpiStoreP& ep, int M, int N,
-                            int K, int nb, hipStream_t s) {
+                            int K, int nb, hipStream_t s, const uint32_t* amax = nullptr) {
   constexpr int NT = WM * WN * 64;
   using AL = RowsKLoader<BM, NT>;
   using BL = RowsKLoader<BN, NT>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), nb);
-  launch_f32_gemm<BM, BN, WM, WN, AL, BL, EpiStore, RowsKP, RowsKP>(grid, s, ap, bp, ep, M, N, K, K, 1);
+  launch_f32_gemm<BM, BN, WM, WN, AL, BL, EpiStore, RowsKP, RowsKP>(grid, s, ap, bp, ep, M, N, K, K, 1,
+                                                                    amax);
   NSM_LAUNCH_CHECK("wino_gemm");
   return 0;
 }
@@ -1985,6 +1986,21 @@ static bool wino_n64_bm256() {
 
 extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p,
                              int cout_p, int tile, float* Mb, void* stream) {
+  return nsm_wino_gemm_s(V, U, B, H, W, cin_p, cout_p, tile, Mb, nullptr, stream);
+}
+
+extern "C" int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream) {
+  NSM_CHECK_ARG(x && out && n > 0, "absmax: bad args");
+  const long long g = std::min<long long>(ceil_div(n, 1024), 2048);
+  hipLaunchKernelGGL(absmax_kernel, dim3((int)g), dim3(256), 0, as_stream(stream), x,
+                     (long long)n, out);
+  NSM_LAUNCH_CHECK("absmax");
+  return 0;
+}
+
+extern "C" int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int W, int cin_p,
+                               int cout_p, int tile, float* Mb, const uint32_t* amax,
+                               void* stream) {
   NSM_CHECK_ARG(V && U && Mb && cin_p % 32 == 0 && cout_p % 32 == 0, "wino_gemm: bad args");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_gemm: bad tile or shape");
@@ -1999,15 +2015,15 @@ extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W
   // two dispatch rounds on
   if (N >= 128)
     return (mb128 * ceil_div(N, 128) * nb >= (f32_split() ? 512 : 1024))
-               ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s)
-               : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s);
+               ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s, amax)
+               : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s, amax);
   if (N >= 64) {
     // 256x64 (4 waves of 64x64) where the batched grid still has >= 2048 blocks
     if (N == 64 && wino_n64_bm256() && f32_split() && ceil_div(M, 256) * nb >= 2048)
-      return launch_wino_gemm<256, 64, 4, 1>(ap, bp, ep, M, N, K, nb, s);
-    return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, nb, s);
+      return launch_wino_gemm<256, 64, 4, 1>(ap, bp, ep, M, N, K, nb, s, amax);
+    return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, nb, s, amax);
   }
-  return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, nb, s);
+  return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, nb, s, amax);
 }
 
 // thread slots per channel of the statistics form of the output transform:

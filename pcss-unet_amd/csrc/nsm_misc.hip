@@ -98,9 +98,19 @@ __global__ void __launch_bounds__(256) dropout_masks_kernel(const int* __restric
   }
 }
 
+// profiling marker (nsm_stage_mark): no work, its grid encodes the stage
+__global__ void __launch_bounds__(64) stage_mark_kernel(int code) {}
+
 }  // namespace nsm
 
 using namespace nsm;
+
+extern "C" int nsm_stage_mark(int code, void* stream) {
+  NSM_CHECK_ARG(code >= 0 && code < 4096, "stage_mark: bad code");
+  hipLaunchKernelGGL(stage_mark_kernel, dim3(code + 1), dim3(64), 0, as_stream(stream), code);
+  NSM_LAUNCH_CHECK("stage_mark");
+  return 0;
+}
 
 extern "C" int nsm_dropout_masks(const int* desc, int njobs, int B, uint64_t seed, float* out,
                                  void* stream) {

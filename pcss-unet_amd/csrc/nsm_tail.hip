@@ -251,7 +251,9 @@ __global__ void __launch_bounds__(TAIL_THREADS) tail_repair_kernel(
   const float mean = (float)w.seg_d[4 * sgi + 0];
   const float stdv = (float)w.seg_d[4 * sgi + 1];
   const float mx = (float)w.seg_d[4 * sgi + 2];
-  const uint64_t key = seed ^ ((uint64_t)(uint32_t)step[0] << 40);
+  // keyed by the tail-call counter step[1] (advances on every call, skipped
+  // steps included), so consecutive repairs draw independent normals
+  const uint64_t key = seed ^ ((uint64_t)(uint32_t)step[1] << 40);
   double s2 = 0.0;
   int bad = 0;
   for (int64_t i = lo + threadIdx.x; i < hi; i += TAIL_THREADS) {
@@ -323,6 +325,10 @@ __global__ void __launch_bounds__(1024) tail_finalize_kernel(
       // main.py:368 unscale_ (x 1/scale), then :371-397 on the unscaled grad
       const float inv_s = (float)(1.0 / (double)scale);
       float n2 = (n1 * f1) * inv_s;
+      // an overflowed norm (finite values, sum of squares > FLT_MAX): the
+      // reference's factor 1/max(1, inf) = 0 zeroes the gradient, whose norm
+      // is then 0 and the step goes on (main.py:361-365); inf * 0 is NaN here
+      if (n1 == __builtin_inff()) n2 = 0.f;
       // a non-finite survivor of the repair (:374-381) is impossible once
       // zeroed; only an infinite norm (overflowed sum of squares) is left
       if (!zero && !(n2 == n2)) ++nonfin;
@@ -399,6 +405,7 @@ __global__ void __launch_bounds__(1024) tail_finalize_kernel(
     flags[6] = nresc_t;
     flags[7] = nzero_t;
     if (!skip) step[0] = step[0] + 1;
+    step[1] = step[1] + 1;  // tail calls (the repair-noise key)
   }
 }
 

@@ -34,6 +34,8 @@ _SIGS = {
     "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, I, I, P, I, P, Z, P]),
     "nsm_wino_input": (I, [P, I, I, I, I, I, I, I, P, P]),
     "nsm_wino_gemm": (I, [P, P, I, I, I, I, I, I, P, P]),
+    "nsm_wino_gemm_s": (I, [P, P, I, I, I, I, I, I, P, P, P]),
+    "nsm_absmax": (I, [P, L, P, P]),
     "nsm_set_f32_split": (I, [I]),
     "nsm_wino_output": (I, [P, I, I, I, I, I, P, P, I, P]),
     "nsm_wino_wgrad_ws": (Z, [I, I, I, I, I, I]),
@@ -112,6 +114,7 @@ _SIGS = {
     "nsm_nhwc_to_nchw": (I, [P, I, I, I, I, I, P, I, P]),
     "nsm_range_flag": (I, [P, L, F, F, P, P]),
     "nsm_dropout_masks": (I, [P, I, I, U64, P, P]),
+    "nsm_stage_mark": (I, [I, P]),
     "nsm_prep_items": (L, [P]),
     "nsm_prep_weights": (I, [P, I, L, P]),
 }

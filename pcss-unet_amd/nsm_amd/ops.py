@@ -91,10 +91,25 @@ class Partials:
         self._merged = None
 
 
+# Stage markers for per-stage PMC attribution (tools/stage_pmc.py): with
+# NSM_STAGE_MARKS=1 every stage is bracketed by nsm_stage_mark launches whose
+# grid encodes the stage (code = STAGE_CODES[tag] + 1 blocks; 0 = stage end).
+STAGE_NAMES = ["conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv8", "conv9", "head"]
+STAGE_CODES = {f"{n}.{d}": 1 + 2 * i + j for i, n in enumerate(STAGE_NAMES)
+               for j, d in enumerate(("fwd", "bwd"))}
+STAGE_CODES.update({"dp.bn_broadcast": 40, "dp.allreduce_wait": 41})
+MARK_STAGES = os.environ.get("NSM_STAGE_MARKS", "0") == "1"
+
+
+def _mark(code):
+    call("nsm_stage_mark", code, stream())
+
+
 class stage:
     """Context manager: if `tag` is registered in PROBES, bracket everything
     launched inside with HIP events on the current stream (bench.py uses it
-    for the per-stage roofline table)."""
+    for the per-stage roofline table); with NSM_STAGE_MARKS=1 also with
+    marker launches (per-stage rocprofv3 counters)."""
     __slots__ = ("tag", "end")
 
     def __init__(self, tag):
@@ -102,12 +117,16 @@ class stage:
         self.end = None
 
     def __enter__(self):
+        if MARK_STAGES and self.tag in STAGE_CODES:
+            _mark(STAGE_CODES[self.tag])
         self.end = _probe(self.tag)
         return self
 
     def __exit__(self, *exc):
         if self.end is not None:
             self.end.record()
+        if MARK_STAGES and self.tag in STAGE_CODES:
+            _mark(0)
         return False
 
 

@@ -160,14 +160,22 @@ class FlatAdamW(torch.optim.Optimizer):
         self._partial = torch.empty(nb, dtype=torch.float32, device=dev)
         self._sumsq = torch.empty((), dtype=torch.float32, device=dev)
         self._coef = torch.empty((), dtype=torch.float32, device=dev)
-        # device state of the reference tail
-        self._step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        # device state of the reference tail: [AdamW steps taken, tail calls]
+        self._step_dev = torch.zeros(2, dtype=torch.int32, device=dev)
         self.flags = torch.zeros(8, dtype=torch.int32, device=dev)
         self.stat = torch.zeros(4, dtype=torch.float32, device=dev)
         if sanitize:
             self._plan(offs, dev)
         if seed is None:
             seed = int.from_bytes(os.urandom(8), "little") >> 1
+            # data parallel: every rank must draw the same repair noise, or the
+            # replicas diverge at the first NaN repair (all ranks hold the same
+            # averaged gradient) -> rank 0's seed everywhere
+            if world_size > 1 and dist.is_available() and dist.is_initialized():
+                bdev = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+                t = torch.tensor([seed], dtype=torch.int64, device=bdev)
+                dist.broadcast(t, 0)
+                seed = int(t.item())
         self.seed = seed
 
     def _plan(self, offs, dev):
@@ -241,7 +249,7 @@ class FlatAdamW(torch.optim.Optimizer):
 
     # ---- inspection (these synchronise; not for the hot loop) ----------------
     def steps_taken(self):
-        return int(self._step_dev.item()) if self.sanitize else self.step_count
+        return int(self._step_dev[0].item()) if self.sanitize else self.step_count
 
     def last_flags(self):
         """{name: value} of the last sanitised step's decisions (host sync)."""
@@ -304,4 +312,4 @@ class FlatAdamW(torch.optim.Optimizer):
             raise ValueError(f"FlatAdamW keeps one step count; checkpoint has {sorted(steps)}")
         s = steps.pop()
         self.step_count = s
-        self._step_dev.fill_(s)
+        self._step_dev[0] = s

@@ -363,7 +363,8 @@ class Unet(nn.Module):
                        "step tail's NaN/Inf/norm decisions instead")
         if self._bn_broadcast is not None and self.training:
             group, src = self._bn_broadcast
-            self.broadcast_buffers(src, group)
+            with ops.stage("dp.bn_broadcast"):   # timed by bench.py at N > 1
+                self.broadcast_buffers(src, group)
         return _UnetFn.apply(x, self, *params)
 
 

@@ -28,6 +28,10 @@ def test_bench_spawns_two_ranks():
     assert len(line) == 1
     d = json.loads(line[0])
     assert d["n_gpus"] == 2 and d["world_size"] == 2 and d["backend"] == "gloo" and d["dry_run"]
+    # at N > 1 the run measures configs[1] (headline) and configs[3]'s 64/GPU bf16 share
+    wl = {w["config"]: w for w in d["workloads"]}
+    assert wl["configs[1]"]["global_batch"] == 16 and wl["configs[1]"]["dtype"] == "f32"
+    assert wl["configs[3]"]["global_batch"] == 128 and wl["configs[3]"]["dtype"] == "bf16"
 
 
 def test_bench_rejects_world_mismatch():

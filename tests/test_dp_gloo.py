@@ -153,3 +153,37 @@ def test_bn_buffers_broadcast_from_rank0():
         assert np.array_equal(res[1][1][k], res[0][0][k]), k   # rank 1 now has rank 0's
         assert np.array_equal(res[0][1][k], res[0][0][k]), k   # rank 0 unchanged
     assert any(not np.array_equal(res[1][0][k], res[0][0][k]) for k in keys)
+
+
+def _seed_worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pcss-unet_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import nsm_amd
+    ps = [torch.nn.Parameter(torch.zeros(10)), torch.nn.Parameter(torch.zeros(3))]
+    opt = nsm_amd.FlatAdamW(ps, world_size=world, sanitize=True)      # no seed given
+    solo = nsm_amd.FlatAdamW([torch.nn.Parameter(torch.zeros(4))], world_size=1, sanitize=True)
+    q.put((rank, opt.seed, solo.seed))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_flat_adamw_repair_seed_shared_across_ranks():
+    """without an explicit seed every rank drew its own, so the
+    NaN-repair noise (main.py:336) differed per rank and the replicas
+    diverged. Under DP the seed is rank 0's everywhere."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_seed_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict((r, (a, b)) for r, a, b in (q.get(timeout=250) for _ in range(world)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0]
+    assert res[0][1] != res[1][1]    # world_size=1 optimizers keep their own draw

@@ -20,7 +20,7 @@ import torch
 from oracle import unet_ref as O
 from oracle.weights import make_state, synthetic_batch
 from test_gpu_model import _rel, build
-from util import GRAD_REL_L2, LOSS_REL, OUT_ABS, RUN_TOL
+from util import GRAD_REL_L2, LOSS_REL, OUT_ABS, RUN_TOL, record_margin
 
 pytestmark = pytest.mark.gpu
 torch.set_num_threads(16)
@@ -45,7 +45,9 @@ def test_configs0_eval_256(device):
         out = m(torch.from_numpy(x_np).to(device)).cpu()
         ref, _ = O.forward(O.torch_state(np_sd), torch.from_numpy(x_np), training=False)
     assert out.shape == (1, 1, 256, 256)
-    assert (out - ref).abs().max().item() <= OUT_ABS
+    err = (out - ref).abs().max().item()
+    record_margin("configs0_eval_256", out_max_abs=err, out_bound=OUT_ABS)
+    assert err <= OUT_ABS
 
 
 def test_configs1_b8_fp32_train_step_vs_oracle(device):
@@ -81,7 +83,13 @@ def test_configs1_b8_fp32_train_step_vs_oracle(device):
         worst.append((e, k))
         assert e <= GRAD_REL_L2, (k, e)
     print("worst grad rel-L2", sorted(worst, reverse=True)[:3])
-    assert ((x.grad.cpu() - xo.grad).norm() / xo.grad.norm()).item() <= GRAD_REL_L2
+    xg = ((x.grad.cpu() - xo.grad).norm() / xo.grad.norm()).item()
+    record_margin("configs1_b8_fp32_train_step", out_max_abs=err, out_bound=OUT_ABS,
+                  loss_rel=abs(loss.item() - lo.item()) / lo.item(), loss_bound=LOSS_REL,
+                  worst_grad_rel_l2=[[k, e] for e, k in sorted(worst, reverse=True)[:5]],
+                  grad_bound=GRAD_REL_L2, x_grad_rel_l2=xg,
+                  f32_split=__import__("os").environ.get("NSM_F32_SPLIT", "1"))
+    assert xg <= GRAD_REL_L2
     msd = m.state_dict()
     for k, v in sd.items():
         if "running" in k:
@@ -122,6 +130,8 @@ def test_configs2_b64_bf16_small_res_vs_oracle(device):
     ref_xg, our_xg = _rel(xgbf, xg32), _rel(x.grad.cpu(), xg32)
     print(f"configs[2] B=64 128^2: out ours {our_out:.2e} ref-autocast {ref_out:.2e}; "
           f"x_grad ours {our_xg:.2e} ref {ref_xg:.2e}")
+    record_margin("configs2_b64_bf16_128", out_max_abs=our_out, out_bound=1.5 * ref_out,
+                  x_grad_rel_l2=our_xg, x_grad_bound=1.5 * ref_xg)
     assert our_out <= 1.5 * ref_out
     assert our_xg <= 1.5 * ref_xg
     for k, prm in m.named_parameters():

@@ -72,3 +72,52 @@ def test_overlapped_grad_allreduce_two_ranks():
     assert (res[0][1] == want).all()
     assert (res[1][1] == want).all()
     assert abs(want).sum() > 0
+
+
+def _repair_worker(rank, world, port, q):
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pcss-unet_amd"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import nsm_amd
+    from nsm_amd.optim import flat_grad
+    from oracle.weights import make_state, synthetic_batch
+    dev = torch.device("cuda", 0)
+    m = nsm_amd.Unet(in_ch=7, dropout_rate=0.0).to(dev).train()
+    m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in make_state(7, 42).items()})
+    opt = nsm_amd.FlatAdamW(m.parameters(), lr=1e-3, weight_decay=1e-3, max_grad_norm=1.0,
+                            world_size=world, sanitize=True)       # no seed: rank 0's is shared
+    x_np, y_np = synthetic_batch(4, 7, 64, 64)
+    x = torch.from_numpy(x_np[2 * rank:2 * rank + 2]).to(dev)
+    y = torch.from_numpy(y_np[2 * rank:2 * rank + 2]).to(dev)
+    crit = nsm_amd.CustomLoss(dev, 0.9, vgg_weights=False)
+    crit(m(x), y, x).backward()
+    g = flat_grad(list(m.parameters()))
+    if rank == 0:   # a few NaNs on one rank: after the sum every rank repairs them
+        g[1000:1400] = float("nan")
+    nsm_amd.allreduce_grads(m.parameters())
+    opt.step()
+    torch.cuda.synchronize()
+    fl = opt.last_flags()
+    q.put((rank, opt.seed, fl["repaired"], fl["skip"], opt.flat.cpu().numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_repaired_step_keeps_replicas_identical():
+    """a NaN repair under DP must draw the same noise on every
+    rank, so the parameters stay bitwise identical after opt.step()."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_repair_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=500) for _ in range(2)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert res[0][0] == res[1][0]                     # shared seed
+    assert res[0][1] == 1 and res[0][2] == 0          # repaired, step taken
+    assert (res[0][3] == res[1][3]).all()

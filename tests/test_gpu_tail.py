@@ -107,3 +107,60 @@ def test_device_noise_repair_stays_finite_and_close():
     mu, sd = g[ok].mean(), g[ok].std()
     z = (rep - mu) / (sd * 0.1)
     assert abs(z.mean().item()) < 0.2 and 0.8 < z.std().item() < 1.2
+
+
+def test_overflowing_norm_steps_like_reference():
+    """A gradient whose values are finite but whose norm overflows fp32: the
+    reference's pre-unscale clip factor 1/max(1, inf/1000) is 0 (main.py:
+    361-365), the parameter's gradient becomes 0 and the step is taken; the
+    device tail must decide the same and match the oracle's AdamW step."""
+    import nsm_amd
+    from oracle.step_tail_ref import sanitize_and_clip
+    g0 = torch.tensor([3e38, 3e38, 1.0, -2.0])
+    g1 = torch.tensor([0.5, -0.25, 0.125])
+    init = [torch.tensor([0.1, -0.2, 0.3, 0.4]), torch.tensor([1.0, 2.0, -1.0])]
+    # reference (oracle restatement of main.py:287-423 + torch AdamW)
+    ref = [torch.nn.Parameter(t.clone()) for t in init]
+    for p, g in zip(ref, (g0, g1)):
+        p.grad = g.clone()
+    assert not sanitize_and_clip(ref, 0, 200)
+    assert torch.equal(ref[0].grad, torch.zeros(4))
+    ropt = torch.optim.AdamW(ref, lr=1e-3, weight_decay=1e-3)
+    ropt.step()
+    # device
+    ps = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    opt = nsm_amd.FlatAdamW(ps, lr=1e-3, weight_decay=1e-3, max_grad_norm=1.0, sanitize=True,
+                            seed=1)
+    for p, g in zip(ps, (g0, g1)):
+        p.grad = g.clone().to(DEV)
+    opt.step()
+    fl = opt.last_flags()
+    assert fl["skip"] == 0 and fl["nonfinite"] == 0, fl
+    assert opt.steps_taken() == 1
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p.detach().cpu(), r.detach(), rtol=1e-6, atol=1e-7)
+
+
+def test_repair_noise_fresh_after_skipped_step():
+    """The repair noise is keyed by the tail-call counter: a repaired step that
+    is then skipped (post-clip norm > 10, main.py:408-418) does not advance
+    the AdamW step, yet the next repair draws different normals."""
+    import nsm_amd
+    torch.manual_seed(1)
+    n = 20000
+    p = torch.nn.Parameter(torch.zeros(n, device=DEV))
+    opt = nsm_amd.FlatAdamW([p], lr=1e-3, weight_decay=0.0, max_grad_norm=1e9, sanitize=True,
+                            seed=7)
+    G = torch.randn(n, device=DEV) * 100.0      # norm ~1.4e4: rescaled to 1e3, still > 10
+    bad = torch.randperm(n, device=DEV)[:300]
+    G[bad] = float("nan")
+    draws = []
+    for _ in range(2):
+        p.grad = G.clone()
+        opt.step()
+        fl = opt.last_flags()
+        assert fl["repaired"] == 1 and fl["skip"] == 1 and fl["postclip"] == 1, fl
+        draws.append(p.grad[bad].clone())
+    assert opt.steps_taken() == 0
+    assert int(opt._step_dev[1].item()) == 2
+    assert (draws[0] != draws[1]).float().mean().item() > 0.99

@@ -1,4 +1,5 @@
 """Shared helpers for parity tests (test infrastructure)."""
+import json
 import os
 
 import numpy as np
@@ -65,3 +66,23 @@ def check_grads(named_grads, fx, report=None, rel=None, bias_abs=None):
         if not ok:
             fails.append((k, float(err)))
     return fails
+
+
+MARGINS = os.path.join(os.path.dirname(GOLDEN), "..", "gpurun_out", "parity_margins.json")
+
+
+def record_margin(test, **vals):
+    """Keep how close a parity test sits to its bounds: merge {test: vals} into
+    gpurun_out/parity_margins.json (copied to profiles/<round>/ and committed)."""
+    path = os.path.abspath(MARGINS)
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    d = {}
+    if os.path.exists(path):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except ValueError:
+            d = {}
+    d[test] = vals
+    with open(path, "w") as f:
+        json.dump(d, f, indent=1, sort_keys=True)

@@ -36,6 +36,21 @@ kind, path, outp = sys.argv[1], sys.argv[2], sys.argv[3]
 match, triple = KINDS[kind]
 rows = list(csv.DictReader(open(path)))
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+# a run with NSM_STAGE_MARKS=1: keep conv6's forward launches only (its
+# input-gradient twins have the same kernel and grid), markers dropped
+marked = any("stage_mark_kernel" in r["Kernel_Name"] for r in rows)
+if marked:
+    keep, cur = [], 0
+    for r in rows:
+        if "stage_mark_kernel" in r["Kernel_Name"]:
+            cur = int(r["Grid_Size_X"]) // 64 - 1
+        else:
+            r["_stage"] = cur
+            keep.append(r)
+    rows = keep
+    CONV6_FWD = 9   # nsm_amd/ops.py STAGE_CODES["conv6.fwd"]
+    _m = match
+    match = lambda r: r["_stage"] == CONV6_FWD and _m(r)  # noqa: E731
 dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6  # noqa: E731
 spans, parts = [], [[], [], []]
 for i, r in enumerate(rows):
@@ -50,13 +65,14 @@ for i, r in enumerate(rows):
             parts[k].append(dur(x))
     else:
         spans.append(dur(r))
-if not triple and len(spans) > 2:
+if not triple and len(spans) > 2 and not marked:
     # the same kernel/grid also runs conv6.conv.4's input gradient (K = 512):
     # keep the cluster above the largest gap in the sorted durations (K = 9216)
     srt = sorted(spans)
     gap = max(range(1, len(srt)), key=lambda i: srt[i] - srt[i - 1])
     spans = srt[gap:]
-out = {"kind": kind, "launches": len(spans), "span_ms_mean": statistics.mean(spans),
+out = {"kind": kind, "launches": len(spans), "forward_only": marked,
+       "span_ms_mean": statistics.mean(spans),
        "span_ms_median": statistics.median(spans)}
 if triple:
     out.update({"wino_input_ms": statistics.mean(parts[0]), "gemm_ms": statistics.mean(parts[1]),

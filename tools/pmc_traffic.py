@@ -1,81 +1,108 @@
-"""Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes for the dominant
-convolution into a traffic JSON (HBM bytes per launch next to the
-algorithmic bytes); bench.py reads it into roofline.traffic.
+"""HBM traffic per launch of the dominant convolution kernel, from rocprofv3
+PMC passes of a bench.py run with NSM_STAGE_MARKS=1 (the stage markers tell
+conv6's forward launches from its input-gradient twins of the same shape);
+bench.py reads the JSON into roofline.traffic.
 
-Correction per MI355X_MICROARCH.md §HBM: FETCH_SIZE (KB) reads exactly half
-the bytes of a 16-B/lane coalesced stream on gfx950 -> x2 (the kernels below
-load 16 B per lane: buffer_load_dwordx4 / f32x4 / buffer_load ... lds);
-WRITE_SIZE (KB) is exact for 16-B/lane stores and reported as measured.
-
-usage: python tools/pmc_traffic.py {f32|bf16} FETCH_DIR WRITE_DIR OUT_JSON
-  f32 : conv6.conv.0 forward as a whole = the three consecutive dispatches
-        wino_input -> Winograd batched GEMM (F(6x6,3x3): grid 8x8x64 blocks,
-        F(4x4): 16x8x36; B=8) -> wino_output (the dgrad twin has the same shapes and is
-        averaged in); algorithmic bytes = x + y + weights (direct conv)
-  bf16: LDS-DMA implicit GEMM of conv6.conv.0 fwd (+ its dgrad twin, same
-        shape), gemm_bf16_dma_kernel<256,256>, grid 4x1024 blocks of 512, B=64
+usage: python tools/pmc_traffic.py KIND OUT_JSON PMC_CSV [PMC_CSV ...]
+  f32_gemm : conv6.conv.0 fwd Winograd batched GEMM alone (B=8, F(6x6):
+             gemm_f32s_kernel<128,128,2,2,RowsKLoader x2,EpiStore> grid 8x8x64)
+  f32      : conv6.conv.0 fwd as a whole = wino_input + that GEMM + wino_output
+  bf16     : conv6.conv.0 fwd LDS-DMA implicit GEMM, gemm_bf16_dma_kernel<256,256,..,
+             ConvActDma,..> grid 4x1024 blocks (B=64)
+Bytes per launch: reads = 32/64/128 x TCC_EA0_RDREQ_{32B,64B,128B}_sum (the
+L2's fabric read requests by size; Infinity-Cache hits included), cross-
+checked against FETCH_SIZE x 2 (MI355X_MICROARCH.md §HBM); writes =
+WRITE_SIZE (exact for 16-B/lane stores).
 """
-import csv
 import json
+import os
 import sys
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from stage_pmc import CODES, is_mark, load_pmc  # noqa: E402
+
 B8_CONV6 = 8 * 64 * 64
+F32_GEMM = lambda n: (n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n  # noqa: E731
+                      and ("gemm_f32_kernel" in n or "gemm_f32s_kernel" in n))
 KINDS = {
-    "f32": dict(
-        match=lambda n: n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n
-        and ("gemm_f32_kernel" in n or "gemm_f32s_kernel" in n),
-        grid=(8 * 8 * 64 * 256, 16 * 8 * 36 * 256), triple=True,
-        alg=(2 * B8_CONV6 * 1024 + 9 * 1024 * 1024 + 1024) * 4,
-        desc="conv6.conv.0 fwd (+ dgrad twin), B=8: wino_input + gemm_f32_kernel<128,128,2,2,"
-             "RowsKLoader<128,256>x2,EpiStore> (F(6x6): grid 8x8x64; F(4x4): 16x8x36) + "
-             "wino_output"),
-    "bf16": dict(
-        match=lambda n: "gemm_bf16_dma_kernel<256, 256" in n and "ConvActDma" in n,
-        grid=(4 * 1024 * 512,), triple=False,
-        alg=(2 * 262144 * 1024 + 9 * 1024 * 1024) * 2,
-        desc="gemm_bf16_dma_kernel<256,256,2,4,2,...,ConvActDma,RowsKDma,EpiStoreB> grid 4x1024 "
-             "(implicit-GEMM 3x3 conv6.conv.0 fwd + dgrad, M=262144 N=1024 K=9216, B=64)"),
+    "f32_gemm": dict(match=F32_GEMM, grid=8 * 8 * 64 * 256, triple=False,
+                     alg=64 * (2 * 968 * 1024 + 1024 * 1024) * 4,
+                     desc="conv6.conv.0 fwd Winograd F(6x6) batched GEMM, B=8: gemm_f32s_kernel"
+                          "<128,128,2,2,RowsKLoader<128,256>x2,EpiStore> grid 8x8x64 (64 x M=968 "
+                          "N=1024 K=1024); algorithmic bytes = V + U read + M written, fp32"),
+    "f32": dict(match=F32_GEMM, grid=8 * 8 * 64 * 256, triple=True,
+                alg=(2 * B8_CONV6 * 1024 + 9 * 1024 * 1024 + 1024) * 4,
+                desc="conv6.conv.0 fwd as a whole, B=8: wino_input + the GEMM above + "
+                     "wino_output; algorithmic bytes = x + y + weights (direct conv)"),
+    "bf16": dict(match=lambda n: "gemm_bf16_dma_kernel<256, 256" in n and "ConvActDma" in n,
+                 grid=4 * 1024 * 512, triple=False,
+                 alg=(2 * 262144 * 1024 + 9 * 1024 * 1024) * 2,
+                 desc="conv6.conv.0 fwd bf16 LDS-DMA implicit GEMM, B=64: gemm_bf16_dma_kernel"
+                      "<256,256,...,ConvActDma,RowsKDma,EpiStoreB> grid 4x1024 (M=262144 N=1024 "
+                      "K=9216)"),
 }
+FWD = [c for c, n in CODES.items() if n == "conv6.fwd"][0]
 
 
-def rows(d, counter):
-    out = {}
-    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-        if r["Counter_Name"] != counter:
+def launches(path, k):
+    """Counter dicts of the matching launches inside conv6.fwd (summed with the
+    two neighbours for a triple), markers skipped."""
+    disp = load_pmc(path)
+    seq, cur = [], None
+    for name, grid, (cnt, _) in disp:
+        if is_mark(name):
+            code = grid // 64 - 1
+            cur = code if code else None
             continue
-        did = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
-        out[did] = (r["Kernel_Name"], r["Grid_Size"], float(r["Counter_Value"]))
-    return out
-
-
-def per_launch(d, counter, k):
-    rs = rows(d, counter)
-    vals, names = [], set()
-    for did, (name, grid, v) in sorted(rs.items()):
-        if not (k["match"](name) and grid in {str(g) for g in k["grid"]}):
+        seq.append((name, grid, cnt, cur))
+    out, names = [], set()
+    for i, (name, grid, cnt, cur) in enumerate(seq):
+        if cur != FWD or not k["match"](name) or grid != k["grid"]:
             continue
         if k["triple"]:
-            if did - 1 not in rs or did + 1 not in rs:
-                continue
-            names.update((rs[did - 1][0][:60], rs[did + 1][0][:60]))
-            v = rs[did - 1][2] + v + rs[did + 1][2]
-        vals.append(v)
-    return vals, sorted(names)
+            tot = dict(cnt)
+            for j in (i - 1, i + 1):
+                names.add(seq[j][0][:60])
+                for c, v in seq[j][2].items():
+                    tot[c] = tot.get(c, 0.0) + v
+            cnt = tot
+        out.append(cnt)
+    return out, names
 
 
-kind = sys.argv[1]
-k = KINDS[kind]
-f, nf = per_launch(sys.argv[2], "FETCH_SIZE", k)
-w, nw = per_launch(sys.argv[3], "WRITE_SIZE", k)
-fetch_kb = sum(f) / len(f)
-write_kb = sum(w) / len(w)
-out = {"kernel": k["desc"], "launches_sampled": len(f), "fetch_size_kb_raw": fetch_kb,
-       "write_size_kb": write_kb, "fetch_bytes_corrected": fetch_kb * 1024 * 2,
-       "write_bytes": write_kb * 1024,
-       "traffic_bytes_per_launch": fetch_kb * 1024 * 2 + write_kb * 1024,
-       "algorithmic_bytes_per_launch": k["alg"],
-       "neighbour_kernels": sorted(set(nf) | set(nw)),
-       "note": "FETCH_SIZE doubled per the gfx950 calibration (16-B/lane loads); includes "
-               "Infinity-Cache hits, which the counter does not exclude"}
-json.dump(out, open(sys.argv[4], "w"), indent=1)
-print(json.dumps(out, indent=1))
+def main():
+    kind, outp, paths = sys.argv[1], sys.argv[2], sys.argv[3:]
+    k = KINDS[kind]
+    acc, n_by, names = {}, {}, set()
+    for p in paths:
+        ls, nm = launches(p, k)
+        names |= nm
+        for cnt in ls:
+            for c, v in cnt.items():
+                acc[c] = acc.get(c, 0.0) + v
+                n_by[c] = n_by.get(c, 0) + 1
+    avg = {c: acc[c] / n_by[c] for c in acc}
+    out = {"kernel": k["desc"], "launches_sampled": max(n_by.values()) if n_by else 0,
+           "counters_per_launch": avg, "algorithmic_bytes_per_launch": k["alg"],
+           "neighbour_kernels": sorted(names)}
+    if "TCC_EA0_RDREQ_128B_sum" in avg:
+        rest = max(0.0, avg.get("TCC_EA0_RDREQ_sum", 0.0) - avg["TCC_EA0_RDREQ_32B_sum"]
+                   - avg["TCC_EA0_RDREQ_64B_sum"] - avg["TCC_EA0_RDREQ_128B_sum"])
+        out["read_bytes"] = (32 * avg["TCC_EA0_RDREQ_32B_sum"] + 64 * (avg["TCC_EA0_RDREQ_64B_sum"]
+                             + rest) + 128 * avg["TCC_EA0_RDREQ_128B_sum"])
+    if "FETCH_SIZE" in avg:
+        out["fetch_bytes_x2"] = avg["FETCH_SIZE"] * 1024 * 2
+    if "WRITE_SIZE" in avg:
+        out["write_bytes"] = avg["WRITE_SIZE"] * 1024
+    rd = out.get("read_bytes", out.get("fetch_bytes_x2"))
+    if rd is not None and "write_bytes" in out:
+        out["traffic_bytes_per_launch"] = rd + out["write_bytes"]
+        out["traffic_over_algorithmic"] = round(out["traffic_bytes_per_launch"] / k["alg"], 3)
+    out["note"] = ("reads from the sized fabric read requests (FETCH_SIZE x 2 beside them as the "
+                   "guide's cross-check); Infinity-Cache hits are counted, not excluded")
+    json.dump(out, open(outp, "w"), indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
