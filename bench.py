@@ -80,9 +80,28 @@ def vgg_fwd_flops(H, W):
 STAGES = ["conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv8", "conv9", "head"]
 
 
+def f32_split_mode():
+    """NSM_F32_SPLIT as libnsm reads it: 2 (default) f16x2 for the Winograd
+    GEMMs + bf16x3 for the direct ones, 1 bf16x3 everywhere, 0 fp32 MFMA."""
+    v = int(os.environ.get("NSM_F32_SPLIT", "2"))
+    return min(max(v, 0), 2)
+
+
+def pipe_products(bf16):
+    """16-bit MFMA products per fp32 product: (Winograd GEMMs, direct GEMMs)
+    and the dense peak of the pipe that runs them."""
+    if bf16:
+        return (1, 1), BF16_PEAK_TFLOPS
+    m = f32_split_mode()
+    if m == 0:
+        return (1, 1), FP32_PEAK_TFLOPS
+    return ((3, 6) if m == 2 else (6, 6)), BF16_PEAK_TFLOPS
+
+
 def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=128, tile=4, passes=3):
-    """Per stage: (algorithmic FLOPs, executed MFMA FLOPs, HBM bytes) of one
-    train step (passes=3: fwd + dgrad + wgrad) or one forward (passes=1).
+    """Per stage: (algorithmic FLOPs, executed fp32-product FLOPs of the
+    Winograd GEMMs, of the direct GEMMs, HBM bytes) of one train step
+    (passes=3: fwd + dgrad + wgrad) or one forward (passes=1).
 
     Algorithmic = SURVEY.md §8(d): conv FLOPs 2*H*W*Cin*Cout*k^2 per pass;
     bytes = (Cin+Cout)*H*W*s + weights*s per conv and pass. Executed counts
@@ -104,13 +123,15 @@ def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=128, tile=4, passes=3):
         cp = (ci + 31) // 32 * 32
         m = tile(cp, h, w) if callable(tile) else tile
         T = B * ((h + m - 1) // m) * ((w + m - 1) // m)
-        f3 = 2.0 * (m + 2) ** 2 * T * ci * ci if cp >= wino_min else 18.0 * px * ci * ci
+        wino = cp >= wino_min
+        f3 = 2.0 * (m + 2) ** 2 * T * ci * ci if wino else 18.0 * px * ci * ci
         f1 = 2.0 * px * ci * co
         by = ((ci + ci) * px + 9 * ci * ci + (ci + co) * px + ci * co) * bytes_per
-        out[f"conv{k}"] = (passes * f, passes * (f3 + f1), passes * by)
+        out[f"conv{k}"] = (passes * f, passes * (f3 if wino else 0.0),
+                           passes * (f1 + (0.0 if wino else f3)), passes * by)
     px = B * R[0] * R[1]
     fh = 2.0 * px * 16 * 4
-    out["head"] = (passes * fh, passes * fh, passes * (16 * px + 4 * px) * bytes_per)
+    out["head"] = (passes * fh, 0.0, 0.0, passes * (16 * px + 4 * px) * bytes_per)
     return out
 
 
@@ -121,8 +142,9 @@ STAGE_COLS = ["stage", "ms", "alg_tflops", "mfma_frac", "hbm_frac", "meas_gbs", 
 def stage_table(work, times_ms, pipe_mult, peak, measured=None):
     """Per-stage rows (STAGE_COLS): live time (HIP events), algorithmic
     (direct-conv) TFLOP/s, `mfma_frac` = the matrix-core work the stage issues
-    on the pipe that runs it (fp32 split: pipe_mult = 6 bf16 products per fp32
-    product) / time / that pipe's dense peak, `hbm_frac` = algorithmic bytes /
+    on the pipe that runs it (pipe_mult = 16-bit products per fp32 product of
+    its Winograd GEMMs and of its direct GEMMs: f16x2 3, bf16 split 6;
+    pipe_products) / time / that pipe's dense peak, `hbm_frac` = algorithmic bytes /
     time / 8 TB/s; with a committed PMC summary (tools/stage_pmc.py) of the same
     configuration: measured HBM bytes (TCC fabric requests + WRITE_SIZE) / live
     time, their ratio to the algorithmic bytes, MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES
@@ -134,7 +156,7 @@ def stage_table(work, times_ms, pipe_mult, peak, measured=None):
         if st not in times_ms:
             continue
         t = times_ms[st] * 1e-3
-        fl, ex, by = work[st]
+        fl, exw, exd, by = work[st]
         m = ms_.get(st, {})
         mb = m.get("hbm_bytes")
         mf = None
@@ -142,7 +164,7 @@ def stage_table(work, times_ms, pipe_mult, peak, measured=None):
             mf = (m["bf16_mfma_flops"] / (BF16_PEAK_TFLOPS * 1e12)
                   + m.get("f32_mfma_flops", 0.0) / (FP32_PEAK_TFLOPS * 1e12)) / t
         rows.append([st, round(t * 1e3, 3), round(fl / t / 1e12, 1),
-                     round(pipe_mult * ex / t / (peak * 1e12), 3),
+                     round((pipe_mult[0] * exw + pipe_mult[1] * exd) / t / (peak * 1e12), 3),
                      round(by / t / (HBM_PEAK_GBS * 1e9), 3),
                      round(mb / t / 1e9) if mb else None,
                      round(mb / t / (HBM_PEAK_GBS * 1e9), 3) if mb else None,
@@ -229,10 +251,11 @@ def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
     """Roofline object of the step's dominant kernel: conv6.conv.0's forward
     Winograd batched GEMM (nsm_wino_gemm, (m+2)^2 GEMMs of T x 1024 x 1024),
     timed per launch with HIP events on its stream. Priced on the pipe that
-    runs it: with the exact 3-way split (default) every fp32 product is 6 bf16
-    MFMA products, so achieved = 6 x 2*(m+2)^2*T*1024^2 / launch time against
-    the dense bf16 peak (frac <= 1); NSM_F32_SPLIT=0 runs the fp32 MFMA (one
-    product each, fp32 peak). `whole_conv` adds the two Winograd transforms
+    runs it: with the f16x2 split (default) every fp32 product is 3 f16 MFMA
+    products (6 bf16 ones under the three-way bf16 split, NSM_F32_SPLIT=1), so
+    achieved = 3 x 2*(m+2)^2*T*1024^2 / launch time against the dense 16-bit
+    peak (frac <= 1); NSM_F32_SPLIT=0 runs the fp32 MFMA (one product each,
+    fp32 peak). `whole_conv` adds the two Winograd transforms
     (input + output): its time, the same work / that time, and SURVEY.md
     §8(d)'s direct-convolution FLOPs / that time (`direct_equiv_tflops`, a
     rate, not a roofline position: Winograd issues 5x fewer products)."""
@@ -244,14 +267,18 @@ def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
     alg_bytes = (2 * B * h6 * w6 * 1024 + 9 * 1024 * 1024 + 1024) * 4
     ex_flops = nb * 2.0 * T6 * 1024 * 1024
     gemm_bytes = nb * (2 * T6 * 1024 + 1024 * 1024) * 4  # read V, U; write M
-    split = os.environ.get("NSM_F32_SPLIT", "1") != "0"
-    mult, peak = (6, BF16_PEAK_TFLOPS) if split else (1, FP32_PEAK_TFLOPS)
+    mode = f32_split_mode()
+    mult, peak = {0: (1, FP32_PEAK_TFLOPS), 1: (6, BF16_PEAK_TFLOPS),
+                  2: (3, BF16_PEAK_TFLOPS)}[mode]
     work = mult * ex_flops
     achieved = work / (gemm_ms * 1e-3) / 1e12
     return {"kernel": f"conv6.conv.0.fwd Winograd F({m}x{m},3x3) batched GEMM nsm_wino_gemm "
                       f"({nb} x M={T6} N=1024 K=1024), B={B} at {h6}x{w6}: "
-                      + ("gemm_f32s_kernel (fp32 via the exact 3-way bf16 split, 6 products on "
-                         "v_mfma_f32_32x32x16_bf16)" if split else "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)"),
+                      + {2: "gemm_f32h_kernel (fp32 via the f16x2 split of power-of-two scaled "
+                            "operands, 3 products on v_mfma_f32_32x32x16_f16)",
+                         1: "gemm_f32s_kernel (fp32 via the exact 3-way bf16 split, 6 products on "
+                            "v_mfma_f32_32x32x16_bf16)",
+                         0: "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)"}[mode],
             "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
             "frac": round(achieved / peak, 4),
             "basis": (f"matrix-core work issued per launch on the pipe that runs it ({mult} x "
@@ -515,20 +542,19 @@ def train_measure(args, world, rank, dev):
         fw, bw = nops.PROBES.pop(st + ".fwd"), nops.PROBES.pop(st + ".bwd")
         if fw and bw:
             times[st] = mean_ms(fw) + mean_ms(bw)
-    split = os.environ.get("NSM_F32_SPLIT", "1") != "0"
     full = (H, W, C) == (512, 512, 7)
+    pipe_mult, peak = pipe_products(bf16)
     if bf16:
         work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30)
         roof = direct_roofline(B, H, W, kern_ms, len(evs))
         traffic, traffic_src = (load_traffic("traffic_conv6_fwd_bf16.json") if B == 64 and full
                                 else (None, None))
-        pipe_mult, peak, tag = 1, BF16_PEAK_TFLOPS, f"b{B}_bf16"
+        tag = f"b{B}_bf16"
     else:
         work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=wino_tile)
         traffic, traffic_src = (load_traffic("traffic_conv6_fwd_gemm_f32.json") if B == 8 and full
                                 else (None, None))
         roof = dominant_roofline(B, H, W, kern_ms, gemm_ms, len(evs), wino_tile(1024, H // 8, W // 8))
-        pipe_mult, peak = (6, BF16_PEAK_TFLOPS) if split else (1, FP32_PEAK_TFLOPS)
         tag = f"b{B}_f32"
     roof.update({"traffic": traffic, "traffic_source": traffic_src})
     measured, measured_src = load_stage_pmc(tag) if full else (None, None)
@@ -628,9 +654,7 @@ def infer_measure(args, world, rank, dev):
     evs = nops.PROBES.pop(probe_tag)
     gevs = nops.PROBES.pop(probe_tag + ".gemm", [])
     times = {st: mean_ms(nops.PROBES.pop(st + ".fwd")) for st in STAGES}
-    split = os.environ.get("NSM_F32_SPLIT", "1") != "0"
-    pipe_mult, peak = (6, BF16_PEAK_TFLOPS) if (split and not bf16) else \
-        (1, BF16_PEAK_TFLOPS if bf16 else FP32_PEAK_TFLOPS)
+    pipe_mult, peak = pipe_products(bf16)
     if bf16:
         work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30, passes=1)
         roof = direct_roofline(B, H, W, mean_ms(evs), len(evs))

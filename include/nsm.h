@@ -38,6 +38,12 @@ extern "C" {
  * its NHWC tensors in that type and computes in fp32 */
 #define NSM_F32 0
 #define NSM_BF16 1
+
+/* An operand-maximum slot (the `amax` arguments below): NSM_AMAX_WORDS uint32,
+ * zeroed before its producer runs. It holds max|x| of one fp32 GEMM operand as
+ * 64 partial maxima (fp32 bit patterns, compared as unsigned) on separate
+ * 128-B lines; the f16x2 GEMMs reduce them to the operand's scale. */
+#define NSM_AMAX_WORDS 2048
 #define NSM_PACK_FWD 0   /* w[co][ci][k][k] -> [co_p][tap][ci_p]            */
 #define NSM_PACK_DGRAD 1 /* w[co][ci][k][k] -> [ci_p][tap'][co_p], tap'=k*k-1-tap */
 
@@ -66,6 +72,8 @@ typedef struct {
   long long base;
   const float* src;
   void* dst;
+  uint32_t* amax; /* kinds 0, 2 (may be NULL): atomic max of |written| as fp32
+                     bits (zeroed beforehand): the f16x2 GEMM operand scale */
 } NsmPrepJob;
 long long nsm_prep_items(const NsmPrepJob* job);
 int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items, void* stream);
@@ -117,28 +125,35 @@ int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int 
 /* nsm_wino_input of the bilinear align_corners resize of x [B][hi][wi][ldx] to
  * H x W (Unetmodel.py:51-60,122-130: the decoder's x2 upsample feeding a
  * Winograd conv): the resized tensor is sampled inside the transform and never
- * written (relu must be 0 when hi, wi != H, W). */
+ * written (relu must be 0 when hi, wi != H, W). amax (device, may be NULL):
+ * atomic max of |V| as fp32 bits, the f16x2 GEMM's operand scale
+ * (nsm_wino_gemm_s); zero it beforehand. */
 int nsm_wino_input_resize(const float* x, int ldx, int B, int hi, int wi, int H, int W, int cin_p,
-                          int tile, int relu, float* V, void* stream);
+                          int tile, int relu, float* V, uint32_t* amax, void* stream);
 int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
                   int tile, float* Mb, void* stream);
-/* nsm_wino_gemm with the operands' absolute maxima: amax (device) = bits of
- * max|V|, max|U| (fp32 bit patterns compare as unsigned). With the fp32 split
- * on, the GEMM then runs the f16x2 split (power-of-two scaled operands, two
- * fp16 terms, three f16 MFMA products; nsm_conv_split16.inc) instead of the
- * bf16 three-way split; amax NULL = nsm_wino_gemm. */
+/* nsm_wino_gemm with the operands' absolute maxima: amax_v / amax_u (device)
+ * = bits of max|V|, max|U| (fp32 bit patterns compare as unsigned). With the
+ * fp32 split on, the GEMM then runs the f16x2 split (power-of-two scaled
+ * operands, two fp16 terms, three f16 MFMA products; nsm_conv_split16.inc)
+ * instead of the bf16 three-way split; NULL maxima = nsm_wino_gemm. */
 int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int W, int cin_p, int cout_p,
-                    int tile, float* Mb, const uint32_t* amax, void* stream);
-/* atomic max of |x[i]| (as fp32 bits) into *out over n floats; *out must be
- * zeroed first. NaN counts above +Inf. The maxima a GEMM operand needs when
- * its producer does not record them. */
+                    int tile, float* Mb, const uint32_t* amax_v, const uint32_t* amax_u,
+                    void* stream);
+/* max|x[i]| over n floats into the operand-maximum slot out (NSM_AMAX_WORDS,
+ * zeroed first; NaN counts above +Inf): the maximum a GEMM operand needs when
+ * its producer does not record it. */
 int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
-/* fp32 GEMM arithmetic of the Winograd layers (the batched GEMMs of
- * nsm_wino_gemm / nsm_conv3x3_wino and the weight gradient of
- * nsm_conv3x3_wgrad_wino): 1 (default, env NSM_F32_SPLIT) = each fp32 operand
- * split exactly into three bf16 terms, the six products above fp32 rounding
- * on v_mfma_f32_32x32x16_bf16 with fp32 accumulation (fp32 accuracy, 2.67x
- * fewer MFMA cycles); 0 = v_mfma_f32_32x32x2_f32. Returns the previous mode.
+/* fp32 GEMM arithmetic of every fp32 convolution (the batched GEMMs of
+ * nsm_wino_gemm / nsm_conv3x3_wino, the weight gradient of
+ * nsm_conv3x3_wgrad_wino, the direct implicit GEMMs): 2 (default, env
+ * NSM_F32_SPLIT) = the f16x2 split (power-of-two scaled operands as two fp16
+ * terms, three v_mfma_f32_32x32x16_f16 products, fp32 accumulation) for the
+ * GEMMs whose callers pass their operands' maxima, the bf16 split elsewhere;
+ * 1 = each fp32 operand split exactly into three bf16 terms, the six products
+ * above fp32 rounding on v_mfma_f32_32x32x16_bf16 with fp32 accumulation
+ * (fp32 accuracy, 2.67x fewer MFMA cycles); 0 = v_mfma_f32_32x32x2_f32.
+ * Returns the previous mode.
  * Replaces no reference interface (the reference runs cuDNN fp32 convs,
  * Unetmodel.py:16-27); host-wide setting, not per stream. */
 int nsm_set_f32_split(int mode);
@@ -164,9 +179,10 @@ int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int
 /* Both Winograd transforms of a 3x3 conv's output gradient dy [B*H*W][c_p]
  * from one read: V = the input transform for its input-gradient conv (as
  * nsm_wino_input), dM = the transform nsm_conv3x3_wgrad_wino applies (each
- * [(tile+2)^2][T][c_p]); then nsm_conv3x3_wgrad_wino_dm takes dM instead of dy. */
+ * [(tile+2)^2][T][c_p]); then nsm_conv3x3_wgrad_wino_dm takes dM instead of dy.
+ * amax_v / amax_dm (device, may be NULL): atomic max of |V| / |dM| (fp32 bits). */
 int nsm_wino_dual_input(const float* dy, int lddy, int B, int H, int W, int c_p, int tile,
-                        float* V, float* dM, void* stream);
+                        float* V, float* dM, uint32_t* amax_v, uint32_t* amax_dm, void* stream);
 /* As nsm_wino_dual_input, with dy not materialised: each element is the
  * first BatchNorm's backward of g (grad wrt its LeakyReLU(+Dropout2d) output)
  * and y (its input), exactly what nsm_bn_bwd_apply(g, y, ..., coef) would
@@ -174,10 +190,13 @@ int nsm_wino_dual_input(const float* dy, int lddy, int B, int H, int W, int c_p,
 int nsm_wino_dual_input_bn(const float* g, int ldg, const float* y, int ldy, int B, int H, int W,
                            int c_p, int tile, const float* scale, const float* shift, float slope,
                            const float* mask, const float* mean, const float* coef, float* V,
-                           float* dM, void* stream);
+                           float* dM, uint32_t* amax_v, uint32_t* amax_dm, void* stream);
+/* amax_dm / amax_v (device, both or neither): max|dM|, max|V| as recorded by
+ * their producers -> the weight-gradient GEMM runs the f16x2 split. */
 int nsm_conv3x3_wgrad_wino_dm(const float* dM, const float* V, int B, int H, int W, int cin_p,
                               int cout_p, int cin, int cout, int tile, float* dw, float* ws,
-                              size_t ws_floats, void* stream);
+                              size_t ws_floats, const uint32_t* amax_dm, const uint32_t* amax_v,
+                              void* stream);
 
 /* nsm_conv_wgrad: dw[co][ci][kh][kw] (real cout x cin, reference layout) =
  *   sum_p dy[p][co] * pro(x[p+off(tap)][ci]); deterministic split-K over

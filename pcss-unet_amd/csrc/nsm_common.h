@@ -148,6 +148,39 @@ __device__ __forceinline__ float ld1(const bf16_t* p) { return __uint_as_float((
 __device__ __forceinline__ void st1(float* p, float v) { *p = v; }
 __device__ __forceinline__ void st1(bf16_t* p, float v) { *p = (bf16_t)(pack_bf2(v, 0.f) & 0xFFFFu); }
 
+// ---- |x| maxima of f16x2 GEMM operands (nsm_conv_split16.inc) ---------------
+// fp32 bit patterns of |x| compare as unsigned (NaN above +Inf). An operand's
+// maximum lives in a slot of NSM_AMAX_WORDS uint32 (include/nsm.h): 64 partial
+// maxima on separate 128-B lines, so the atomics of thousands of producer
+// waves spread over 64 addresses instead of queueing on one. A producer folds
+// what it stores into a per-thread max and flushes it once per wave (every
+// lane of the wave must reach amax_flush) into the line of its block;
+// consumers reduce the 64 lines (amax_read). out == NULL: nothing recorded.
+constexpr int AMAX_LINES = 64, AMAX_STRIDE = 32;  // NSM_AMAX_WORDS = 2048
+__device__ __forceinline__ void amax_fold(uint32_t& m, float v) {
+  m = max(m, __float_as_uint(v) & 0x7fffffffu);
+}
+__device__ __forceinline__ void amax_fold(uint32_t& m, f32x4 v) {
+  amax_fold(m, v.x);
+  amax_fold(m, v.y);
+  amax_fold(m, v.z);
+  amax_fold(m, v.w);
+}
+__device__ __forceinline__ void amax_flush(uint32_t m, uint32_t* out) {
+  if (!out) return;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  const uint32_t line = (blockIdx.x + 7u * blockIdx.y + 13u * blockIdx.z) & (AMAX_LINES - 1);
+  if ((threadIdx.x & 63) == 0 && m) atomicMax(out + line * AMAX_STRIDE, m);
+}
+// the maximum a slot holds (uniform over the wave; all 64 lanes must call)
+__device__ __forceinline__ uint32_t amax_read(const uint32_t* p) {
+  uint32_t m = p[(threadIdx.x & 63) * AMAX_STRIDE];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  return m;
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace nsm

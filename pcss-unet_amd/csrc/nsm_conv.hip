@@ -1157,8 +1157,17 @@ template <int MT> struct CGt { __device__ static constexpr float c(int i, int j)
 
 // y[i] = sum_j C(i, j) x[j] over the nonzero compile-time coefficients (after
 // unrolling every coefficient is a constant: zeros vanish, +-1 become moves/negations)
+__device__ __forceinline__ float vfma(float c, float x, float a) { return __builtin_fmaf(c, x, a); }
+__device__ __forceinline__ f32x4 vfma(float c, f32x4 x, f32x4 a) {
+  return __builtin_elementwise_fma(f32x4{c, c, c, c}, x, a);
+}
+
 template <class C, int NO, int NI, typename T>
 __device__ __forceinline__ void wmat(const T (&x)[NI], T (&y)[NO]) {
+  // every rounding spelled out (fma where |c| != 1, no contraction left to the
+  // compiler): the same transform inlined into different kernels gives the
+  // same bits (tests/test_gpu_ops.py: dual transform == separate transforms)
+#pragma clang fp contract(off)
 #pragma unroll
   for (int i = 0; i < NO; ++i) {
     T acc{};
@@ -1167,8 +1176,10 @@ __device__ __forceinline__ void wmat(const T (&x)[NI], T (&y)[NO]) {
     for (int j = 0; j < NI; ++j) {
       const float c = C::c(i, j);
       if (c == 0.f) continue;
-      const T term = c == 1.f ? x[j] : (c == -1.f ? -x[j] : c * x[j]);
-      acc = first ? term : acc + term;
+      if (first) acc = c == 1.f ? x[j] : (c == -1.f ? -x[j] : c * x[j]);
+      else if (c == 1.f) acc = acc + x[j];
+      else if (c == -1.f) acc = acc - x[j];
+      else acc = vfma(c, x[j], acc);
       first = false;
     }
     y[i] = acc;
@@ -1229,11 +1240,13 @@ template <int MT, bool RELU, bool UP>
 __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict__ x, int ld, int H,
                                                          int W, int C, int TH, int TW, long long T,
                                                          float* __restrict__ V, int hi, int wi,
-                                                         float sh, float sw) {
+                                                         float sh, float sw,
+                                                         uint32_t* __restrict__ amax) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int C4 = C / CW;
   const long long total = T * C4;
+  uint32_t am = 0;  // max|V| of this thread (the f16x2 GEMM's operand scale)
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C4) * CW;
@@ -1317,8 +1330,12 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
 #pragma unroll
     for (int a = 0; a < A; ++a)
 #pragma unroll
-      for (int e = 0; e < A; ++e) *(VT*)(out + (a * A + e) * plane) = v[a][e];
+      for (int e = 0; e < A; ++e) {
+        *(VT*)(out + (a * A + e) * plane) = v[a][e];
+        if (amax) amax_fold(am, v[a][e]);
+      }
   }
+  amax_flush(am, amax);
 }
 
 // STATS: also the BatchNorm batch statistics of the written values (the
@@ -1488,11 +1505,14 @@ __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict_
                                                         int W, int C, int TH, int TW, long long T,
                                                         float* __restrict__ V,
                                                         float* __restrict__ dM,
-                                                        WinoBnSrc bn = WinoBnSrc{}) {
+                                                        WinoBnSrc bn = WinoBnSrc{},
+                                                        uint32_t* __restrict__ amax_v = nullptr,
+                                                        uint32_t* __restrict__ amax_dm = nullptr) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int C4 = C / CW;
   const long long total = T * C4;
+  uint32_t amv = 0, amd = 0;  // max|V|, max|dM| (the f16x2 GEMMs' operand scales)
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C4) * CW;
@@ -1543,7 +1563,10 @@ __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict_
 #pragma unroll
       for (int a = 0; a < A; ++a)
 #pragma unroll
-        for (int e = 0; e < A; ++e) *(VT*)(out + (a * A + e) * plane) = v[a][e];
+        for (int e = 0; e < A; ++e) {
+          *(VT*)(out + (a * A + e) * plane) = v[a][e];
+          if (amax_v) amax_fold(amv, v[a][e]);
+        }
     }
     VT g[MT][MT], sm[A][A];
 #pragma unroll
@@ -1555,8 +1578,13 @@ __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict_
 #pragma unroll
     for (int a = 0; a < A; ++a)
 #pragma unroll
-      for (int e = 0; e < A; ++e) *(VT*)(out + (a * A + e) * plane) = sm[a][e];
+      for (int e = 0; e < A; ++e) {
+        *(VT*)(out + (a * A + e) * plane) = sm[a][e];
+        if (amax_dm) amax_fold(amd, sm[a][e]);
+      }
   }
+  amax_flush(amv, amax_v);
+  amax_flush(amd, amax_dm);
 }
 
 // dst[b][i] = sum_s src[b][s][i] (float4 lanes, fixed order): the split-K
@@ -1625,7 +1653,7 @@ __host__ __device__ inline long long nsm_prep_items_dev(const NsmPrepJob& j) {
 template <int MT>
 __device__ __forceinline__ void wino_weight_item(const float* __restrict__ w, int cout, int cin,
                                                  int n_p, int k_p, int flip, float* __restrict__ U,
-                                                 int idx) {
+                                                 int idx, uint32_t& am) {
   constexpr int A = MT + 2;
   const int k = idx % k_p, n = idx / k_p;
   const int co = flip ? k : n, ci = flip ? n : k;
@@ -1644,7 +1672,10 @@ __device__ __forceinline__ void wino_weight_item(const float* __restrict__ w, in
 #pragma unroll
   for (int a = 0; a < A; ++a)
 #pragma unroll
-    for (int b = 0; b < A; ++b) U[(a * A + b) * plane + (size_t)n * k_p + k] = u[a][b];
+    for (int b = 0; b < A; ++b) {
+      U[(a * A + b) * plane + (size_t)n * k_p + k] = u[a][b];
+      amax_fold(am, u[a][b]);
+    }
 }
 
 constexpr int PREP_ITEMS = 2048;  // items per block: 8 per thread
@@ -1662,6 +1693,7 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
   }
   const NsmPrepJob& j = jobs[lo];
   const long long items = nsm_prep_items_dev(j);
+  uint32_t am = 0;  // max|written| (the f16x2 GEMMs' operand scale, j.amax)
   for (int r = 0; r < PREP_ITEMS / 256; ++r) {
     const long long li = blk0 - j.base + r * 256 + threadIdx.x;
     if (li >= items) break;
@@ -1677,22 +1709,27 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
         v = (co < cout && ci < cin) ? j.src[((size_t)co * cin + ci) * taps + (taps - 1 - tap)]
                                     : 0.f;
       }
-      if (j.kind == 0) ((float*)j.dst)[idx] = v;
-      else ((bf16_t*)j.dst)[idx] = (bf16_t)(pack_bf2(v, 0.f) & 0xFFFFu);
+      if (j.kind == 0) {
+        ((float*)j.dst)[idx] = v;
+        amax_fold(am, v);
+      } else {
+        ((bf16_t*)j.dst)[idx] = (bf16_t)(pack_bf2(v, 0.f) & 0xFFFFu);
+      }
     } else if (j.kind == 2) {
       float* U = (float*)j.dst;
-      if (j.a[5] == 6) wino_weight_item<6>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx);
-      else if (j.a[5] == 4) wino_weight_item<4>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx);
-      else wino_weight_item<2>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx);
+      if (j.a[5] == 6) wino_weight_item<6>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx, am);
+      else if (j.a[5] == 4) wino_weight_item<4>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx, am);
+      else wino_weight_item<2>(j.src, j.a[0], j.a[1], j.a[2], j.a[3], j.a[4], U, idx, am);
     } else {
       ((float*)j.dst)[idx] = idx < j.a[0] ? j.src[idx] : 0.f;
     }
   }
+  amax_flush(am, j.amax);  // uniform per block (a block serves one job)
 }
 
 template <int BM, int BN, int WM, int WN>
 static int launch_wino_gemm(const RowsKP& ap, const RowsKP& bp, const EpiStoreP& ep, int M, int N,
-                            int K, int nb, hipStream_t s, const uint32_t* amax = nullptr) {
+                            int K, int nb, hipStream_t s, AmaxPair amax = AmaxPair{nullptr, nullptr}) {
   constexpr int NT = WM * WN * 64;
   using AL = RowsKLoader<BM, NT>;
   using BL = RowsKLoader<BN, NT>;
@@ -1944,7 +1981,8 @@ extern "C" int nsm_wino_weight(const float* w, int cout, int cin, int n_p, int k
 }
 
 extern "C" int nsm_wino_input_resize(const float* x, int ldx, int B, int hi, int wi, int H, int W,
-                                     int cin_p, int tile, int relu, float* V, void* stream) {
+                                     int cin_p, int tile, int relu, float* V, uint32_t* amax,
+                                     void* stream) {
   NSM_CHECK_ARG(x && V && cin_p % 32 == 0 && ldx % 4 == 0 && ldx >= cin_p, "wino_input: bad args");
   NSM_CHECK_ARG(hi > 0 && wi > 0, "wino_input: bad source shape");
   NSM_CHECK_ARG(!(relu && (hi != H || wi != W)), "wino_input: relu with a resize");
@@ -1956,7 +1994,7 @@ extern "C" int nsm_wino_input_resize(const float* x, int ldx, int B, int hi, int
   const float sh = ac_scale(hi, H), sw = ac_scale(wi, W);
 #define NSM_WI(m, r, u)                                                                           \
   hipLaunchKernelGGL((wino_input_kernel<m, r, u>), grid, dim3(256), 0, s, x, ldx, H, W, cin_p,     \
-                     g.TH, g.TW, g.T, V, hi, wi, sh, sw)
+                     g.TH, g.TW, g.T, V, hi, wi, sh, sw, amax)
   if (tile == 2) {
     if (up) NSM_WI(2, false, true); else if (relu) NSM_WI(2, true, false); else NSM_WI(2, false, false);
   } else if (tile == 4) {
@@ -1971,7 +2009,7 @@ extern "C" int nsm_wino_input_resize(const float* x, int ldx, int B, int hi, int
 
 extern "C" int nsm_wino_input(const float* x, int ldx, int B, int H, int W, int cin_p, int tile,
                               int relu, float* V, void* stream) {
-  return nsm_wino_input_resize(x, ldx, B, H, W, H, W, cin_p, tile, relu, V, stream);
+  return nsm_wino_input_resize(x, ldx, B, H, W, H, W, cin_p, tile, relu, V, nullptr, stream);
 }
 
 // 256x64 tiles for the 64-channel Winograd GEMMs (conv9 at 256^2: fwd 122 ->
@@ -1986,7 +2024,7 @@ static bool wino_n64_bm256() {
 
 extern "C" int nsm_wino_gemm(const float* V, const float* U, int B, int H, int W, int cin_p,
                              int cout_p, int tile, float* Mb, void* stream) {
-  return nsm_wino_gemm_s(V, U, B, H, W, cin_p, cout_p, tile, Mb, nullptr, stream);
+  return nsm_wino_gemm_s(V, U, B, H, W, cin_p, cout_p, tile, Mb, nullptr, nullptr, stream);
 }
 
 extern "C" int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream) {
@@ -1999,8 +2037,8 @@ extern "C" int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream
 }
 
 extern "C" int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int W, int cin_p,
-                               int cout_p, int tile, float* Mb, const uint32_t* amax,
-                               void* stream) {
+                               int cout_p, int tile, float* Mb, const uint32_t* amax_v,
+                               const uint32_t* amax_u, void* stream) {
   NSM_CHECK_ARG(V && U && Mb && cin_p % 32 == 0 && cout_p % 32 == 0, "wino_gemm: bad args");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_gemm: bad tile or shape");
@@ -2015,15 +2053,15 @@ extern "C" int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int
   // two dispatch rounds on
   if (N >= 128)
     return (mb128 * ceil_div(N, 128) * nb >= (f32_split() ? 512 : 1024))
-               ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s, amax)
-               : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s, amax);
+               ? launch_wino_gemm<128, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s, AmaxPair{amax_v, amax_u})
+               : launch_wino_gemm<64, 128, 2, 2>(ap, bp, ep, M, N, K, nb, s, AmaxPair{amax_v, amax_u});
   if (N >= 64) {
     // 256x64 (4 waves of 64x64) where the batched grid still has >= 2048 blocks
     if (N == 64 && wino_n64_bm256() && f32_split() && ceil_div(M, 256) * nb >= 2048)
-      return launch_wino_gemm<256, 64, 4, 1>(ap, bp, ep, M, N, K, nb, s, amax);
-    return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, nb, s, amax);
+      return launch_wino_gemm<256, 64, 4, 1>(ap, bp, ep, M, N, K, nb, s, AmaxPair{amax_v, amax_u});
+    return launch_wino_gemm<128, 64, 2, 2>(ap, bp, ep, M, N, K, nb, s, AmaxPair{amax_v, amax_u});
   }
-  return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, nb, s, amax);
+  return launch_wino_gemm<128, 32, 4, 1>(ap, bp, ep, M, N, K, nb, s, AmaxPair{amax_v, amax_u});
 }
 
 // thread slots per channel of the statistics form of the output transform:
@@ -2193,19 +2231,21 @@ extern "C" size_t nsm_wino_wgrad_ws(int B, int H, int W, int cin_p, int cout_p, 
 
 template <int BM, int BN, int WM, int WN>
 static int launch_wino_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& ep, int M,
-                             int N, int K, int kchunk, int splits, int nb, hipStream_t s) {
+                             int N, int K, int kchunk, int splits, int nb, hipStream_t s,
+                             AmaxPair amax) {
   constexpr int NT = WM * WN * 64;
   using AL = PixRowsLoader<BM, NT, false, false>;
   using BL = PixRowsLoader<BN, NT, false, false>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), nb * splits);
   launch_f32_gemm<BM, BN, WM, WN, AL, BL, EpiSlabV, PixRowsP, PixRowsP>(grid, s, ap, bp, ep, M, N, K,
-                                                                        kchunk, splits);
+                                                                        kchunk, splits, amax);
   NSM_LAUNCH_CHECK("wino_wgrad_gemm");
   return 0;
 }
 
 extern "C" int nsm_wino_dual_input(const float* dy, int lddy, int B, int H, int W, int c_p,
-                                   int tile, float* V, float* dM, void* stream) {
+                                   int tile, float* V, float* dM, uint32_t* amax_v,
+                                   uint32_t* amax_dm, void* stream) {
   NSM_CHECK_ARG(dy && V && dM && c_p % 32 == 0 && lddy % 4 == 0 && lddy >= c_p,
                 "wino_dual_input: bad args");
   WinoGeom g;
@@ -2214,13 +2254,13 @@ extern "C" int nsm_wino_dual_input(const float* dy, int lddy, int B, int H, int 
   hipStream_t s = as_stream(stream);
   if (tile == 2)
     hipLaunchKernelGGL(wino_dual_kernel<2>, grid, dim3(256), 0, s, dy, lddy, H, W, c_p, g.TH, g.TW,
-                       g.T, V, dM);
+                       g.T, V, dM, WinoBnSrc{}, amax_v, amax_dm);
   else if (tile == 4)
     hipLaunchKernelGGL(wino_dual_kernel<4>, grid, dim3(256), 0, s, dy, lddy, H, W, c_p, g.TH, g.TW,
-                       g.T, V, dM);
+                       g.T, V, dM, WinoBnSrc{}, amax_v, amax_dm);
   else
     hipLaunchKernelGGL(wino_dual_kernel<6>, grid, dim3(256), 0, s, dy, lddy, H, W, c_p, g.TH, g.TW,
-                       g.T, V, dM);
+                       g.T, V, dM, WinoBnSrc{}, amax_v, amax_dm);
   NSM_LAUNCH_CHECK("wino_dual_input");
   return 0;
 }
@@ -2229,7 +2269,7 @@ extern "C" int nsm_wino_dual_input_bn(const float* g, int ldg, const float* y, i
                                       int H, int W, int c_p, int tile, const float* scale,
                                       const float* shift, float slope, const float* mask,
                                       const float* mean, const float* coef, float* V, float* dM,
-                                      void* stream) {
+                                      uint32_t* amax_v, uint32_t* amax_dm, void* stream) {
   NSM_CHECK_ARG(g && y && V && dM && scale && shift && mean && coef && c_p % 32 == 0 &&
                     ldg % 4 == 0 && ldg >= c_p && ldy % 4 == 0 && ldy >= c_p,
                 "wino_dual_input_bn: bad args");
@@ -2238,7 +2278,7 @@ extern "C" int nsm_wino_dual_input_bn(const float* g, int ldg, const float* y, i
   dim3 grid(grid_1d(geo.T * c_p / (tile == 6 ? 1 : 4)));
   hipStream_t s = as_stream(stream);
   const WinoBnSrc bn{y, ldy, scale, shift, mean, coef, mask, slope};
-#define A_ g, ldg, H, W, c_p, geo.TH, geo.TW, geo.T, V, dM, bn
+#define A_ g, ldg, H, W, c_p, geo.TH, geo.TW, geo.T, V, dM, bn, amax_v, amax_dm
   if (tile == 2) hipLaunchKernelGGL((wino_dual_kernel<2, true>), grid, dim3(256), 0, s, A_);
   else if (tile == 4) hipLaunchKernelGGL((wino_dual_kernel<4, true>), grid, dim3(256), 0, s, A_);
   else hipLaunchKernelGGL((wino_dual_kernel<6, true>), grid, dim3(256), 0, s, A_);
@@ -2249,7 +2289,7 @@ extern "C" int nsm_wino_dual_input_bn(const float* g, int ldg, const float* y, i
 
 static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float* V, int B, int H,
                       int W, int cin_p, int cout_p, int cin, int cout, int tile, float* dw,
-                      float* ws, size_t ws_floats, void* stream);
+                      float* ws, size_t ws_floats, void* stream, AmaxPair amax = AmaxPair{});
 
 extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int H,
                                       int W, int cin_p, int cout_p, int cin, int cout, int tile,
@@ -2261,15 +2301,17 @@ extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V,
 // the weight gradient from a dM nsm_wino_dual_input already wrote (no dY read)
 extern "C" int nsm_conv3x3_wgrad_wino_dm(const float* dM, const float* V, int B, int H, int W,
                                          int cin_p, int cout_p, int cin, int cout, int tile,
-                                         float* dw, float* ws, size_t ws_floats, void* stream) {
+                                         float* dw, float* ws, size_t ws_floats,
+                                         const uint32_t* amax_dm, const uint32_t* amax_v,
+                                         void* stream) {
   NSM_CHECK_ARG(dM, "conv3x3_wgrad_wino_dm: null dM");
   return wgrad_wino(nullptr, cout_p, dM, V, B, H, W, cin_p, cout_p, cin, cout, tile, dw, ws,
-                    ws_floats, stream);
+                    ws_floats, stream, AmaxPair{amax_dm, amax_v});
 }
 
 static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float* V, int B, int H,
                       int W, int cin_p, int cout_p, int cin, int cout, int tile, float* dw,
-                      float* ws, size_t ws_floats, void* stream) {
+                      float* ws, size_t ws_floats, void* stream, AmaxPair amax) {
   NSM_CHECK_ARG((dy || dM_in) && V && dw && ws, "conv3x3_wgrad_wino: null pointer");
   NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0 && lddy % 4 == 0 && cin <= cin_p &&
                     cout <= cout_p, "conv3x3_wgrad_wino: bad channels");
@@ -2317,7 +2359,7 @@ static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float
   int rc;
 #define NSM_WW(bm, bn, wm, wn) \
   if (pl.BM == bm && pl.BN == bn) \
-    rc = launch_wino_wgrad<bm, bn, wm, wn>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, nb, s); \
+    rc = launch_wino_wgrad<bm, bn, wm, wn>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, nb, s, amax); \
   else
   NSM_WW(128, 128, 2, 2)
   NSM_WW(128, 64, 2, 2)
@@ -2327,7 +2369,7 @@ static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float
   NSM_WW(32, 128, 1, 4)
   NSM_WW(64, 32, 2, 1)
   NSM_WW(32, 64, 1, 2)
-  rc = launch_wino_wgrad<32, 32, 1, 1>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, nb, s);
+  rc = launch_wino_wgrad<32, 32, 1, 1>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, nb, s, amax);
 #undef NSM_WW
   if (rc) return rc;
   // split-K partials -> one dU per xi with a parallel, fixed-order sum (the
@@ -2363,7 +2405,7 @@ namespace nsm {
 // 1: fp32 GEMMs on the bf16 matrix cores by the exact split (default), 0: on
 // v_mfma_f32_32x32x2_f32; returns the previous mode
 extern "C" int nsm_set_f32_split(int mode) {
-  const int prev = f32_split() ? 1 : 0;
-  g_f32_split = mode ? 1 : 0;
+  const int prev = f32_split_mode();
+  g_f32_split = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
   return prev;
 }

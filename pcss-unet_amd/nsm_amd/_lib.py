@@ -34,7 +34,7 @@ _SIGS = {
     "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, I, I, P, I, P, Z, P]),
     "nsm_wino_input": (I, [P, I, I, I, I, I, I, I, P, P]),
     "nsm_wino_gemm": (I, [P, P, I, I, I, I, I, I, P, P]),
-    "nsm_wino_gemm_s": (I, [P, P, I, I, I, I, I, I, P, P, P]),
+    "nsm_wino_gemm_s": (I, [P, P, I, I, I, I, I, I, P, P, P, P]),
     "nsm_absmax": (I, [P, L, P, P]),
     "nsm_set_f32_split": (I, [I]),
     "nsm_wino_output": (I, [P, I, I, I, I, I, P, P, I, P]),
@@ -56,16 +56,16 @@ _SIGS = {
     "nsm_resize_fwd_act": (I, [P, I, I, I, I, P, I, I, P, P, F, P, I, P]),
     "nsm_up2_resize_fwd_act": (I, [P, I, I, I, I, P, I, I, P, P, F, P, I, P]),
     "nsm_bn_act_pool": (I, [P, I, I, I, I, P, P, F, P, P, I, P]),
-    "nsm_wino_dual_input": (I, [P, I, I, I, I, I, I, P, P, P]),
-    "nsm_wino_dual_input_bn": (I, [P, I, P, I, I, I, I, I, I, P, P, F, P, P, P, P, P, P]),
-    "nsm_conv3x3_wgrad_wino_dm": (I, [P, P, I, I, I, I, I, I, I, I, P, P, Z, P]),
+    "nsm_wino_dual_input": (I, [P, I, I, I, I, I, I, P, P, P, P, P]),
+    "nsm_wino_dual_input_bn": (I, [P, I, P, I, I, I, I, I, I, P, P, F, P, P, P, P, P, P, P, P]),
+    "nsm_conv3x3_wgrad_wino_dm": (I, [P, P, I, I, I, I, I, I, I, I, P, P, Z, P, P, P]),
     "nsm_conv_fwd_act": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, F, P, I, I, P]),
     "nsm_wino_output_act": (I, [P, I, I, I, I, I, P, P, I, P, P, F, P, I, P]),
     "nsm_bnred_chunks": (I, [I, I, I, I, I]),
     "nsm_avgpool2_bwd_add_bnred": (I, [P, I, I, I, I, P, P, I, P, P, P, P, P, F, P, P]),
     "nsm_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P]),
     "nsm_up2_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P]),
-    "nsm_wino_input_resize": (I, [P, I, I, I, I, I, I, I, I, I, P, P]),
+    "nsm_wino_input_resize": (I, [P, I, I, I, I, I, I, I, I, I, P, P, P]),
     "nsm_wino_output_stats": (I, [P, I, I, I, I, I, P, P, I, P, I, P]),
     "nsm_wino_stat_slots": (I, [I, I, I, I, I]),
     "nsm_conv1x1_bnbwd_chunks": (I, [I, I, I, I, I]),

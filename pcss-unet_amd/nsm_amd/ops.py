@@ -38,9 +38,11 @@ def empty(*shape, device):
 
 
 def set_f32_split(mode):
-    """fp32 GEMMs on the bf16 matrix cores by the exact three-way split (1,
-    the default; fp32 accuracy, csrc/nsm_conv_split.inc) or on the fp32 MFMA
-    (0). Returns the previous mode."""
+    """Arithmetic of the fp32 GEMMs: 2 (default) = the f16x2 split of
+    power-of-two scaled operands (csrc/nsm_conv_split16.inc) where the operand
+    maxima are passed (the Winograd GEMMs of the model path), the bf16 split
+    elsewhere; 1 = the exact three-way bf16 split everywhere
+    (csrc/nsm_conv_split.inc); 0 = the fp32 MFMA. Returns the previous mode."""
     from ._lib import lib
     return int(lib.nsm_set_f32_split(int(mode)))
 
@@ -53,6 +55,28 @@ def pack_conv_weight(w, cout_p, cin_p, mode, dtype=F32):
     out = torch.empty(cout_p * taps * cin_p, dtype=dtype, device=w.device)
     fn = "nsm_pack_conv_weight_bf16" if dtype == BF16 else "nsm_pack_conv_weight"
     call(fn, ptr(w), cout, cin, k, cout_p, cin_p, mode, ptr(out), stream())
+    return out
+
+
+AMAX_WORDS = 2048   # include/nsm.h NSM_AMAX_WORDS: one operand-maximum slot
+
+
+def amax_slots(n, device):
+    """n zeroed operand-maximum slots (include/nsm.h NSM_AMAX_WORDS each)."""
+    return torch.zeros(n * AMAX_WORDS, dtype=torch.int32, device=device)
+
+
+def amax_slot(buf, i):
+    """Slot i of an amax_slots buffer (None -> None)."""
+    return None if buf is None else buf[i * AMAX_WORDS:(i + 1) * AMAX_WORDS]
+
+
+def absmax(x, out=None):
+    """Operand-maximum slot holding max|x| (nsm_absmax): the f16x2 GEMM
+    operand scale of a tensor whose producer did not record it."""
+    if out is None:
+        out = amax_slots(1, x.device)
+    call("nsm_absmax", ptr(x), x.numel(), ptr(out), stream())
     return out
 
 
@@ -196,7 +220,8 @@ def wino_weight(w, n_p, k_p, flip, tile=4):
 
 
 def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, relu=False,
-                 stats=False, nslot=None, src_hw=None, act=None, v_in=None):
+                 stats=False, nslot=None, src_hw=None, act=None, v_in=None, amax_v=None,
+                 amax_u=None):
     """3x3 (pad 1) convolution of x [B*H*W, cin_p] via Winograd F(tile x tile, 3x3).
     keep_v=True also returns the transformed input V [(tile+2)^2][T][cin_p],
     reused by the Winograd weight gradient. stats=True returns (y, V|None,
@@ -207,7 +232,11 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     align_corners resize to H x W that the input transform samples on the fly.
     act=(BNState, res|None): eval BN + LeakyReLU (+ skip) applied by the output
     transform (nsm_wino_output_act). v_in: x's input transform already made
-    (wino_dual_input); x is then not read."""
+    (wino_dual_input); x is then not read.
+    amax_v / amax_u: operand-maximum slots (amax_slot) of max|V| / max|U| (V's is zeroed by the
+    caller and filled by the input transform, or by wino_dual_input for v_in;
+    U's by the weight preparation): with both, the GEMM runs the f16x2 split
+    (csrc/nsm_conv_split16.inc), else the bf16 split."""
     from ._lib import lib
     cin_p = x.shape[1]
     M = B * H * W
@@ -223,9 +252,11 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     else:
         V = empty(nb * T * cin_p, device=x.device)    # kept alive for the wgrad
         call("nsm_wino_input_resize", ptr(x), x.stride(0), B, hi, wi, H, W, cin_p, tile,
-             int(relu), ptr(V), st)
+             int(relu), ptr(V), ptr(amax_v), st)
     ev = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
-    call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb), st)
+    both = amax_v is not None and amax_u is not None
+    call("nsm_wino_gemm_s", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb),
+         ptr(amax_v) if both else None, ptr(amax_u) if both else None, st)
     if ev is not None:
         ev.record()
     part = None
@@ -256,16 +287,17 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     return (y, V) if keep_v else y
 
 
-def wino_dual_input(dy, B, H, W, tile=4):
+def wino_dual_input(dy, B, H, W, tile=4, amax=(None, None)):
     """(Vd, dM) of the output gradient dy [B*H*W, C_p] from one read of it:
     Vd feeds conv3x3_wino(v_in=Vd) (the input gradient), dM feeds
-    conv3x3_wgrad_wino(dM=dM) (the weight gradient)."""
+    conv3x3_wgrad_wino(dM=dM) (the weight gradient). amax: zeroed operand-maximum
+    slots (or None) receiving max|Vd|, max|dM| (the f16x2 GEMMs' operand scales)."""
     c_p = dy.shape[1]
     n = (tile + 2) ** 2 * wino_tiles(B, H, W, tile) * c_p
     Vd = empty(n, device=dy.device)
     dM = empty(n, device=dy.device)
     call("nsm_wino_dual_input", ptr(dy), dy.stride(0), B, H, W, c_p, tile, ptr(Vd), ptr(dM),
-         stream())
+         ptr(amax[0]), ptr(amax[1]), stream())
     return Vd, dM
 
 
@@ -280,7 +312,7 @@ class DeferredBnBwd:
         self.shape, self.device, self.dtype = g.shape, g.device, g.dtype
 
 
-def wino_dual_input_bn(d, y, st, mask, B, H, W, tile=4, slope=0.2):
+def wino_dual_input_bn(d, y, st, mask, B, H, W, tile=4, slope=0.2, amax=(None, None)):
     """wino_dual_input of the BN backward d = DeferredBnBwd(g, coef) of BN
     input y (state st, Dropout2d mask [B][C] or None): dY is never stored."""
     c_p = y.shape[1]
@@ -289,13 +321,15 @@ def wino_dual_input_bn(d, y, st, mask, B, H, W, tile=4, slope=0.2):
     dM = empty(n, device=y.device)
     call("nsm_wino_dual_input_bn", ptr(d.g), d.g.stride(0), ptr(y), y.stride(0), B, H, W, c_p,
          tile, ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(d.coef),
-         ptr(Vd), ptr(dM), stream())
+         ptr(Vd), ptr(dM), ptr(amax[0]), ptr(amax[1]), stream())
     return Vd, dM
 
 
-def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, dM=None):
+def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, dM=None,
+                       amax=(None, None)):
     """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino, same tile).
-    dM: dy's transform from wino_dual_input (dy is then not read)."""
+    dM: dy's transform from wino_dual_input (dy is then not read). amax = (max|dM|,
+    max|V|) slots: with both (and dM given) the GEMM runs the f16x2 split."""
     from ._lib import lib
     cout_p = dy.shape[1]
     n = int(lib.nsm_wino_wgrad_ws(B, H, W, cin_p, cout_p, tile))
@@ -305,8 +339,10 @@ def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, d
         call("nsm_conv3x3_wgrad_wino", ptr(dy), dy.stride(0), ptr(V), B, H, W, cin_p, cout_p, cin,
              cout, tile, ptr(dw), ptr(ws), n, stream())
     else:
+        both = amax[0] is not None and amax[1] is not None
         call("nsm_conv3x3_wgrad_wino_dm", ptr(dM), ptr(V), B, H, W, cin_p, cout_p, cin, cout,
-             tile, ptr(dw), ptr(ws), n, stream())
+             tile, ptr(dw), ptr(ws), n, ptr(amax[0]) if both else None,
+             ptr(amax[1]) if both else None, stream())
     if ev is not None:
         ev.record()
 

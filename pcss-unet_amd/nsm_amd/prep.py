@@ -21,7 +21,7 @@ from ._lib import call, lib, ptr, stream
 
 class NsmPrepJob(ctypes.Structure):
     _fields_ = [("kind", ctypes.c_int), ("a", ctypes.c_int * 7), ("base", ctypes.c_longlong),
-                ("src", ctypes.c_void_p), ("dst", ctypes.c_void_p)]
+                ("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("amax", ctypes.c_void_p)]
 
 
 KIND_PACK_F32, KIND_PACK_BF16, KIND_WINO, KIND_PAD = 0, 1, 2, 3
@@ -46,6 +46,9 @@ class LazyBlockWeights:
         return ops.wino_weight(self.blk.conv[0].weight.detach(), self.cip, self.cip, flip=flip,
                                tile=tile)
 
+    def amax_U1(self, flip):
+        return None      # no recorded maximum: the bf16 split runs
+
     def w1(self, mode):
         return ops.pack_conv_weight(self.blk.conv[0].weight.detach(), self.cip, self.cip, mode,
                                     self.dtype)
@@ -67,6 +70,10 @@ class _PreparedBlock:
     def U1(self, tile, flip):
         return self.t[("U1", flip)]
 
+    def amax_U1(self, flip):
+        """max|U| of the step's Winograd weight (written by the prep launch)."""
+        return self.t.get(("amaxU1", flip))
+
     def w1(self, mode):
         return self.t[("w1", mode)]
 
@@ -87,8 +94,14 @@ class StepWeights:
         self.blocks = {}
         jobs, keep = [], []
         base = 0
+        n_wino = sum(1 for k in shapes if ops.pad32(mod.block(k).conv[0].in_channels) >= wino_min
+                     and dtype == torch.float32) * 2
+        # per-step maxima of the Winograd weights (the f16x2 GEMMs' operand
+        # scales), zeroed by run() before the prep launch refills them
+        self.amax = ops.amax_slots(max(n_wino, 1), dev)
+        n_am = 0
 
-        def add(kind, a, src, shape_numel, out_dtype):
+        def add(kind, a, src, shape_numel, out_dtype, amax=None):
             nonlocal base
             out = torch.empty(shape_numel, dtype=out_dtype, device=dev)
             j = NsmPrepJob()
@@ -98,6 +111,7 @@ class StepWeights:
             j.base = base
             j.src = src.data_ptr()
             j.dst = out.data_ptr()
+            j.amax = amax.data_ptr() if amax is not None else None
             n = int(lib.nsm_prep_items(ctypes.byref(j)))
             assert n > 0, (kind, a)
             base += n
@@ -121,8 +135,12 @@ class StepWeights:
             if cip >= wino_min and dtype == torch.float32:
                 tile = wino_tile(cip, h, w)
                 for flip in ((False, True) if training else (False,)):
+                    am = ops.amax_slot(self.amax, n_am)
+                    n_am += 1
+                    pb.t[("amaxU1", flip)] = am
                     pb.t[("U1", flip)] = add(KIND_WINO, (ci, ci, cip, cip, int(flip), tile),
-                                             c0.weight, (tile + 2) ** 2 * cip * cip, torch.float32)
+                                             c0.weight, (tile + 2) ** 2 * cip * cip, torch.float32,
+                                             amax=am)
             else:
                 for mode in modes:
                     pb.t[("w1", mode)] = add(pk, (ci, ci, 9, cip, cip, mode), c0.weight,
@@ -142,6 +160,7 @@ class StepWeights:
         return len(ps) == len(self.ptrs) and all(p.data_ptr() == q for p, q in zip(ps, self.ptrs))
 
     def run(self):
+        self.amax.zero_()
         call("nsm_prep_weights", ptr(self.table), self.njobs, self.total, stream())
 
     def block(self, k):

@@ -419,7 +419,18 @@ def _masks_for(mod, B, device, training):
 
 class _BlockSaved:
     __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop", "V", "A1",
-                 "pw", "Z")
+                 "pw", "Z", "am")
+
+
+def _slot(am, i):
+    """Slot i of a block's operand-maximum slots (V, Vd, dM), or None."""
+    return ops.amax_slot(am, i)
+
+
+def _block_slots(amax, k):
+    """Block k's three operand-maximum slots of the step's buffer, or None."""
+    w = ops.AMAX_WORDS
+    return None if amax is None else amax[3 * k * w:(3 * k + 3) * w]
 
 
 def fuses_resize(blk, dtype):
@@ -429,7 +440,7 @@ def fuses_resize(blk, dtype):
             and ops.pad32(blk.conv[0].in_channels) >= WINOGRAD_MIN_CHANNELS)
 
 
-def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res):
+def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
     """Eval: both convs with BN (running statistics) + LeakyReLU (+ the skip
     add) in their epilogues — nothing but A1 and the block output is stored."""
     c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
@@ -441,7 +452,8 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res):
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         tile = wino_tile(cip, H, W)
         A1 = ops.conv3x3_wino(xin, B, H, W, pw.U1(tile, False), b1, cip, tile=tile,
-                              tag=name + ".conv.0.fwd", src_hw=src_hw, act=(bn1, None))
+                              tag=name + ".conv.0.fwd", src_hw=src_hw, act=(bn1, None),
+                              amax_v=_slot(am, 0), amax_u=pw.amax_U1(False))
     else:
         assert src_hw is None
         A1 = ops.conv_fwd_act(xin, B, H, W, pw.w1(ops.PACK_FWD), b1, cip, 3, bn1, slope=SLOPE,
@@ -453,17 +465,20 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res):
     s.X = s.Y1 = s.Y2 = s.mask = s.V = s.A1 = None
     s.bn1, s.bn2, s.pw, s.Z = bn1, bn2, pw, Z
     s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
+    s.am = am
     return s
 
 
 def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse_out=False,
-               res=None):
+               res=None, am=None):
     """pw: the block's weight layouts (prep.StepWeights.block, all written by the
     step's single preparation launch), or None to build them here per call.
     src=(x_low, hi, wi): X is the bilinear resize of x_low to H x W, sampled
     inside the Winograd input transform (X is None then; fuses_resize).
     fuse_out (eval, EVAL_FUSED): the block output lrelu(bn2(Y2)) (+ res) is
-    produced by the convs' epilogues, returned as s.Z (Y1/Y2 not stored)."""
+    produced by the convs' epilogues, returned as s.Z (Y1/Y2 not stored).
+    am: the block's 3 zeroed int32 slots for max|V|, max|Vd|, max|dM| (the
+    Winograd GEMMs' f16x2 operand scales), or None (bf16 split)."""
     c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
     ci, co = c0.in_channels, c4.out_channels
     cip, cop = ops.pad32(ci), ops.pad32(co)
@@ -475,7 +490,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     if pw is None:
         pw = LazyBlockWeights(blk, dtype)
     if fuse_out and not training and EVAL_FUSED:
-        return _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res)
+        return _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am)
     b1 = pw.vec("b1")
     V = None
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
@@ -486,10 +501,12 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
             # the output transform also writes the BN batch-statistics partials
             Y1, V, part1 = ops.conv3x3_wino(xin, B, H, W, U1, b1, cip, tile=tile,
                                             tag=name + ".conv.0.fwd", keep_v=True, stats=True,
-                                            src_hw=src_hw)
+                                            src_hw=src_hw, amax_v=_slot(am, 0),
+                                            amax_u=pw.amax_U1(False))
         else:
             Y1, V = ops.conv3x3_wino(xin, B, H, W, U1, b1, cip, tile=tile,
-                                     tag=name + ".conv.0.fwd", keep_v=True, src_hw=src_hw)
+                                     tag=name + ".conv.0.fwd", keep_v=True, src_hw=src_hw,
+                                     amax_v=_slot(am, 0), amax_u=pw.amax_U1(False))
         if training and part1 is None:
             part1 = ops.bn_partials(Y1)
     else:
@@ -525,6 +542,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     s.V = V if training else None  # Winograd-domain input, reused by the weight gradient
     s.A1 = A1 if training else None  # activated 1x1 operand, reused by its weight gradient
     s.Z = None
+    s.am = am
     return s
 
 
@@ -564,12 +582,15 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         dM = None
         if need_dx and DUAL_TRANSFORM:
             # dY1's two Winograd transforms (dgrad input, wgrad) from one read
+            am2 = (_slot(s.am, 1), _slot(s.am, 2))
             if isinstance(dY1, ops.DeferredBnBwd):
-                Vd, dM = ops.wino_dual_input_bn(dY1, s.Y1, s.bn1, s.mask, B, H, W, tile=tile)
+                Vd, dM = ops.wino_dual_input_bn(dY1, s.Y1, s.bn1, s.mask, B, H, W, tile=tile,
+                                                amax=am2)
             else:
-                Vd, dM = ops.wino_dual_input(dY1, B, H, W, tile=tile)
+                Vd, dM = ops.wino_dual_input(dY1, B, H, W, tile=tile, amax=am2)
         ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=tile,
-                               tag=name + ".conv.0.wgrad", dM=dM)
+                               tag=name + ".conv.0.wgrad", dM=dM,
+                               amax=(_slot(s.am, 2), _slot(s.am, 0)))
         s.V = None
     else:
         ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
@@ -579,7 +600,8 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         tile = wino_tile(s.cip, H, W)
         U1d = s.pw.U1(tile, True)
         return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=tile,
-                                tag=name + ".conv.0.dgrad", v_in=Vd)
+                                tag=name + ".conv.0.dgrad", v_in=Vd, amax_v=_slot(s.am, 1),
+                                amax_u=s.pw.amax_U1(True))
     w1d = s.pw.w1(ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
 
@@ -634,13 +656,17 @@ class _UnetFn(torch.autograd.Function):
         X = ops.input_prep(x32, cin_p, cdt)
         masks = _masks_for(mod, B, dev, training)
         sw = _step_weights(mod, cdt, Rh, Rw, training)
+        # per-step maxima of the Winograd GEMM operands V, Vd, dM of every block
+        # (their producers fill them; zeroed here, one launch)
+        amax = ops.amax_slots(3 * 10, dev) if sw else None
 
         saved, c, shapes = {}, {}, {}
         inp, h, w = X, Rh, Rw
         for k in ENCODER:
             with ops.stage(f"conv{k}.fwd"):
                 s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}",
-                               pw=sw.block(k) if sw else None, fuse_out=True)
+                               pw=sw.block(k) if sw else None, fuse_out=True,
+                               am=_block_slots(amax, k))
                 saved[k], shapes[k] = s, (h, w)
                 if s.Z is not None:
                     c[k] = s.Z
@@ -680,7 +706,8 @@ class _UnetFn(torch.autograd.Function):
                 ups[k] = (h, w, h2, w2, th, tw)
                 res = c[SKIP_OF[k]] if k in SKIP_OF else None
                 s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}",
-                               pw=sw.block(k) if sw else None, src=src, fuse_out=True, res=res)
+                               pw=sw.block(k) if sw else None, src=src, fuse_out=True, res=res,
+                               am=_block_slots(amax, k))
                 saved[k] = s
                 if s.Z is not None:
                     cur = s.Z

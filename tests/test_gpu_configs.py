@@ -88,7 +88,7 @@ def test_configs1_b8_fp32_train_step_vs_oracle(device):
                   loss_rel=abs(loss.item() - lo.item()) / lo.item(), loss_bound=LOSS_REL,
                   worst_grad_rel_l2=[[k, e] for e, k in sorted(worst, reverse=True)[:5]],
                   grad_bound=GRAD_REL_L2, x_grad_rel_l2=xg,
-                  f32_split=__import__("os").environ.get("NSM_F32_SPLIT", "1"))
+                  f32_split=__import__("os").environ.get("NSM_F32_SPLIT", "2"))
     assert xg <= GRAD_REL_L2
     msd = m.state_dict()
     for k, v in sd.items():

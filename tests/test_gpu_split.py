@@ -1,7 +1,9 @@
-"""GPU: the fp32 GEMMs of the Winograd layers on the bf16 matrix cores by the
-exact three-way split (csrc/nsm_conv_split.inc) carry fp32 accuracy: against a
-float64 convolution their error stays within that of the v_mfma_f32_32x32x2_f32
-path on the same inputs (both modes through the C ABI, same seeded data)."""
+"""GPU: the fp32 GEMMs of the Winograd layers on the 16-bit matrix cores carry
+fp32 accuracy — the exact three-way bf16 split (csrc/nsm_conv_split.inc, mode
+1) and the f16x2 split of power-of-two scaled operands (nsm_conv_split16.inc,
+mode 2, operand maxima recorded by the producers): against a float64
+convolution their error stays within that of the v_mfma_f32_32x32x2_f32 path
+on the same inputs (all modes through the C ABI, same seeded data)."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -21,7 +23,7 @@ def nchw(y, B, H, W):
 @pytest.fixture(scope="module")
 def ops(device):
     from nsm_amd import ops as O
-    prev = O.set_f32_split(1)
+    prev = O.set_f32_split(2)
     yield O
     O.set_f32_split(prev)
 
@@ -45,24 +47,37 @@ def test_split_matches_fp32_accuracy(ops, device, B, H, W, ci, co, tile):
     ref.backward(dy)
     xs, ws, dys = x.detach().float(), w.detach().float(), dy.float()
     res = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         ops.set_f32_split(mode)
+        # mode 2: the operands' maxima as the model path records them (the
+        # transforms fill V / Vd / dM slots, the weights' from nsm_absmax)
+        am = ops.amax_slots(3, device) if mode == 2 else None
+        sl = (lambda i: ops.amax_slot(am, i)) if mode == 2 else (lambda i: None)
         U = ops.wino_weight(ws.to(device), co, ci, flip=False, tile=tile)
-        y, V = ops.conv3x3_wino(nhwc(xs).to(device), B, H, W, U, None, co, tile=tile, keep_v=True)
+        y, V = ops.conv3x3_wino(nhwc(xs).to(device), B, H, W, U, None, co, tile=tile, keep_v=True,
+                                amax_v=sl(0), amax_u=ops.absmax(U) if mode == 2 else None)
         Ud = ops.wino_weight(ws.to(device), ci, co, flip=True, tile=tile)
-        dx = ops.conv3x3_wino(nhwc(dys).to(device), B, H, W, Ud, None, ci, tile=tile)
+        dyd = nhwc(dys).to(device)
+        Vd, dM = ops.wino_dual_input(dyd, B, H, W, tile=tile, amax=(sl(1), sl(2)))
+        dx = ops.conv3x3_wino(dyd, B, H, W, Ud, None, ci, tile=tile, v_in=Vd, amax_v=sl(1),
+                              amax_u=ops.absmax(Ud) if mode == 2 else None)
         dw = torch.empty(co, ci, 3, 3, device=device)
-        ops.conv3x3_wgrad_wino(nhwc(dys).to(device), V, B, H, W, ci, ci, co, dw, tile=tile)
+        ops.conv3x3_wgrad_wino(dyd, V, B, H, W, ci, ci, co, dw, tile=tile, dM=dM,
+                               amax=(sl(2), sl(0)))
         res[mode] = (_errs(nchw(y.cpu(), B, H, W), ref.detach()),
                      _errs(nchw(dx.cpu(), B, H, W), x.grad),
                      _errs(dw.cpu(), w.grad))
-    ops.set_f32_split(1)
+    ops.set_f32_split(2)
     for i, name in enumerate(("fwd", "dgrad", "wgrad")):
-        (m0, r0), (m1, r1) = res[0][i], res[1][i]
-        print(f"F({tile}) {name}: fp32-MFMA max {m0:.2e} rms {r0:.2e} | split max {m1:.2e} rms {r1:.2e}")
-        # the Winograd transforms dominate both; the GEMM arithmetic must not add error
-        assert r1 <= 1.25 * r0 + 1e-9, (name, r0, r1)
-        assert m1 <= 1.5 * m0 + 1e-8, (name, m0, m1)
+        (m0, r0), (m1, r1), (m2, r2) = res[0][i], res[1][i], res[2][i]
+        print(f"F({tile}) {name}: fp32-MFMA max {m0:.2e} rms {r0:.2e} | bf16 split max {m1:.2e} "
+              f"rms {r1:.2e} | f16x2 max {m2:.2e} rms {r2:.2e}")
+        # the Winograd transforms dominate all; the GEMM arithmetic must not add
+        # error: rms within 1.25x of the fp32 MFMA's; the max (a statistic of a
+        # few elements at these sizes) within 2x
+        for m, r in ((m1, r1), (m2, r2)):
+            assert r <= 1.25 * r0 + 1e-9, (name, r0, r)
+            assert m <= 2.0 * m0 + 1e-8, (name, m0, m)
 
 
 @pytest.mark.parametrize("B,H,W,ci,co,k", [(2, 16, 16, 32, 64, 3), (2, 24, 20, 64, 128, 1),
@@ -88,7 +103,7 @@ def test_split_direct_convs(ops, device, B, H, W, ci, co, k):
         ops.conv_wgrad(nhwc(dys).to(device), nhwc(xs).to(device), B, H, W, k, ci, co, dw)
         res[mode] = (_errs(nchw(y.cpu(), B, H, W), ref.detach()), _errs(nchw(dx.cpu(), B, H, W), x.grad),
                      _errs(dw.cpu(), w.grad))
-    ops.set_f32_split(1)
+    ops.set_f32_split(2)
     for i, name in enumerate(("fwd", "dgrad", "wgrad")):
         (m0, r0), (m1, r1) = res[0][i], res[1][i]
         print(f"direct k{k} {name}: fp32-MFMA max {m0:.2e} rms {r0:.2e} | split max {m1:.2e} rms {r1:.2e}")
@@ -109,7 +124,7 @@ def test_split_train_step_vs_oracle(ops, device):
     oo, _ = O.forward(sd, xo, True, None, 0.0)
     O.custom_loss(oo, torch.from_numpy(y_np), 0.9).backward()
     errs = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         ops.set_f32_split(mode)
         m = Unet(in_ch=7, dropout_rate=0.0)
         m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in np_sd.items()})
@@ -120,8 +135,10 @@ def test_split_train_step_vs_oracle(ops, device):
         ge = max(((p.grad.cpu().double() - sd[k].grad.double()).norm() / sd[k].grad.double().norm()).item()
                  for k, p in m.named_parameters() if not k.endswith("bias"))
         errs[mode] = ((out.detach().cpu() - oo.detach()).abs().max().item(), ge)
-    ops.set_f32_split(1)
+    ops.set_f32_split(2)
     print(f"train step vs oracle: fp32-MFMA out {errs[0][0]:.2e} grad {errs[0][1]:.2e} | "
-          f"split out {errs[1][0]:.2e} grad {errs[1][1]:.2e}")
-    assert errs[1][0] <= 2.0 * errs[0][0] + 1e-6
-    assert errs[1][1] <= 2.0 * errs[0][1] + 1e-6
+          f"bf16 split out {errs[1][0]:.2e} grad {errs[1][1]:.2e} | "
+          f"f16x2 out {errs[2][0]:.2e} grad {errs[2][1]:.2e}")
+    for mode in (1, 2):
+        assert errs[mode][0] <= 2.0 * errs[0][0] + 1e-6
+        assert errs[mode][1] <= 2.0 * errs[0][1] + 1e-6

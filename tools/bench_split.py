@@ -36,7 +36,7 @@ for (B, H, W, ci, co) in shapes:
                                                  ptr(Mb), stream())),
                          ("wgrad", lambda: call("nsm_conv3x3_wgrad_wino_dm", ptr(dM), ptr(V), B, H, W,
                                                   ci, co, ci, co, tile, ptr(dw), ptr(ws), ws.numel(),
-                                                  stream()))):
+                                                  None, None, stream()))):
             if ONLY and name != ONLY:
                 continue
             for _ in range(3):

@@ -43,9 +43,8 @@ for (B, H, W, ci, co) in shapes:
     V = (torch.randn(nb, T, ci, device=dev, generator=g) * cs).reshape(-1).contiguous()
     U = (torch.randn(nb, co, ci, device=dev, generator=g) * 0.03).reshape(-1).contiguous()
     Mb = torch.empty(nb * T * co, device=dev)
-    amax = torch.zeros(2, dtype=torch.int32, device=dev)
-    call("nsm_absmax", ptr(V), V.numel(), ptr(amax[0:1]), stream())
-    call("nsm_absmax", ptr(U), U.numel(), ptr(amax[1:2]), stream())
+    amax = ops.amax_slots(2, dev)
+    av, au = ops.absmax(V, ops.amax_slot(amax, 0)), ops.absmax(U, ops.amax_slot(amax, 1))
     flop = 2.0 * nb * T * ci * co
     res, acc = [], []
     for name, mode, fn in (
@@ -54,7 +53,7 @@ for (B, H, W, ci, co) in shapes:
             ("bf16x3", 1, lambda: call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, ci, co, t,
                                        ptr(Mb), stream())),
             ("f16x2", 1, lambda: call("nsm_wino_gemm_s", ptr(V), ptr(U), B, H, W, ci, co, t,
-                                      ptr(Mb), ptr(amax), stream()))):
+                                      ptr(Mb), ptr(av), ptr(au), stream()))):
         ops.set_f32_split(mode)
         ms = timeit(fn)
         res.append(f"{name} {ms:.3f} ms {6 if name == 'bf16x3' else 3 if name == 'f16x2' else 1}x"

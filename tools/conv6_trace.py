@@ -24,7 +24,7 @@ def grid_blocks(r):
 # default there) grid 8x8x64 blocks, F(4x4) 16x8x36
 CONV6_GRIDS = ((8, 8, 64), (16, 8, 36))
 KINDS = {
-    "f32": (lambda r: ("gemm_f32_kernel" in r["Kernel_Name"] or "gemm_f32s_kernel" in r["Kernel_Name"])
+    "f32": (lambda r: any(k in r["Kernel_Name"] for k in ("gemm_f32_kernel", "gemm_f32s_kernel", "gemm_f32h_kernel"))
             and r["Kernel_Name"].count("RowsKLoader<128, 256>") == 2
             and grid_blocks(r) in CONV6_GRIDS, True),
     "bf16": (lambda r: "gemm_bf16_dma_kernel<256, 256" in r["Kernel_Name"]

@@ -23,7 +23,7 @@ from stage_pmc import CODES, is_mark, load_pmc  # noqa: E402
 
 B8_CONV6 = 8 * 64 * 64
 F32_GEMM = lambda n: (n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n  # noqa: E731
-                      and ("gemm_f32_kernel" in n or "gemm_f32s_kernel" in n))
+                      and any(k in n for k in ("gemm_f32_kernel", "gemm_f32s_kernel", "gemm_f32h_kernel")))
 KINDS = {
     "f32_gemm": dict(match=F32_GEMM, grid=8 * 8 * 64 * 256, triple=False,
                      alg=64 * (2 * 968 * 1024 + 1024 * 1024) * 4,
