@@ -101,7 +101,10 @@ int nsm_conv_stat_rows(int B, int H, int W, int cout_p);
 int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, int cin_p, const float* wpk,
                        const float* bias, int cout_p, int ksize, float* y, int ldy,
                        const float* pro_scale, const float* pro_shift, const float* pro_mask,
-                       float slope, float* stats, void* stream);
+                       float slope, float* stats, const uint32_t* amax_x, const uint32_t* amax_w,
+                       void* stream);
+/* amax_x / amax_w (device operand-maximum slots of x and wpk, both or neither;
+ * ignored with a prologue): the GEMM runs the f16x2 split (NSM_F32_SPLIT=2). */
 
 /* Winograd F(m x m, 3x3) 3x3 convolution (same padding 1) for deep layers,
  * tile m in {2, 4, 6}, alpha = m + 2, T = B*ceil(H/m)*ceil(W/m) tiles:
@@ -207,7 +210,7 @@ size_t nsm_conv_wgrad_ws(int B, int H, int W, int cin_p, int cout_p, int ksize);
 int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx, int B, int H, int W,
                    int cin_p, int cout_p, int ksize, const float* pro_scale, const float* pro_shift,
                    const float* pro_mask, float slope, float* ws, size_t ws_floats, int cin, int cout,
-                   float* dw, void* stream);
+                   float* dw, const uint32_t* amax_dy, const uint32_t* amax_x, void* stream);
 
 /* ---- BatchNorm2d(eps, momentum) train/eval (Unetmodel.py:22,27) ----------- */
 int nsm_reduce_chunks(int M, int C); /* partial-buffer rows for the two below */
@@ -239,7 +242,7 @@ int nsm_bn_finalize_eval(const float* run_mean, const float* run_var, const floa
  * none), fused with the additive skip (Unetmodel.py:125,131,137) */
 int nsm_bn_act(const void* y, int ldy, int M, int C, const float* scale, const float* shift,
                float slope, const float* mask, int HW, const void* res, int ldres, void* out,
-               int ldo, int dtype, void* stream);
+               int ldo, int dtype, uint32_t* amax, void* stream);
 /* backward of  z = lrelu(mask * ... ) chains around a train-mode BN:
  *   dz = g * mask[b][c] * lrelu'(y*scale+shift); partial {sum dz, sum dz*xhat}. */
 int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy, int M, int C, int HW,
@@ -259,7 +262,9 @@ int nsm_sum_rows(const float* part, int nrows, int width, int group, float* out,
 int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, int M, int C, int HW,
                      const float* scale, const float* shift, float slope, const float* mask,
                      const float* mean, const float* coef, void* dy, int lddy, int dtype,
-                     void* stream);
+                     uint32_t* amax, void* stream);
+/* amax (bn_act, bn_bwd_apply; fp32 only, may be NULL): the operand-maximum
+ * slot receiving max|out| / max|dy| for the f16x2 GEMM that consumes it. */
 
 /* ---- resampling -------------------------------------------------------------
  * AvgPool2d(2) (Unetmodel.py:40,43,46): floor mode. bwd: dx = skip + dy/4. */
@@ -447,6 +452,7 @@ int nsm_conv1x1_dgrad_bnbwd(const void* dy2, int lddy2, int B, int H, int W, int
                             const float* scale, const float* shift, const float* mean,
                             const float* invstd, const float* mask, float slope, int mode,
                             float* partial, const float* coef, void* out, int ldo, int dtype,
+                            const uint32_t* amax_dy2, const uint32_t* amax_w,
                             void* stream);
 int nsm_conv1x1_bnbwd_chunks(int B, int H, int W, int cip, int dtype);
 /* rows per BN-partial chunk of nsm_conv_fwd_bf16 (its M tile) */

@@ -784,14 +784,17 @@ __global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_
 // ---------------------------------------------------------------------------
 // Host launchers
 // ---------------------------------------------------------------------------
+// amax: the operands' maxima (f16x2 split); a prologue (PRO) transforms the
+// operand after its producer recorded the maximum, so it runs the bf16 split
 template <int BM, int BN, int WM, int WN, bool PRO, class EP = EpiStore>
 static int launch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const typename EP::P& ep, int M,
-                           int N, int K, hipStream_t s) {
+                           int N, int K, hipStream_t s, AmaxPair amax = AmaxPair{}) {
   constexpr int NT = WM * WN * 64;
   using AL = ConvActLoader<BM, NT, PRO>;
   using BL = RowsKLoader<BN, NT>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), 1);
-  launch_f32_gemm<BM, BN, WM, WN, AL, BL, EP, ConvActP, RowsKP>(grid, s, ap, bp, ep, M, N, K, K, 1);
+  launch_f32_gemm<BM, BN, WM, WN, AL, BL, EP, ConvActP, RowsKP>(grid, s, ap, bp, ep, M, N, K, K, 1,
+                                                                PRO ? AmaxPair{} : amax);
   NSM_LAUNCH_CHECK("conv_fwd");
   return 0;
 }
@@ -832,38 +835,39 @@ static int conv_fwd_bm_f(long long M, int N) {
 
 template <bool PRO, class EP = EpiStore>
 static int dispatch_conv_fwd(const ConvActP& ap, const RowsKP& bp, const typename EP::P& ep, int M,
-                             int N, int K, hipStream_t s) {
+                             int N, int K, hipStream_t s, AmaxPair amax = AmaxPair{}) {
   // Tile choice: 128x128 (2x2 waves of 64x64) wherever N allows; narrower N
   // tiles for the 32/64-channel layers; BM=64 when the grid would not cover
   // the 256 CUs twice.
   long long mb128 = ceil_div(M, 128);
   if (N >= 128) {
     if (mb128 * ceil_div(N, 128) >= 512)
-      return launch_conv_fwd<128, 128, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
-    return launch_conv_fwd<64, 128, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
+      return launch_conv_fwd<128, 128, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s, amax);
+    return launch_conv_fwd<64, 128, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s, amax);
   }
   if (N >= 64) {
     if (n64_bm256() && mb128 >= 4096 && N == 64)
-      return launch_conv_fwd<256, 64, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
+      return launch_conv_fwd<256, 64, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s, amax);
     if (mb128 * ceil_div(N, 64) >= 512)
-      return launch_conv_fwd<128, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
-    return launch_conv_fwd<64, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s);
+      return launch_conv_fwd<128, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s, amax);
+    return launch_conv_fwd<64, 64, 2, 2, PRO, EP>(ap, bp, ep, M, N, K, s, amax);
   }
   if (n32_bm256() && mb128 >= 4096)
-    return launch_conv_fwd<256, 32, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
-  if (mb128 >= 512) return launch_conv_fwd<128, 32, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
-  return launch_conv_fwd<64, 32, 2, 1, PRO, EP>(ap, bp, ep, M, N, K, s);
+    return launch_conv_fwd<256, 32, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s, amax);
+  if (mb128 >= 512) return launch_conv_fwd<128, 32, 4, 1, PRO, EP>(ap, bp, ep, M, N, K, s, amax);
+  return launch_conv_fwd<64, 32, 2, 1, PRO, EP>(ap, bp, ep, M, N, K, s, amax);
 }
 
 template <int BM, int BN, int WM, int WN, bool SHIFT, bool PRO>
 static int launch_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& ep, int M, int N,
-                        int K, int kchunk, int splits, hipStream_t s) {
+                        int K, int kchunk, int splits, hipStream_t s, AmaxPair amax) {
   constexpr int NT = WM * WN * 64;
   using AL = PixRowsLoader<BM, NT, false, false>;
   using BL = PixRowsLoader<BN, NT, SHIFT, PRO>;
   dim3 grid(ceil_div(M, BM), ceil_div(N, BN), splits);
   launch_f32_gemm<BM, BN, WM, WN, AL, BL, EpiSlabV, PixRowsP, PixRowsP>(grid, s, ap, bp, ep, M, N, K,
-                                                                        kchunk, splits);
+                                                                        kchunk, splits,
+                                                                        PRO ? AmaxPair{} : amax);
   NSM_LAUNCH_CHECK("conv_wgrad");
   return 0;
 }
@@ -871,10 +875,10 @@ static int launch_wgrad(const PixRowsP& ap, const PixRowsP& bp, const EpiSlabP& 
 template <bool SHIFT, bool PRO>
 static int dispatch_wgrad(int BM, int BN, const PixRowsP& ap, const PixRowsP& bp,
                           const EpiSlabP& ep, int M, int N, int K, int kchunk, int splits,
-                          hipStream_t s) {
+                          hipStream_t s, AmaxPair amax = AmaxPair{}) {
 #define NSM_WG(bm, bn, wm, wn) \
   if (BM == bm && BN == bn)    \
-    return launch_wgrad<bm, bn, wm, wn, SHIFT, PRO>(ap, bp, ep, M, N, K, kchunk, splits, s);
+    return launch_wgrad<bm, bn, wm, wn, SHIFT, PRO>(ap, bp, ep, M, N, K, kchunk, splits, s, amax);
   NSM_WG(128, 128, 2, 2)
   NSM_WG(128, 64, 2, 2)
   NSM_WG(128, 32, 4, 1)
@@ -1805,7 +1809,7 @@ extern "C" int nsm_conv_fwd(const float* x, int ldx, int B, int H, int W, int ci
                             int ldy, const float* pro_scale, const float* pro_shift,
                             const float* pro_mask, float slope, void* stream) {
   return nsm_conv_fwd_stats(x, ldx, B, H, W, cin_p, wpk, bias, cout_p, ksize, y, ldy, pro_scale,
-                            pro_shift, pro_mask, slope, nullptr, stream);
+                            pro_shift, pro_mask, slope, nullptr, nullptr, nullptr, stream);
 }
 
 extern "C" int nsm_conv_stat_rows(int B, int H, int W, int cout_p) {
@@ -1816,7 +1820,8 @@ extern "C" int nsm_conv_stat_rows(int B, int H, int W, int cout_p) {
 extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, int cin_p,
                                   const float* wpk, const float* bias, int cout_p, int ksize,
                                   float* y, int ldy, const float* pro_scale, const float* pro_shift,
-                                  const float* pro_mask, float slope, float* stats, void* stream) {
+                                  const float* pro_mask, float slope, float* stats,
+                                  const uint32_t* amax_x, const uint32_t* amax_w, void* stream) {
   NSM_CHECK_ARG(x && wpk && y, "conv_fwd: null pointer");
   NSM_CHECK_ARG(B > 0 && H > 0 && W > 0, "conv_fwd: bad shape");
   NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0, "conv_fwd: channels must be multiples of 32");
@@ -1847,7 +1852,7 @@ extern "C" int nsm_conv_fwd_stats(const float* x, int ldx, int B, int H, int W, 
   EpiStoreP ep{y, ldy, bias, stats, 0, nullptr, nullptr, 0.f, nullptr, 0, f32_epi_vec()};
   hipStream_t s = as_stream(stream);
   if (pro_scale) return dispatch_conv_fwd<true>(ap, bp, ep, (int)Ml, cout_p, K, s);
-  return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s);
+  return dispatch_conv_fwd<false>(ap, bp, ep, (int)Ml, cout_p, K, s, AmaxPair{amax_x, amax_w});
 }
 
 static int conv_fwd_act_f32(const float* x, int ldx, int B, int H, int W, int cin_p,
@@ -1887,7 +1892,7 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
                               int W, int cin_p, int cout_p, int ksize, const float* pro_scale,
                               const float* pro_shift, const float* pro_mask, float slope,
                               float* ws, size_t ws_floats, int cin, int cout, float* dw,
-                              void* stream) {
+                              const uint32_t* amax_dy, const uint32_t* amax_x, void* stream) {
   NSM_CHECK_ARG(dy && x && ws && dw, "conv_wgrad: null pointer");
   NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0, "conv_wgrad: channels must be x32");
   NSM_CHECK_ARG(ksize == 1 || ksize == 3, "conv_wgrad: ksize %d", ksize);
@@ -1928,12 +1933,15 @@ extern "C" int nsm_conv_wgrad(const float* dy, int lddy, const float* x, int ldx
   EpiSlabP ep{ws, f32_epi_vec()};
   hipStream_t s = as_stream(stream);
   int rc;
+  const AmaxPair am{amax_dy, amax_x};
   if (ksize == 3)
-    rc = dispatch_wgrad<true, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
+    rc = dispatch_wgrad<true, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s,
+                                     am);
   else if (pro_scale)
     rc = dispatch_wgrad<false, true>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
   else
-    rc = dispatch_wgrad<false, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits, s);
+    rc = dispatch_wgrad<false, false>(pl.BM, pl.BN, ap, bp, ep, M, N, (int)Kl, pl.kchunk, pl.splits,
+                                      s, am);
   if (rc) return rc;
   return wgrad_finish(ws, pl, M, N, cin_p, ksize * ksize, cin, cout, dw, s);
 }

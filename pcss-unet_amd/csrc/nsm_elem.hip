@@ -254,18 +254,25 @@ __global__ void __launch_bounds__(256) bn_act_kernel(const T* __restrict__ y, in
                                                      const float* __restrict__ shift, float slope,
                                                      const float* __restrict__ mask,
                                                      const T* __restrict__ res, int ldres,
-                                                     T* __restrict__ out, int ldo) {
+                                                     T* __restrict__ out, int ldo,
+                                                     uint32_t* __restrict__ amax) {
   const int ppb = blockDim.x / C8, tp = threadIdx.x / C8;
   const int c = (threadIdx.x - tp * C8) * 8;
   const F8 sc = ldf8(scale + c), sh = ldf8(shift + c);
   const int pstep = gridDim.x * ppb;
+  uint32_t am = 0;  // max|out| (an f16x2 GEMM operand scale, fp32 only)
   for (int p = blockIdx.x * ppb + tp; p < M; p += pstep) {
     F8 o = lrelu8(ld8(y + (size_t)p * ldy + c) * sc + sh, slope);
     // Dropout2d after the LeakyReLU (Unetmodel.py:23-24)
     if (mask) o = o * ld8(mask + (size_t)fdiv((uint32_t)p, fdHW) * (C8 * 8) + c);
     if (res) o += ld8(res + (size_t)p * ldres + c);
     st8(out + (size_t)p * ldo + c, o);
+    if (amax) {
+      amax_fold(am, o.a);
+      amax_fold(am, o.b);
+    }
   }
+  amax_flush(am, amax);
 }
 
 // dz = g * mask[b][c] * lrelu'(y*scale+shift)
@@ -361,19 +368,26 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
     const T* __restrict__ g, int ldg, const T* __restrict__ y, int ldy, int M, int C, int C8,
     FastDiv fdHW, const float* __restrict__ scale, const float* __restrict__ shift, float slope,
     const float* __restrict__ mask, const float* __restrict__ mean,
-    const float* __restrict__ coef, T* __restrict__ dy, int lddy) {
+    const float* __restrict__ coef, T* __restrict__ dy, int lddy, uint32_t* __restrict__ amax) {
   const int ppb = blockDim.x / C8, tp = threadIdx.x / C8;
   const int c = (threadIdx.x - tp * C8) * 8;
   const F8 sc = ldf8(scale + c), sh = ldf8(shift + c), mu = ldf8(mean + c);
   const F8 k1 = ldf8(coef + c), k2 = ldf8(coef + C + c), k3 = ldf8(coef + 2 * C + c);
   const int pstep = gridDim.x * ppb;
+  uint32_t am = 0;  // max|dy| (an f16x2 GEMM operand scale, fp32 only)
   for (int p = blockIdx.x * ppb + tp; p < M; p += pstep) {
     const F8 v = ld8(y + (size_t)p * ldy + c);
     const F8 gg = ld8(g + (size_t)p * ldg + c);
     const int b = mask ? (int)fdiv((uint32_t)p, fdHW) : 0;
     const F8 dz = bn_dz8(gg, v, sc, sh, slope, mask, b, C, c);
-    st8(dy + (size_t)p * lddy + c, k1 * dz + k2 * (v - mu) + k3);
+    const F8 d = k1 * dz + k2 * (v - mu) + k3;
+    st8(dy + (size_t)p * lddy + c, d);
+    if (amax) {
+      amax_fold(am, d.a);
+      amax_fold(am, d.b);
+    }
   }
+  amax_flush(am, amax);
 }
 
 // BN-backward reduction fused into the kernel that PRODUCES a block output's
@@ -1860,7 +1874,7 @@ static void pix_launch(long long M, int C8, dim3& grid, dim3& block) {
 extern "C" int nsm_bn_act(const void* y, int ldy, int M, int C, const float* scale,
                           const float* shift, float slope, const float* mask, int HW,
                           const void* res, int ldres, void* out, int ldo, int dtype,
-                          void* stream) {
+                          uint32_t* amax, void* stream) {
   NSM_CHECK_ARG(y && scale && shift && out && C % 8 == 0 && C <= 2048 && ldy % 8 == 0 &&
                     ldo % 8 == 0 && (!res || ldres % 8 == 0) && (!mask || HW > 0),
                 "bn_act: bad args");
@@ -1872,11 +1886,11 @@ extern "C" int nsm_bn_act(const void* y, int ldy, int M, int C, const float* sca
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(bn_act_kernel<bf16_t>, g, b, 0, as_stream(stream), NSM_CT(bf16_t, y), ldy,
                        M, C / 8, fh, scale, shift, slope, mask, NSM_CT(bf16_t, res), ldres,
-                       NSM_T(bf16_t, out), ldo);
+                       NSM_T(bf16_t, out), ldo, nullptr);
   else
     hipLaunchKernelGGL(bn_act_kernel<float>, g, b, 0, as_stream(stream), NSM_CT(float, y), ldy, M,
                        C / 8, fh, scale, shift, slope, mask, NSM_CT(float, res), ldres,
-                       NSM_T(float, out), ldo);
+                       NSM_T(float, out), ldo, amax);
   NSM_LAUNCH_CHECK("bn_act");
   return 0;
 }
@@ -1916,7 +1930,7 @@ extern "C" int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int 
 extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, int M, int C,
                                 int HW, const float* scale, const float* shift, float slope,
                                 const float* mask, const float* mean, const float* coef, void* dy,
-                                int lddy, int dtype, void* stream) {
+                                int lddy, int dtype, uint32_t* amax, void* stream) {
   NSM_CHECK_ARG(g && y && scale && shift && mean && coef && dy && C % 8 == 0 && C <= 2048 &&
                     ldg % 8 == 0 && ldy % 8 == 0 && lddy % 8 == 0 && (!mask || HW > 0),
                 "bn_bwd_apply: bad args");
@@ -1928,11 +1942,11 @@ extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, 
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, gr, b, 0, as_stream(stream),
                        NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, C / 8, fh, scale,
-                       shift, slope, mask, mean, coef, NSM_T(bf16_t, dy), lddy);
+                       shift, slope, mask, mean, coef, NSM_T(bf16_t, dy), lddy, nullptr);
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, gr, b, 0, as_stream(stream),
                        NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, C / 8, fh, scale,
-                       shift, slope, mask, mean, coef, NSM_T(float, dy), lddy);
+                       shift, slope, mask, mean, coef, NSM_T(float, dy), lddy, amax);
   NSM_LAUNCH_CHECK("bn_bwd_apply");
   return 0;
 }

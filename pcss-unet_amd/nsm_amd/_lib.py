@@ -28,7 +28,7 @@ _SIGS = {
     "nsm_pad_vec": (I, [P, I, I, P, P]),
     "nsm_conv_fwd": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P]),
     "nsm_conv_stat_rows": (I, [I, I, I, I]),
-    "nsm_conv_fwd_stats": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
+    "nsm_conv_fwd_stats": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P, P, P]),
     "nsm_wino_ws": (Z, [I, I, I, I, I, I]),
     "nsm_wino_weight": (I, [P, I, I, I, I, I, I, P, P]),
     "nsm_conv3x3_wino": (I, [P, I, I, I, I, I, P, P, I, I, I, P, I, P, Z, P]),
@@ -41,17 +41,17 @@ _SIGS = {
     "nsm_wino_wgrad_ws": (Z, [I, I, I, I, I, I]),
     "nsm_conv3x3_wgrad_wino": (I, [P, I, P, I, I, I, I, I, I, I, I, P, P, Z, P]),
     "nsm_conv_wgrad_ws": (Z, [I, I, I, I, I, I]),
-    "nsm_conv_wgrad": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
+    "nsm_conv_wgrad": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P, P, P]),
     "nsm_reduce_chunks": (I, [I, I]),
     "nsm_reduce_rows": (I, [I, I]),
     "nsm_bn_stats": (I, [P, I, I, I, P, I, I, P]),
     "nsm_bn_finalize_train": (I, [P, I, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P]),
     "nsm_bn_partials_merge": (I, [P, I, I, I, I, I, P, P]),
     "nsm_bn_finalize_eval": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
-    "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, P, I, I, P]),
+    "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, P, I, I, P, P]),
     "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
     "nsm_bn_bwd_finalize": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
-    "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
+    "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P, P]),
     "nsm_sum_rows": (I, [P, I, I, I, P, P]),
     "nsm_resize_fwd_act": (I, [P, I, I, I, I, P, I, I, P, P, F, P, I, P]),
     "nsm_up2_resize_fwd_act": (I, [P, I, I, I, I, P, I, I, P, P, F, P, I, P]),
@@ -70,7 +70,7 @@ _SIGS = {
     "nsm_wino_stat_slots": (I, [I, I, I, I, I]),
     "nsm_conv1x1_bnbwd_chunks": (I, [I, I, I, I, I]),
     "nsm_conv1x1_dgrad_bnbwd": (I, [P, I, I, I, I, I, P, I, P, I, P, P, P, P, P, F, I, P, P, P, I,
-                                    I, P]),
+                                    I, P, P, P]),
     "nsm_avgpool2_fwd": (I, [P, I, I, I, I, P, I, P]),
     "nsm_avgpool2_bwd_add": (I, [P, I, I, I, I, P, P, I, P]),
     "nsm_resize_fwd": (I, [P, I, I, I, I, P, I, I, I, P]),

@@ -154,15 +154,25 @@ class stage:
         return False
 
 
-def conv_fwd(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None, slope=0.2):
+def conv_fwd(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None, slope=0.2,
+             amax=(None, None)):
     """x: [B*H*W, cin_p]; returns y [B*H*W, cout_p]. pro=(scale, shift, mask|None):
-    the operand loader applies lrelu(x*scale+shift, slope)*mask."""
+    the operand loader applies lrelu(x*scale+shift, slope)*mask. amax =
+    (max|x|, max|wpk|) operand-maximum slots: with both (fp32, no prologue)
+    the GEMM runs the f16x2 split."""
     return conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro, out, tag, stats=False,
-                       slope=slope)[0]
+                       slope=slope, amax=amax)[0]
+
+
+def _pair(amax):
+    """Both slots' pointers, or (None, None) unless both are given."""
+    if amax[0] is None or amax[1] is None:
+        return None, None
+    return ptr(amax[0]), ptr(amax[1])
 
 
 def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=None, stats=True,
-                slope=0.2):
+                slope=0.2, amax=(None, None)):
     """conv_fwd returning (y, Partials|None): with stats=True the GEMM epilogue
     also emits the BN batch-statistics partials of y."""
     from ._lib import lib
@@ -180,10 +190,13 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
         nchunk = -(-M // rpc)
         part = Partials(empty(nchunk * 2 * cout_p, device=x.device), nchunk, rpc)
     ev = _probe(tag)
-    fn = "nsm_conv_fwd_bf16" if x.dtype == BF16 else "nsm_conv_fwd_stats"
-    call(fn, ptr(x), x.stride(0), B, H, W, cin_p, ptr(wpk), ptr(bias), cout_p,
-         ksize, ptr(y), y.stride(0), ptr(sc), ptr(sh), ptr(mk), slope,
-         ptr(part.buf) if part is not None else None, stream())
+    args = (ptr(x), x.stride(0), B, H, W, cin_p, ptr(wpk), ptr(bias), cout_p, ksize, ptr(y),
+            y.stride(0), ptr(sc), ptr(sh), ptr(mk), slope,
+            ptr(part.buf) if part is not None else None)
+    if x.dtype == BF16:
+        call("nsm_conv_fwd_bf16", *args, stream())
+    else:
+        call("nsm_conv_fwd_stats", *args, *_pair(amax), stream())
     if ev is not None:
         ev.record()
     return y, part
@@ -347,8 +360,9 @@ def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, d
         ev.record()
 
 
-def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None):
-    """dw (reference layout [cout, cin, k, k], contiguous) <- sum_p dy (x) x."""
+def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None, amax=(None, None)):
+    """dw (reference layout [cout, cin, k, k], contiguous) <- sum_p dy (x) x.
+    amax = (max|dy|, max|x|) slots: the fp32 GEMM runs the f16x2 split."""
     from ._lib import lib
     cout_p, cin_p = dy.shape[1], x.shape[1]
     bf = dy.dtype == BF16
@@ -361,9 +375,12 @@ def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None):
     if pro is not None:
         sc, sh, mk = pro
     ev = _probe(tag)
-    call("nsm_conv_wgrad_bf16" if bf else "nsm_conv_wgrad", ptr(dy), dy.stride(0), ptr(x),
-         x.stride(0), B, H, W, cin_p, cout_p, ksize, ptr(sc), ptr(sh), ptr(mk), 0.2, ptr(ws), n,
-         cin, cout, ptr(dw), stream())
+    args = (ptr(dy), dy.stride(0), ptr(x), x.stride(0), B, H, W, cin_p, cout_p, ksize, ptr(sc),
+            ptr(sh), ptr(mk), 0.2, ptr(ws), n, cin, cout, ptr(dw))
+    if bf:
+        call("nsm_conv_wgrad_bf16", *args, stream())
+    else:
+        call("nsm_conv_wgrad", *args, *_pair(amax), stream())
     if ev is not None:
         ev.record()
 
@@ -467,25 +484,27 @@ def bn_eval(bn_mod, C, c_real, eps, device, gamma=None, beta=None):
     return st
 
 
-def bn_act(y, st, slope=0.2, res=None, out=None, mask=None, HW=0):
-    """lrelu(y*scale+shift) (* mask[b, c] with b = row // HW) (+ res)."""
+def bn_act(y, st, slope=0.2, res=None, out=None, mask=None, HW=0, amax=None):
+    """lrelu(y*scale+shift) (* mask[b, c] with b = row // HW) (+ res).
+    amax: operand-maximum slot receiving max|out| (fp32)."""
     M, C = y.shape
     o = out if out is not None else like(M, C, y)
     assert res is None or res.dtype == y.dtype
     assert mask is None or HW > 0
     call("nsm_bn_act", ptr(y), y.stride(0), M, C, ptr(st.scale), ptr(st.shift), slope, ptr(mask),
          HW, ptr(res), res.stride(0) if res is not None else 0, ptr(o), o.stride(0), dt(y),
-         stream())
+         ptr(amax) if y.dtype == F32 else None, stream())
     return o
 
 
 def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, part=None,
-           defer=False):
+           defer=False, amax=None):
     """Backward through lrelu(.)*mask after a train-mode BN: returns dy
     (grad wrt the BN input) and writes dgamma/dbeta/dbias_prev (real chans).
     part=(partial, nchunk): the {sum dz, sum dz*xhat} partials already written
     by g's producer (GradPart), so the reduce pass is skipped. defer=True:
-    DeferredBnBwd(g, coef) instead of dy (its consumer forms dy itself)."""
+    DeferredBnBwd(g, coef) instead of dy (its consumer forms dy itself).
+    amax: operand-maximum slot receiving max|dy| (fp32)."""
     M, C = y.shape
     assert g.dtype == y.dtype
     if part is None:
@@ -510,7 +529,7 @@ def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, par
     dy = like(M, C, y)
     call("nsm_bn_bwd_apply", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
          ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy), dy.stride(0), dt(y),
-         stream())
+         ptr(amax) if y.dtype == F32 else None, stream())
     return dy
 
 
@@ -518,7 +537,7 @@ SUM_ROWS_ABOVE = int(os.environ.get("NSM_SUM_ROWS_ABOVE", "512"))  # BN-backward
 
 
 def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
-                         recompute, slope=0.2, tag=None, defer=False):
+                         recompute, slope=0.2, tag=None, defer=False, amax=(None, None)):
     """dY1 of a DoubleConv's first BN from dY2 (grad wrt the 1x1 conv output):
     the 1x1 input gradient dA1 = dY2 W2 with the BN + LeakyReLU + Dropout2d
     backward in its epilogue (nsm_conv1x1_dgrad_bnbwd) — the same values as
@@ -526,7 +545,8 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     recompute=True: a partials-only GEMM pass, then the GEMM again writing dY1
     (dA1 never stored); False: one pass storing dA1 + partials, then
     nsm_bn_bwd_apply. defer=True (with recompute=False): DeferredBnBwd(dA1,
-    coef) instead of dy, the apply pass left to the consumer."""
+    coef) instead of dy, the apply pass left to the consumer. amax = (max|dY2|,
+    max|w2d|) slots: the fp32 GEMM passes run the f16x2 split."""
     from ._lib import lib
     M, cop = dY2.shape
     C = y.shape[1]
@@ -539,8 +559,9 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     args = (ptr(dY2), dY2.stride(0), B, H, W, cop, ptr(w2d), C, ptr(y), y.stride(0),
             ptr(st.scale), ptr(st.shift), ptr(st.mean), ptr(st.invstd), ptr(mask), slope)
     ev = _probe(tag)
+    am = _pair(amax) if dtc == NSM_F32 else (None, None)
     call("nsm_conv1x1_dgrad_bnbwd", *args, 0 if recompute else 1, ptr(partial), None, ptr(dA1),
-         dA1.stride(0) if dA1 is not None else 0, dtc, stream())
+         dA1.stride(0) if dA1 is not None else 0, dtc, *am, stream())
     if nchunk > SUM_ROWS_ABOVE:
         G = -(-nchunk // SUM_ROWS_ABOVE)
         n2 = -(-nchunk // G)
@@ -557,11 +578,11 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     dy = like(M, C, y)
     if recompute:
         call("nsm_conv1x1_dgrad_bnbwd", *args, 2, None, ptr(coef), ptr(dy), dy.stride(0), dtc,
-             stream())
+             *am, stream())
     else:
         call("nsm_bn_bwd_apply", ptr(dA1), dA1.stride(0), ptr(y), y.stride(0), M, C, H * W,
              ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy),
-             dy.stride(0), dtc, stream())
+             dy.stride(0), dtc, None, stream())
     if ev is not None:
         ev.record()
     return dy

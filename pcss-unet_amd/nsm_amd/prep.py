@@ -49,6 +49,9 @@ class LazyBlockWeights:
     def amax_U1(self, flip):
         return None      # no recorded maximum: the bf16 split runs
 
+    def amax_w2(self, mode):
+        return None
+
     def w1(self, mode):
         return ops.pack_conv_weight(self.blk.conv[0].weight.detach(), self.cip, self.cip, mode,
                                     self.dtype)
@@ -74,6 +77,10 @@ class _PreparedBlock:
         """max|U| of the step's Winograd weight (written by the prep launch)."""
         return self.t.get(("amaxU1", flip))
 
+    def amax_w2(self, mode):
+        """max|packed 1x1 weight| (fp32 packs; written by the prep launch)."""
+        return self.t.get(("amaxw2", mode))
+
     def w1(self, mode):
         return self.t[("w1", mode)]
 
@@ -94,8 +101,9 @@ class StepWeights:
         self.blocks = {}
         jobs, keep = [], []
         base = 0
-        n_wino = sum(1 for k in shapes if ops.pad32(mod.block(k).conv[0].in_channels) >= wino_min
-                     and dtype == torch.float32) * 2
+        # slots: Winograd U (fwd, dgrad) and the packed 1x1 weights (fwd, dgrad)
+        n_wino = (sum(1 for k in shapes if ops.pad32(mod.block(k).conv[0].in_channels) >= wino_min)
+                  * 2 + len(shapes) * 2) if dtype == torch.float32 else 0
         # per-step maxima of the Winograd weights (the f16x2 GEMMs' operand
         # scales), zeroed by run() before the prep launch refills them
         self.amax = ops.amax_slots(max(n_wino, 1), dev)
@@ -146,7 +154,13 @@ class StepWeights:
                     pb.t[("w1", mode)] = add(pk, (ci, ci, 9, cip, cip, mode), c0.weight,
                                              cip * 9 * cip, dtype)
             for mode in modes:
-                pb.t[("w2", mode)] = add(pk, (co, ci, 1, cop, cip, mode), c4.weight, cop * cip, dtype)
+                am = None
+                if dtype == torch.float32:
+                    am = ops.amax_slot(self.amax, n_am)
+                    n_am += 1
+                    pb.t[("amaxw2", mode)] = am
+                pb.t[("w2", mode)] = add(pk, (co, ci, 1, cop, cip, mode), c4.weight, cop * cip, dtype,
+                                         amax=am)
             self.blocks[k] = pb
         self.total = base
         self.njobs = len(jobs)

@@ -422,15 +422,20 @@ class _BlockSaved:
                  "pw", "Z", "am")
 
 
+# a block's operand-maximum slots (the f16x2 GEMMs' operand scales, filled by
+# the operands' producers): Winograd V, Vd, dM; the 1x1 conv's A1 and dY2
+AM_V, AM_VD, AM_DM, AM_A1, AM_DY2, AM_PER_BLOCK = 0, 1, 2, 3, 4, 5
+
+
 def _slot(am, i):
-    """Slot i of a block's operand-maximum slots (V, Vd, dM), or None."""
+    """Slot i of a block's operand-maximum slots, or None."""
     return ops.amax_slot(am, i)
 
 
 def _block_slots(amax, k):
-    """Block k's three operand-maximum slots of the step's buffer, or None."""
-    w = ops.AMAX_WORDS
-    return None if amax is None else amax[3 * k * w:(3 * k + 3) * w]
+    """Block k's operand-maximum slots of the step's buffer, or None."""
+    w = ops.AMAX_WORDS * AM_PER_BLOCK
+    return None if amax is None else amax[k * w:(k + 1) * w]
 
 
 def fuses_resize(blk, dtype):
@@ -453,7 +458,7 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
         tile = wino_tile(cip, H, W)
         A1 = ops.conv3x3_wino(xin, B, H, W, pw.U1(tile, False), b1, cip, tile=tile,
                               tag=name + ".conv.0.fwd", src_hw=src_hw, act=(bn1, None),
-                              amax_v=_slot(am, 0), amax_u=pw.amax_U1(False))
+                              amax_v=_slot(am, AM_V), amax_u=pw.amax_U1(False))
     else:
         assert src_hw is None
         A1 = ops.conv_fwd_act(xin, B, H, W, pw.w1(ops.PACK_FWD), b1, cip, 3, bn1, slope=SLOPE,
@@ -477,8 +482,8 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     inside the Winograd input transform (X is None then; fuses_resize).
     fuse_out (eval, EVAL_FUSED): the block output lrelu(bn2(Y2)) (+ res) is
     produced by the convs' epilogues, returned as s.Z (Y1/Y2 not stored).
-    am: the block's 3 zeroed int32 slots for max|V|, max|Vd|, max|dM| (the
-    Winograd GEMMs' f16x2 operand scales), or None (bf16 split)."""
+    am: the block's zeroed operand-maximum slots (AM_*: the f16x2 GEMMs'
+    operand scales), or None (bf16 split)."""
     c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
     ci, co = c0.in_channels, c4.out_channels
     cip, cop = ops.pad32(ci), ops.pad32(co)
@@ -501,12 +506,12 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
             # the output transform also writes the BN batch-statistics partials
             Y1, V, part1 = ops.conv3x3_wino(xin, B, H, W, U1, b1, cip, tile=tile,
                                             tag=name + ".conv.0.fwd", keep_v=True, stats=True,
-                                            src_hw=src_hw, amax_v=_slot(am, 0),
+                                            src_hw=src_hw, amax_v=_slot(am, AM_V),
                                             amax_u=pw.amax_U1(False))
         else:
             Y1, V = ops.conv3x3_wino(xin, B, H, W, U1, b1, cip, tile=tile,
                                      tag=name + ".conv.0.fwd", keep_v=True, src_hw=src_hw,
-                                     amax_v=_slot(am, 0), amax_u=pw.amax_U1(False))
+                                     amax_v=_slot(am, AM_V), amax_u=pw.amax_U1(False))
         if training and part1 is None:
             part1 = ops.bn_partials(Y1)
     else:
@@ -524,9 +529,10 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     A1 = None
     if BF16_MATERIALIZE_ACT if dtype == torch.bfloat16 else F32_MATERIALIZE_ACT:
         # the same fp32 arithmetic and bf16 rounding as the fused operand prologue
-        A1 = ops.bn_act(Y1, bn1, SLOPE, mask=mask, HW=H * W)
+        A1 = ops.bn_act(Y1, bn1, SLOPE, mask=mask, HW=H * W, amax=_slot(am, AM_A1))
         Y2, part2 = ops.conv_fwd_bn(A1, B, H, W, w2, b2, cop, 1, tag=name + ".conv.4.fwd",
-                                    stats=training)
+                                    stats=training,
+                                    amax=(_slot(am, AM_A1), pw.amax_w2(ops.PACK_FWD)))
     else:
         Y2, part2 = ops.conv_fwd_bn(Y1, B, H, W, w2, b2, cop, 1, pro=(bn1.scale, bn1.shift, mask),
                                     tag=name + ".conv.4.fwd", stats=training)
@@ -555,11 +561,13 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
     HW = H * W
     g = grads
     dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias],
-                     part=gpart)
+                     part=gpart, amax=_slot(s.am, AM_DY2))
     dtype = G.dtype
     w2d = s.pw.w2(ops.PACK_DGRAD)
+    am_w2d = (_slot(s.am, AM_DY2), s.pw.amax_w2(ops.PACK_DGRAD))
     if s.A1 is not None:
-        ops.conv_wgrad(dY2, s.A1, B, H, W, 1, ci, co, g[c4.weight], tag=name + ".conv.4.wgrad")
+        ops.conv_wgrad(dY2, s.A1, B, H, W, 1, ci, co, g[c4.weight], tag=name + ".conv.4.wgrad",
+                       amax=(_slot(s.am, AM_DY2), _slot(s.am, AM_A1)))
         s.A1 = None
     else:
         ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
@@ -571,9 +579,10 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
     if mode:
         dY1 = ops.conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
                                        g[bn1m.bias], g[c0.bias], mode == 2,
-                                       tag=name + ".conv.4.dgrad", defer=lazy)
+                                       tag=name + ".conv.4.dgrad", defer=lazy, amax=am_w2d)
     else:
-        dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad")
+        dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad",
+                           amax=am_w2d)
         dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias],
                          g[c0.bias], defer=lazy)
     Vd = None
@@ -582,7 +591,7 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         dM = None
         if need_dx and DUAL_TRANSFORM:
             # dY1's two Winograd transforms (dgrad input, wgrad) from one read
-            am2 = (_slot(s.am, 1), _slot(s.am, 2))
+            am2 = (_slot(s.am, AM_VD), _slot(s.am, AM_DM))
             if isinstance(dY1, ops.DeferredBnBwd):
                 Vd, dM = ops.wino_dual_input_bn(dY1, s.Y1, s.bn1, s.mask, B, H, W, tile=tile,
                                                 amax=am2)
@@ -590,7 +599,7 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
                 Vd, dM = ops.wino_dual_input(dY1, B, H, W, tile=tile, amax=am2)
         ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=tile,
                                tag=name + ".conv.0.wgrad", dM=dM,
-                               amax=(_slot(s.am, 2), _slot(s.am, 0)))
+                               amax=(_slot(s.am, AM_DM), _slot(s.am, AM_V)))
         s.V = None
     else:
         ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
@@ -600,7 +609,7 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         tile = wino_tile(s.cip, H, W)
         U1d = s.pw.U1(tile, True)
         return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=tile,
-                                tag=name + ".conv.0.dgrad", v_in=Vd, amax_v=_slot(s.am, 1),
+                                tag=name + ".conv.0.dgrad", v_in=Vd, amax_v=_slot(s.am, AM_VD),
                                 amax_u=s.pw.amax_U1(True))
     w1d = s.pw.w1(ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
@@ -656,9 +665,9 @@ class _UnetFn(torch.autograd.Function):
         X = ops.input_prep(x32, cin_p, cdt)
         masks = _masks_for(mod, B, dev, training)
         sw = _step_weights(mod, cdt, Rh, Rw, training)
-        # per-step maxima of the Winograd GEMM operands V, Vd, dM of every block
-        # (their producers fill them; zeroed here, one launch)
-        amax = ops.amax_slots(3 * 10, dev) if sw else None
+        # per-step maxima of the f16x2 GEMM operands of every block (their
+        # producers fill them; zeroed here, one launch)
+        amax = ops.amax_slots(AM_PER_BLOCK * 10, dev) if sw else None
 
         saved, c, shapes = {}, {}, {}
         inp, h, w = X, Rh, Rw

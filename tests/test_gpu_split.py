@@ -73,10 +73,14 @@ def test_split_matches_fp32_accuracy(ops, device, B, H, W, ci, co, tile):
         print(f"F({tile}) {name}: fp32-MFMA max {m0:.2e} rms {r0:.2e} | bf16 split max {m1:.2e} "
               f"rms {r1:.2e} | f16x2 max {m2:.2e} rms {r2:.2e}")
         # the Winograd transforms dominate all; the GEMM arithmetic must not add
-        # error: rms within 1.25x of the fp32 MFMA's; the max (a statistic of a
-        # few elements at these sizes) within 2x
-        for m, r in ((m1, r1), (m2, r2)):
-            assert r <= 1.25 * r0 + 1e-9, (name, r0, r)
+        # error: rms within 1.25x of the fp32 MFMA's (1.5x for the f16x2
+        # split: its 2^-22 per-product representation error shows once the
+        # GEMM's K is a few tiles — K = 4 in the 7x5 case — where the fp32
+        # path adds almost no rounding; at the model's K it is below the fp32
+        # MFMA's, tools/bench_split16.py); the max (a statistic of a few
+        # elements at these sizes) within 2x
+        for m, r, rb in ((m1, r1, 1.25), (m2, r2, 1.5)):
+            assert r <= rb * r0 + 1e-9, (name, r0, r)
             assert m <= 2.0 * m0 + 1e-8, (name, m0, m)
 
 
@@ -84,7 +88,8 @@ def test_split_matches_fp32_accuracy(ops, device, B, H, W, ci, co, tile):
                                            (1, 33, 35, 128, 128, 3), (2, 64, 64, 32, 32, 3)])
 def test_split_direct_convs(ops, device, B, H, W, ci, co, k):
     """Direct implicit-GEMM forward, input gradient and split-K weight gradient
-    (the non-Winograd fp32 GEMMs) in both modes against float64."""
+    (the non-Winograd fp32 GEMMs) in all three modes against float64 (mode 2
+    with the operands' maxima from nsm_absmax)."""
     g = torch.Generator().manual_seed(B * 100 + ci + co + k)
     x = torch.randn(B, ci, H, W, generator=g, dtype=torch.float64, requires_grad=True)
     w = (torch.randn(co, ci, k, k, generator=g, dtype=torch.float64) / (ci * k * k) ** 0.5).requires_grad_(True)
@@ -93,22 +98,26 @@ def test_split_direct_convs(ops, device, B, H, W, ci, co, k):
     ref.backward(dy)
     xs, ws, dys = x.detach().float(), w.detach().float(), dy.float()
     res = {}
-    for mode in (0, 1):
+    for mode in (0, 1, 2):
         ops.set_f32_split(mode)
+        am = (lambda t: ops.absmax(t)) if mode == 2 else (lambda t: None)
+        xd, dyd = nhwc(xs).to(device), nhwc(dys).to(device)
         wp = ops.pack_conv_weight(ws.to(device), co, ci, ops.PACK_FWD)
-        y = ops.conv_fwd(nhwc(xs).to(device), B, H, W, wp, None, co, k)
+        y = ops.conv_fwd(xd, B, H, W, wp, None, co, k, amax=(am(xd), am(wp)))
         wd = ops.pack_conv_weight(ws.to(device), co, ci, ops.PACK_DGRAD)
-        dx = ops.conv_fwd(nhwc(dys).to(device), B, H, W, wd, None, ci, k)
+        dx = ops.conv_fwd(dyd, B, H, W, wd, None, ci, k, amax=(am(dyd), am(wd)))
         dw = torch.empty(co, ci, k, k, device=device)
-        ops.conv_wgrad(nhwc(dys).to(device), nhwc(xs).to(device), B, H, W, k, ci, co, dw)
+        ops.conv_wgrad(dyd, xd, B, H, W, k, ci, co, dw, amax=(am(dyd), am(xd)))
         res[mode] = (_errs(nchw(y.cpu(), B, H, W), ref.detach()), _errs(nchw(dx.cpu(), B, H, W), x.grad),
                      _errs(dw.cpu(), w.grad))
     ops.set_f32_split(2)
     for i, name in enumerate(("fwd", "dgrad", "wgrad")):
-        (m0, r0), (m1, r1) = res[0][i], res[1][i]
-        print(f"direct k{k} {name}: fp32-MFMA max {m0:.2e} rms {r0:.2e} | split max {m1:.2e} rms {r1:.2e}")
-        assert r1 <= 1.5 * r0 + 1e-9, (name, r0, r1)
-        assert m1 <= 2.0 * m0 + 1e-8, (name, m0, m1)
+        (m0, r0), (m1, r1), (m2, r2) = res[0][i], res[1][i], res[2][i]
+        print(f"direct k{k} {name}: fp32-MFMA max {m0:.2e} rms {r0:.2e} | bf16 split max {m1:.2e} "
+              f"rms {r1:.2e} | f16x2 max {m2:.2e} rms {r2:.2e}")
+        for m, r in ((m1, r1), (m2, r2)):
+            assert r <= 1.5 * r0 + 1e-9, (name, r0, r)
+            assert m <= 2.0 * m0 + 1e-8, (name, m0, m)
 
 
 def test_split_train_step_vs_oracle(ops, device):

@@ -52,7 +52,7 @@ for (B, H, W, ci, co) in shapes:
                                         ptr(Mb), stream())),
             ("bf16x3", 1, lambda: call("nsm_wino_gemm", ptr(V), ptr(U), B, H, W, ci, co, t,
                                        ptr(Mb), stream())),
-            ("f16x2", 1, lambda: call("nsm_wino_gemm_s", ptr(V), ptr(U), B, H, W, ci, co, t,
+            ("f16x2", 2, lambda: call("nsm_wino_gemm_s", ptr(V), ptr(U), B, H, W, ci, co, t,
                                       ptr(Mb), ptr(av), ptr(au), stream()))):
         ops.set_f32_split(mode)
         ms = timeit(fn)
