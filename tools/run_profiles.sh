@@ -9,7 +9,7 @@
 #    encoder/decoder stage): one kernel-trace run and four PMC passes, each in
 #    its own run (rocprofv3 does not split counters over passes):
 #      TCC_EA0_RDREQ_{,32B_,64B_,128B_}sum | FETCH_SIZE | WRITE_SIZE |
-#      SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16/_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+#      SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16/_F16/_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
 #    summarised per stage by tools/stage_pmc.py and, for the dominant kernel,
 #    by tools/pmc_traffic.py (bench.py reads both JSONs).
 set -euo pipefail
@@ -37,7 +37,7 @@ run() {  # tag
   pmc $tag rdreq TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum
   pmc $tag fetch FETCH_SIZE
   pmc $tag write WRITE_SIZE
-  pmc $tag sq SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
+  pmc $tag sq SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_INSTS_VALU_MFMA_MOPS_F16 SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
   python3 tools/stage_pmc.py "profiles/$R/stage_pmc_$tag.json" "$OUT/mtrace_$tag.csv" \
       "$OUT/rdreq_$tag.csv" "$OUT/fetch_$tag.csv" "$OUT/write_$tag.csv" "$OUT/sq_$tag.csv" > "$OUT/stage_$tag.txt"
   python3 tools/step_timeline.py "$(f trace_$tag run_kernel_trace.csv)" > "profiles/$R/step_timeline_$tag.txt"

@@ -26,9 +26,10 @@ outside every stage go to "other": input prep, weight prep, loss, tail):
                  the fraction of SIMD-cycles the matrix pipe was busy, at the
                  clock the chip held
   bf16_mfma_flops, f32_mfma_flops
-                 512 x SQ_INSTS_VALU_MFMA_MOPS_{BF16,F32}: the matrix-core work
-                 actually issued, per pipe (the fp32 GEMMs run on the bf16 pipe
-                 by the exact 3-way split: 6 bf16 products per fp32 product)
+                 512 x SQ_INSTS_VALU_MFMA_MOPS_{BF16+F16, F32}: the matrix-core
+                 work actually issued, per pipe (16-bit: bf16 and f16 MFMAs run
+                 at the same rate; the fp32 GEMMs run there by the f16x2 split,
+                 3 products per fp32 product, or the bf16 split, 6)
   mfma_pipe_frac bf16 work / kernel_ms / 2516.6 TFLOP/s + f32 work / kernel_ms
                  / 157.3 TFLOP/s: the fraction of the dense peak of the pipe
                  that ran it (at the 2.4 GHz peak clock)
@@ -145,9 +146,12 @@ def main():
             row["grbm"] = r["GRBM_GUI_ACTIVE"]
             row["prof_ms"] = prof_ms.get(st, 0.0)
         for k, c in (("bf16_mfma_flops", "SQ_INSTS_VALU_MFMA_MOPS_BF16"),
+                     ("f16_mfma_flops", "SQ_INSTS_VALU_MFMA_MOPS_F16"),
                      ("f32_mfma_flops", "SQ_INSTS_VALU_MFMA_MOPS_F32")):
             if r.get(c) is not None:
                 row[k] = 512 * r[c]
+        if "f16_mfma_flops" in row:   # one 16-bit pipe: bf16 and f16 MFMAs at the same rate
+            row["bf16_mfma_flops"] = row.get("bf16_mfma_flops", 0.0) + row.pop("f16_mfma_flops")
         stages[st] = row
     for n in STAGE_NAMES:   # fwd + bwd per stage
         f, b = stages.get(n + ".fwd"), stages.get(n + ".bwd")
