@@ -62,7 +62,10 @@ int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
  * nsm_pack_conv_weight / nsm_pack_conv_weight_bf16 / nsm_wino_weight / nsm_pad_vec
  * calls). kind 0: pack fp32, 1: pack bf16, a = {cout, cin, taps, cout_p, cin_p,
  * mode}; kind 2: Winograd U, a = {cout, cin, n_p, k_p, flip, tile}; kind 3: pad
- * vector, a = {n, n_p}. `base` = the job's first item in the launch (jobs in
+ * vector, a = {n, n_p}; kind 4: Winograd U as an h2 tensor [alpha^2][n_p][2 k_p]
+ * (nsm_to_h2's layout), a as kind 2, amax (required) = the slot the launch first
+ * fills with max|w| of the filters, the scale source of U (beta =
+ * nsm_wino_beta(tile, 2)). `base` = the job's first item in the launch (jobs in
  * ascending base order, consecutive); nsm_prep_items() = the job's extent in
  * the launch (its item count rounded up to whole 2048-item blocks: add it to
  * get the next base; total_items = the sum). jobs_dev: a device copy. */
@@ -73,7 +76,8 @@ typedef struct {
   const float* src;
   void* dst;
   uint32_t* amax; /* kinds 0, 2 (may be NULL): atomic max of |written| as fp32
-                     bits (zeroed beforehand): the f16x2 GEMM operand scale */
+                     bits (zeroed beforehand): the f16x2 GEMM operand scale;
+                     kind 4: max|w| (see above) */
 } NsmPrepJob;
 long long nsm_prep_items(const NsmPrepJob* job);
 int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items, void* stream);
@@ -147,6 +151,43 @@ int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int W, int cin
  * zeroed first; NaN counts above +Inf): the maximum a GEMM operand needs when
  * its producer does not record it. */
 int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
+/* ---- pre-split ("h2") Winograd operands (csrc/nsm_conv_h2.inc) -------------
+ * An h2 tensor is an fp32 [rows][C] matrix X stored as fp16 [rows][2C]: with
+ * s = 2^(15 - ceil(log2(beta * m))), m = the max of the operand-maximum slot
+ * `amax` (of X itself, or of the tensor X is a transform of, beta the
+ * transform's bound), the 8 channels of chunk j are h = f16(x s) at 16j..16j+7
+ * and l = f16(x s - h) at 16j+8..16j+15. Same bytes as fp32; the GEMMs read
+ * both terms by LDS-DMA and multiply h.h + h.l + l.h on the f16 matrix cores.
+ * nsm_to_h2: X [rows][C] (C % 8 == 0) -> h2 (test / benchmark helper). */
+int nsm_to_h2(const float* x, int64_t rows, int C, const uint32_t* amax, float beta, void* out,
+              void* stream);
+/* wino_beta(tile, which): the bound beta of a Winograd transform,
+ * max|out| <= beta * max|in| (which 0: input B^T d B, 1: output gradient
+ * A dY A^T, 2: filter G g G^T) — the factor between an h2 operand's scale
+ * source and the operand */
+float nsm_wino_beta(int tile, int which);
+/* nsm_wino_input_resize writing V as an h2 tensor [alpha^2][T][2 cin_p]; scale
+ * source amax_x = max|x| (recorded by x's producer), beta = wino_beta(tile, 0) */
+int nsm_wino_input_h2(const float* x, int ldx, int B, int hi, int wi, int H, int W, int cin_p,
+                      int tile, void* Vh, const uint32_t* amax_x, void* stream);
+/* nsm_wino_dual_input writing Vd and dM as h2 tensors; scale source amax_dy =
+ * max|dy| (its producer's), betas wino_beta(tile, 0) and (tile, 1) */
+int nsm_wino_dual_input_h2(const float* dy, int lddy, int B, int H, int W, int c_p, int tile,
+                           void* Vh, void* dMh, const uint32_t* amax_dy, void* stream);
+/* the weight gradient of a Winograd conv from h2 dM (nsm_wino_dual_input_h2) and
+ * h2 V (nsm_wino_input_h2): batched split-K GEMMs on the f16 matrix cores, then
+ * the filter transform; ws >= nsm_wino_wgrad_h2_ws floats */
+size_t nsm_wino_wgrad_h2_ws(int B, int H, int W, int cin_p, int cout_p, int tile);
+int nsm_conv3x3_wgrad_wino_h2(const void* dMh, const void* Vh, int B, int H, int W, int cin_p,
+                              int cout_p, int cin, int cout, int tile, float* dw, float* ws,
+                              size_t ws_floats, const uint32_t* amax_dy, const uint32_t* amax_x,
+                              void* stream);
+/* nsm_wino_gemm on h2 operands: V [alpha^2][T][2 cin_p], U [alpha^2][cout_p][2 cin_p]
+ * with their scale sources (amax_v, beta_v), (amax_u, beta_u); Mb fp32 as
+ * nsm_wino_gemm. */
+int nsm_wino_gemm_h2(const void* V, const void* U, int B, int H, int W, int cin_p, int cout_p,
+                     int tile, float* Mb, const uint32_t* amax_v, float beta_v,
+                     const uint32_t* amax_u, float beta_u, void* stream);
 /* fp32 GEMM arithmetic of every fp32 convolution (the batched GEMMs of
  * nsm_wino_gemm / nsm_conv3x3_wino, the weight gradient of
  * nsm_conv3x3_wgrad_wino, the direct implicit GEMMs): 2 (default, env
@@ -295,7 +336,9 @@ int nsm_up2_resize_fwd_act(const void* y2, int B, int h, int w, int C, void* out
  * read of y (Unetmodel.py:27-28,105,108,111) */
 int nsm_bn_act_pool(const void* y, int B, int H, int W, int C, const float* scale,
                     const float* shift, float slope, void* z, void* pooled, int dtype,
-                    void* stream);
+                    uint32_t* amax, void* stream);
+/* (nsm_bn_act_pool's amax: fp32, may be NULL — max|pooled|, the next Winograd
+ * conv's h2 scale source) */
 int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, void* y, int th, int tw,
                        int dtype, void* stream);
 int nsm_up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, int th, int tw,
@@ -453,7 +496,9 @@ int nsm_conv1x1_dgrad_bnbwd(const void* dy2, int lddy2, int B, int H, int W, int
                             const float* invstd, const float* mask, float slope, int mode,
                             float* partial, const float* coef, void* out, int ldo, int dtype,
                             const uint32_t* amax_dy2, const uint32_t* amax_w,
-                            void* stream);
+                            uint32_t* amax_out, void* stream);
+/* (amax_out: fp32 mode 2, may be NULL — max|dy| written, the h2 scale source
+ * of its Winograd transforms) */
 int nsm_conv1x1_bnbwd_chunks(int B, int H, int W, int cip, int dtype);
 /* rows per BN-partial chunk of nsm_conv_fwd_bf16 (its M tile) */
 /* Eval-mode DoubleConv half in one pass (Unetmodel.py:21-28 with BatchNorm on

@@ -498,6 +498,7 @@ struct BnBwdEpiP {
   float slope;
   float* partial;  // [nchunk][2][N]
   int mode;
+  uint32_t* amax = nullptr;  // mode 2 (fp32): max|dy| written (an h2 scale source)
 };
 
 __device__ __forceinline__ f32x4 lrelu_grad_v4(f32x4 z, float slope) {
@@ -557,6 +558,7 @@ struct EpiBnBwd {
                 k2 = red ? zero : *(const f32x4*)(e.coef + N + nc),
                 k3 = red ? zero : *(const f32x4*)(e.coef + 2 * N + nc);
     f32x4 s1 = zero, s2 = zero;
+    uint32_t am = 0;
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
       const int r = (it * 64 + cx.lane) / CPR, m = cx.mb + r;
@@ -565,14 +567,21 @@ struct EpiBnBwd {
       f32x4 dz = g * lrelu_grad_v4(v * sc + sh, e.slope);
       if (mk) dz = dz * *(const f32x4*)(mk + (size_t)fdiv((uint32_t)min(m, M - 1), e.fdHW) * N + nc);
       if (!red) {
-        if (ok) *(f32x4*)(O + (size_t)m * e.ldo + n) = k1 * dz + k2 * (v - mu) + k3;
+        if (ok) {
+          const f32x4 d = k1 * dz + k2 * (v - mu) + k3;
+          *(f32x4*)(O + (size_t)m * e.ldo + n) = d;
+          amax_fold(am, d);
+        }
       } else if (ok) {
         s1 += dz;
         s2 += dz * ((v - mu) * is);
         if (e.mode == 1) *(f32x4*)(O + (size_t)m * e.ldo + n) = g;
       }
     }
-    if (!red) return;
+    if (!red) {
+      amax_flush(am, e.amax);
+      return;
+    }
 #pragma unroll
     for (int o = CPR; o < 64; o <<= 1) {
       s1 += shfl_xor_v4(s1, o);
@@ -1050,6 +1059,15 @@ __global__ void pad_vec_kernel(const float* __restrict__ v, int n, int n_p, floa
 // F(4x4): 36 per 16 (4x fewer). Matrices: exact Cook-Toom tables generated by
 // tools/wino_coeffs.py (F(4x4) uses points 0, 1, -1, 1/2, -2 for lower fp32 error).
 // ===========================================================================
+// Bounds of the Winograd transforms, (max_i sum_j |T_ij|)^2 rounded up:
+// which 0 = the input transform B^T d B, 1 = the output-gradient transform
+// A dY A^T, 2 = the filter transform G g G^T. max|transform| <= beta * max|in|
+// (the h2 operands' scale source, nsm_conv_h2.inc)
+__host__ __device__ constexpr float wino_beta(int tile, int which) {
+  return which == 0   ? (tile == 6 ? 225.f : tile == 4 ? 49.f : 4.f)
+         : which == 1 ? (tile == 6 ? 3969.f : tile == 4 ? 225.f : 4.f)
+                      : (tile == 6 ? 1.5625f : tile == 4 ? 3.5f : 2.25f);
+}
 template <int MT> struct WinoMats;
 template <> struct WinoMats<2> {
   static constexpr int A = 4;
@@ -1234,23 +1252,48 @@ __global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int ci
     for (int b = 0; b < A; ++b) U[(a * A + b) * plane + (size_t)n * k_p + k] = u[a][b];
 }
 
+// the alpha x alpha transform values of tile t, channel(s) c.. of one thread
+// into an h2 tensor [alpha^2][T][2C] (one channel per thread: lane pairs
+// exchange terms, h2_pair_word; four: h2_store4)
+template <int A, typename VT>
+__device__ __forceinline__ void h2_write(bf16_t* __restrict__ out, long long T, int C, long long t,
+                                         int c, const VT (&v)[A][A], float s) {
+  const size_t plane2 = (size_t)T * 2 * C;
+  bf16_t* row = out + (size_t)t * 2 * C;
+#pragma unroll
+  for (int a = 0; a < A; ++a)
+#pragma unroll
+    for (int e = 0; e < A; ++e) {
+      if constexpr (std::is_same<VT, float>::value)
+        *(uint32_t*)(row + (a * A + e) * plane2 + h2_pair_off(c)) = h2_pair_word(v[a][e], s);
+      else
+        h2_store4(row + (a * A + e) * plane2, c, v[a][e], s);
+    }
+}
+
 // RELU: the input is a pre-activation tensor whose consumer applies max(x, 0)
 // (VGG19 feature stack: ReLU folded into the next conv's operand load).
 // UP: x is the low-resolution tensor [B][hi][wi] of a bilinear align_corners
 // resize to H x W (the decoder's x2 upsample, Unetmodel.py:122-130); every
 // patch value is sampled from it as nsm_resize_fwd computes it, so the
 // resized activation is never written to HBM.
-template <int MT, bool RELU, bool UP>
+// H2: V is written as an h2 tensor (nsm_conv_h2.inc) Vh [alpha^2][T][2C] with
+// the scale of hsc (max|x| recorded by x's producer, beta = the transform's bound)
+template <int MT, bool RELU, bool UP, bool H2 = false>
 __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict__ x, int ld, int H,
                                                          int W, int C, int TH, int TW, long long T,
                                                          float* __restrict__ V, int hi, int wi,
                                                          float sh, float sw,
-                                                         uint32_t* __restrict__ amax) {
+                                                         uint32_t* __restrict__ amax,
+                                                         bf16_t* __restrict__ Vh = nullptr,
+                                                         H2Scale hsc = H2Scale{}) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int C4 = C / CW;
   const long long total = T * C4;
   uint32_t am = 0;  // max|V| of this thread (the f16x2 GEMM's operand scale)
+  float hs = 1.f;
+  if constexpr (H2) hs = exp2i(h2_exp(hsc));
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C4) * CW;
@@ -1329,17 +1372,21 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
     }
     VT v[A][A];
     wmat2<CBt<MT>>(d, v);
-    const size_t plane = (size_t)T * C;
-    float* out = V + (size_t)t * C + c;
+    if constexpr (H2) {
+      h2_write<A>(Vh, T, C, t, c, v, hs);
+    } else {
+      const size_t plane = (size_t)T * C;
+      float* out = V + (size_t)t * C + c;
 #pragma unroll
-    for (int a = 0; a < A; ++a)
+      for (int a = 0; a < A; ++a)
 #pragma unroll
-      for (int e = 0; e < A; ++e) {
-        *(VT*)(out + (a * A + e) * plane) = v[a][e];
-        if (amax) amax_fold(am, v[a][e]);
-      }
+        for (int e = 0; e < A; ++e) {
+          *(VT*)(out + (a * A + e) * plane) = v[a][e];
+          if (amax) amax_fold(am, v[a][e]);
+        }
+    }
   }
-  amax_flush(am, amax);
+  if constexpr (!H2) amax_flush(am, amax);
 }
 
 // STATS: also the BatchNorm batch statistics of the written values (the
@@ -1504,19 +1551,30 @@ struct WinoBnSrc {
 __device__ __forceinline__ float vlrelu_grad(float z, float s) { return lrelu_grad(z, s); }
 __device__ __forceinline__ f32x4 vlrelu_grad(f32x4 z, float s) { return lrelu_grad_v4(z, s); }
 
-template <int MT, bool BN = false>
+// H2: V and dM written as h2 tensors (Vh, dMh; scales of hv, hd: max|dy|
+// recorded by dy's producer, beta = each transform's bound)
+template <int MT, bool BN = false, bool H2 = false>
 __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict__ dy, int ld, int H,
                                                         int W, int C, int TH, int TW, long long T,
                                                         float* __restrict__ V,
                                                         float* __restrict__ dM,
                                                         WinoBnSrc bn = WinoBnSrc{},
                                                         uint32_t* __restrict__ amax_v = nullptr,
-                                                        uint32_t* __restrict__ amax_dm = nullptr) {
+                                                        uint32_t* __restrict__ amax_dm = nullptr,
+                                                        bf16_t* __restrict__ Vh = nullptr,
+                                                        bf16_t* __restrict__ dMh = nullptr,
+                                                        H2Scale hv = H2Scale{},
+                                                        H2Scale hd = H2Scale{}) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int C4 = C / CW;
   const long long total = T * C4;
   uint32_t amv = 0, amd = 0;  // max|V|, max|dM| (the f16x2 GEMMs' operand scales)
+  float hsv = 1.f, hsd = 1.f;
+  if constexpr (H2) {
+    hsv = exp2i(h2_exp(hv));
+    hsd = exp2i(h2_exp(hd));
+  }
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C4) * CW;
@@ -1563,14 +1621,18 @@ __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict_
     {
       VT v[A][A];
       wmat2<CBt<MT>>(d, v);
-      float* out = V + (size_t)t * C + c;
+      if constexpr (H2) {
+        h2_write<A>(Vh, T, C, t, c, v, hsv);
+      } else {
+        float* out = V + (size_t)t * C + c;
 #pragma unroll
-      for (int a = 0; a < A; ++a)
+        for (int a = 0; a < A; ++a)
 #pragma unroll
-        for (int e = 0; e < A; ++e) {
-          *(VT*)(out + (a * A + e) * plane) = v[a][e];
-          if (amax_v) amax_fold(amv, v[a][e]);
-        }
+          for (int e = 0; e < A; ++e) {
+            *(VT*)(out + (a * A + e) * plane) = v[a][e];
+            if (amax_v) amax_fold(amv, v[a][e]);
+          }
+      }
     }
     VT g[MT][MT], sm[A][A];
 #pragma unroll
@@ -1578,17 +1640,23 @@ __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict_
 #pragma unroll
       for (int e = 0; e < MT; ++e) g[a][e] = d[a + 1][e + 1];
     wmat2<CA<MT>>(g, sm);
-    float* out = dM + (size_t)t * C + c;
+    if constexpr (H2) {
+      h2_write<A>(dMh, T, C, t, c, sm, hsd);
+    } else {
+      float* out = dM + (size_t)t * C + c;
 #pragma unroll
-    for (int a = 0; a < A; ++a)
+      for (int a = 0; a < A; ++a)
 #pragma unroll
-      for (int e = 0; e < A; ++e) {
-        *(VT*)(out + (a * A + e) * plane) = sm[a][e];
-        if (amax_dm) amax_fold(amd, sm[a][e]);
-      }
+        for (int e = 0; e < A; ++e) {
+          *(VT*)(out + (a * A + e) * plane) = sm[a][e];
+          if (amax_dm) amax_fold(amd, sm[a][e]);
+        }
+    }
   }
-  amax_flush(amv, amax_v);
-  amax_flush(amd, amax_dm);
+  if constexpr (!H2) {
+    amax_flush(amv, amax_v);
+    amax_flush(amd, amax_dm);
+  }
 }
 
 // dst[b][i] = sum_s src[b][s][i] (float4 lanes, fixed order): the split-K
@@ -1648,7 +1716,8 @@ __host__ __device__ inline long long nsm_prep_items_dev(const NsmPrepJob& j) {
   switch (j.kind) {
     case 0:
     case 1: return (long long)j.a[3] * j.a[4] * j.a[2];
-    case 2: return (long long)j.a[2] * j.a[3];
+    case 2:
+    case 4: return (long long)j.a[2] * j.a[3];
     case 3: return j.a[1];
     default: return -1;
   }
@@ -1682,13 +1751,38 @@ __device__ __forceinline__ void wino_weight_item(const float* __restrict__ w, in
     }
 }
 
+// Winograd U as an h2 tensor [alpha^2][n_p][2 k_p] (nsm_conv_h2.inc), scale s
+template <int MT>
+__device__ __forceinline__ void wino_weight_item_h2(const float* __restrict__ w, int cout, int cin,
+                                                    int n_p, int k_p, int flip,
+                                                    bf16_t* __restrict__ U, int idx, float s) {
+  constexpr int A = MT + 2;
+  const int k = idx % k_p, n = idx / k_p;
+  const int co = flip ? k : n, ci = flip ? n : k;
+  float g[3][3];
+  const bool ok = co < cout && ci < cin;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const int sa = flip ? 2 - a : a, sb = flip ? 2 - b : b;
+      g[a][b] = ok ? w[((size_t)co * cin + ci) * 9 + sa * 3 + sb] : 0.f;
+    }
+  float u[A][A];
+  wmat2<CG<MT>>(g, u);
+  h2_write<A>(U, n_p, k_p, n, k, u, s);
+}
+
 constexpr int PREP_ITEMS = 2048;  // items per block: 8 per thread
 
 // blockIdx -> job by a (uniform) binary search over the jobs' first blocks
 // (job.base / PREP_ITEMS: every job starts on a block boundary, see
 // nsm_prep_items), then the block's items of that job, coalesced
+// phase 0: the h2 Winograd jobs (kind 4) record max|w| of their filters into
+// j.amax (the scale source of the U they write in phase 1, beta = wino_beta G);
+// every other job waits for phase 1
 __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __restrict__ jobs,
-                                                           int njobs) {
+                                                           int njobs, int phase) {
   const long long blk0 = (long long)blockIdx.x * PREP_ITEMS;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
@@ -1698,6 +1792,35 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
   const NsmPrepJob& j = jobs[lo];
   const long long items = nsm_prep_items_dev(j);
   uint32_t am = 0;  // max|written| (the f16x2 GEMMs' operand scale, j.amax)
+  if (j.kind == 4) {  // uniform per block
+    const int cout = j.a[0], cin = j.a[1], n_p = j.a[2], k_p = j.a[3], flip = j.a[4];
+    if (phase == 0) {
+      for (int r = 0; r < PREP_ITEMS / 256; ++r) {
+        const long long li = blk0 - j.base + r * 256 + threadIdx.x;
+        if (li >= items) break;
+        const int k = (int)(li % k_p), n = (int)(li / k_p);
+        const int co = flip ? k : n, ci = flip ? n : k;
+        if (co < cout && ci < cin) {
+          const float* g = j.src + ((size_t)co * cin + ci) * 9;
+#pragma unroll
+          for (int q = 0; q < 9; ++q) amax_fold(am, g[q]);
+        }
+      }
+      amax_flush(am, j.amax);
+      return;
+    }
+    const float s = exp2i(h2_exp(H2Scale{j.amax, wino_beta(j.a[5], 2)}));
+    bf16_t* U = (bf16_t*)j.dst;
+    for (int r = 0; r < PREP_ITEMS / 256; ++r) {
+      const long long li = blk0 - j.base + r * 256 + threadIdx.x;
+      if (li >= items) break;
+      if (j.a[5] == 6) wino_weight_item_h2<6>(j.src, cout, cin, n_p, k_p, flip, U, (int)li, s);
+      else if (j.a[5] == 4) wino_weight_item_h2<4>(j.src, cout, cin, n_p, k_p, flip, U, (int)li, s);
+      else wino_weight_item_h2<2>(j.src, cout, cin, n_p, k_p, flip, U, (int)li, s);
+    }
+    return;
+  }
+  if (phase == 0) return;
   for (int r = 0; r < PREP_ITEMS / 256; ++r) {
     const long long li = blk0 - j.base + r * 256 + threadIdx.x;
     if (li >= items) break;
@@ -1798,8 +1921,9 @@ extern "C" int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long
   NSM_CHECK_ARG(jobs_dev && njobs > 0 && total_items > 0 && total_items % PREP_ITEMS == 0,
                 "prep_weights: bad args");
   NSM_CHECK_ARG(total_items / PREP_ITEMS < (1ll << 31), "prep_weights: too many items");
-  hipLaunchKernelGGL(prep_weights_kernel, dim3((unsigned)(total_items / PREP_ITEMS)), dim3(256), 0,
-                     as_stream(stream), jobs_dev, njobs);
+  for (int phase = 0; phase < 2; ++phase)
+    hipLaunchKernelGGL(prep_weights_kernel, dim3((unsigned)(total_items / PREP_ITEMS)), dim3(256), 0,
+                       as_stream(stream), jobs_dev, njobs, phase);
   NSM_LAUNCH_CHECK("prep_weights");
   return 0;
 }
@@ -2298,6 +2422,8 @@ extern "C" int nsm_wino_dual_input_bn(const float* g, int ldg, const float* y, i
 static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float* V, int B, int H,
                       int W, int cin_p, int cout_p, int cin, int cout, int tile, float* dw,
                       float* ws, size_t ws_floats, void* stream, AmaxPair amax = AmaxPair{});
+static int wgrad_wino_finish(float* slab, const WinoWgradPlan& pl, int nb, int M, int N, int cin,
+                             int cout, int tile, float* dw, hipStream_t s);
 
 extern "C" int nsm_conv3x3_wgrad_wino(const float* dy, int lddy, const float* V, int B, int H,
                                       int W, int cin_p, int cout_p, int cin, int cout, int tile,
@@ -2380,8 +2506,13 @@ static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float
   rc = launch_wino_wgrad<32, 32, 1, 1>(ap, bp, ep, M, N, K, pl.kchunk, pl.splits, nb, s, amax);
 #undef NSM_WW
   if (rc) return rc;
-  // split-K partials -> one dU per xi with a parallel, fixed-order sum (the
-  // transform kernel below then reads alpha^2 values per output weight)
+  return wgrad_wino_finish(slab, pl, nb, M, N, cin, cout, tile, dw, s);
+}
+
+// split-K partials -> one dU per xi with a parallel, fixed-order sum (the
+// transform kernel then reads alpha^2 values per output weight) -> dw
+static int wgrad_wino_finish(float* slab, const WinoWgradPlan& pl, int nb, int M, int N, int cin,
+                             int cout, int tile, float* dw, hipStream_t s) {
   const float* du = slab;
   int du_splits = pl.splits;
   if (pl.splits > 1) {
@@ -2409,6 +2540,122 @@ static int wgrad_wino(const float* dy, int lddy, const float* dM_in, const float
 
 namespace nsm {
 #include "nsm_conv_bf16.inc"
+#include "nsm_conv_h2.inc"
+
+extern "C" float nsm_wino_beta(int tile, int which) {
+  return (tile == 2 || tile == 4 || tile == 6) && which >= 0 && which <= 2 ? wino_beta(tile, which)
+                                                                          : 0.f;
+}
+
+extern "C" int nsm_wino_input_h2(const float* x, int ldx, int B, int hi, int wi, int H, int W,
+                                 int cin_p, int tile, void* Vh, const uint32_t* amax_x,
+                                 void* stream) {
+  NSM_CHECK_ARG(x && Vh && amax_x && cin_p % 32 == 0 && ldx % 4 == 0 && ldx >= cin_p,
+                "wino_input_h2: bad args");
+  NSM_CHECK_ARG(hi > 0 && wi > 0 && ((uintptr_t)Vh % 16) == 0, "wino_input_h2: bad source / alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input_h2: bad tile or shape");
+  dim3 grid(grid_1d(g.T * cin_p / (tile == 6 ? 1 : 4)));
+  hipStream_t s = as_stream(stream);
+  const bool up = hi != H || wi != W;
+  const float sh = ac_scale(hi, H), sw = ac_scale(wi, W);
+  const H2Scale sc{amax_x, wino_beta(tile, 0)};
+  bf16_t* V = (bf16_t*)Vh;
+#define NSM_WI(m, u)                                                                             \
+  hipLaunchKernelGGL((wino_input_kernel<m, false, u, true>), grid, dim3(256), 0, s, x, ldx, H, W, \
+                     cin_p, g.TH, g.TW, g.T, nullptr, hi, wi, sh, sw, nullptr, V, sc)
+  if (tile == 2) {
+    if (up) NSM_WI(2, true); else NSM_WI(2, false);
+  } else if (tile == 4) {
+    if (up) NSM_WI(4, true); else NSM_WI(4, false);
+  } else {
+    if (up) NSM_WI(6, true); else NSM_WI(6, false);
+  }
+#undef NSM_WI
+  NSM_LAUNCH_CHECK("wino_input_h2");
+  return 0;
+}
+
+extern "C" int nsm_wino_dual_input_h2(const float* dy, int lddy, int B, int H, int W, int c_p,
+                                      int tile, void* Vh, void* dMh, const uint32_t* amax_dy,
+                                      void* stream) {
+  NSM_CHECK_ARG(dy && Vh && dMh && amax_dy && c_p % 32 == 0 && lddy % 4 == 0 && lddy >= c_p,
+                "wino_dual_input_h2: bad args");
+  NSM_CHECK_ARG(((uintptr_t)Vh % 16) == 0 && ((uintptr_t)dMh % 16) == 0, "wino_dual_input_h2: alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_dual_input_h2: bad tile or shape");
+  dim3 grid(grid_1d(g.T * c_p / (tile == 6 ? 1 : 4)));
+  hipStream_t s = as_stream(stream);
+  const H2Scale hv{amax_dy, wino_beta(tile, 0)}, hd{amax_dy, wino_beta(tile, 1)};
+#define A_ dy, lddy, H, W, c_p, g.TH, g.TW, g.T, nullptr, nullptr, WinoBnSrc{}, nullptr, nullptr, \
+           (bf16_t*)Vh, (bf16_t*)dMh, hv, hd
+  if (tile == 2) hipLaunchKernelGGL((wino_dual_kernel<2, false, true>), grid, dim3(256), 0, s, A_);
+  else if (tile == 4) hipLaunchKernelGGL((wino_dual_kernel<4, false, true>), grid, dim3(256), 0, s, A_);
+  else hipLaunchKernelGGL((wino_dual_kernel<6, false, true>), grid, dim3(256), 0, s, A_);
+#undef A_
+  NSM_LAUNCH_CHECK("wino_dual_input_h2");
+  return 0;
+}
+
+extern "C" size_t nsm_wino_wgrad_h2_ws(int B, int H, int W, int cin_p, int cout_p, int tile) {
+  WinoGeom g;
+  if (!wino_geom(tile, B, H, W, g)) return 0;
+  return plan_wino_wgrad(g.T, cin_p, cout_p, g.alpha2).slab_floats;
+}
+
+extern "C" int nsm_conv3x3_wgrad_wino_h2(const void* dMh, const void* Vh, int B, int H, int W,
+                                         int cin_p, int cout_p, int cin, int cout, int tile,
+                                         float* dw, float* ws, size_t ws_floats,
+                                         const uint32_t* amax_dy, const uint32_t* amax_x,
+                                         void* stream) {
+  NSM_CHECK_ARG(dMh && Vh && dw && ws && amax_dy && amax_x, "conv3x3_wgrad_wino_h2: null pointer");
+  NSM_CHECK_ARG(cin_p % 32 == 0 && cout_p % 32 == 0 && cin <= cin_p && cout <= cout_p,
+                "conv3x3_wgrad_wino_h2: bad channels");
+  NSM_CHECK_ARG(((uintptr_t)dMh % 16) == 0 && ((uintptr_t)Vh % 16) == 0 && ((uintptr_t)ws % 16) == 0,
+                "conv3x3_wgrad_wino_h2: alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "conv3x3_wgrad_wino_h2: bad tile or shape");
+  const int nb = g.alpha2;
+  WinoWgradPlan pl = plan_wino_wgrad(g.T, cin_p, cout_p, nb);
+  if (ws_floats < pl.slab_floats) return fail(NSM_E_WS, "conv3x3_wgrad_wino_h2: workspace too small");
+  NSM_CHECK_ARG(g.T * 2 * (long long)std::max(cin_p, cout_p) < (1ll << 30),
+                "conv3x3_wgrad_wino_h2: operand too large");
+  hipStream_t s = as_stream(stream);
+  const int M = cout_p, N = cin_p;
+  const int rc = wino_wgrad_gemm_h2((const bf16_t*)dMh, (const bf16_t*)Vh, g.T, cin_p, cout_p, nb,
+                                    pl.BM, pl.BN, pl.kchunk, pl.splits, ws,
+                                    H2Scale{amax_dy, wino_beta(tile, 1)},
+                                    H2Scale{amax_x, wino_beta(tile, 0)}, s);
+  if (rc) return rc;
+  return wgrad_wino_finish(ws, pl, nb, M, N, cin, cout, tile, dw, s);
+}
+
+extern "C" int nsm_to_h2(const float* x, int64_t rows, int C, const uint32_t* amax, float beta,
+                         void* out, void* stream) {
+  NSM_CHECK_ARG(x && out && amax && rows > 0 && C > 0 && C % 8 == 0 && beta > 0.f,
+                "to_h2: bad args");
+  const long long g = std::min<long long>(ceil_div(rows * (C / 4), 256), 8192);
+  hipLaunchKernelGGL(to_h2_kernel, dim3((int)g), dim3(256), 0, as_stream(stream), x,
+                     (long long)rows, C, H2Scale{amax, beta}, (bf16_t*)out);
+  NSM_LAUNCH_CHECK("to_h2");
+  return 0;
+}
+
+extern "C" int nsm_wino_gemm_h2(const void* V, const void* U, int B, int H, int W, int cin_p,
+                                int cout_p, int tile, float* Mb, const uint32_t* amax_v,
+                                float beta_v, const uint32_t* amax_u, float beta_u,
+                                void* stream) {
+  NSM_CHECK_ARG(V && U && Mb && amax_v && amax_u && cin_p % 32 == 0 && cout_p % 32 == 0,
+                "wino_gemm_h2: bad args");
+  NSM_CHECK_ARG(((uintptr_t)V % 16) == 0 && ((uintptr_t)U % 16) == 0 && ((uintptr_t)Mb % 16) == 0,
+                "wino_gemm_h2: 16B alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_gemm_h2: bad tile or shape");
+  NSM_CHECK_ARG(g.T * 2 * cin_p < (1ll << 30) && (long long)cout_p * 2 * cin_p < (1ll << 30),
+                "wino_gemm_h2: operand too large");
+  return wino_gemm_h2((const bf16_t*)V, (const bf16_t*)U, g.T, cin_p, cout_p, g.alpha2, Mb,
+                      H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, as_stream(stream));
+}
 
 // 1: fp32 GEMMs on the bf16 matrix cores by the exact split (default), 0: on
 // v_mfma_f32_32x32x2_f32; returns the previous mode

@@ -509,8 +509,10 @@ __global__ void __launch_bounds__(256) bn_act_pool_kernel(const T* __restrict__ 
                                                           const float* __restrict__ scale,
                                                           const float* __restrict__ shift,
                                                           float slope, T* __restrict__ z,
-                                                          T* __restrict__ pooled) {
+                                                          T* __restrict__ pooled,
+                                                          uint32_t* __restrict__ amax) {
   const int Hc = (H + 1) / 2, Wc = (W + 1) / 2, Ho = H / 2, Wo = W / 2, C = C8 * 8;
+  uint32_t am = 0;  // max|pooled| (the next Winograd conv's h2 scale source)
   const uint32_t total = (uint32_t)B * Hc * Wc * C8;
   for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
     const uint32_t p = fdiv(i, fdC8);
@@ -536,9 +538,15 @@ __global__ void __launch_bounds__(256) bn_act_pool_kernel(const T* __restrict__ 
       sum += q[1];
       sum += q[2];
       sum += q[3];
-      st8(pooled + (((size_t)b * Ho + cy) * Wo + cx) * C + c, 0.25f * sum);
+      const F8 pv = 0.25f * sum;
+      st8(pooled + (((size_t)b * Ho + cy) * Wo + cx) * C + c, pv);
+      if (amax) {
+        amax_fold(am, pv.a);
+        amax_fold(am, pv.b);
+      }
     }
   }
+  amax_flush(am, amax);
 }
 
 template <typename T, bool RED>
@@ -1953,7 +1961,7 @@ extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, 
 
 extern "C" int nsm_bn_act_pool(const void* y, int B, int H, int W, int C, const float* scale,
                                const float* shift, float slope, void* z, void* pooled, int dtype,
-                               void* stream) {
+                               uint32_t* amax, void* stream) {
   NSM_CHECK_ARG(y && z && pooled && scale && shift && C % 8 == 0 && H >= 2 && W >= 2,
                 "bn_act_pool: bad args");
   const long long work = (long long)B * ((H + 1) / 2) * ((W + 1) / 2) * (C / 8);
@@ -1964,11 +1972,11 @@ extern "C" int nsm_bn_act_pool(const void* y, int B, int H, int W, int C, const 
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(bn_act_pool_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(bf16_t, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,
-                       NSM_T(bf16_t, z), NSM_T(bf16_t, pooled));
+                       NSM_T(bf16_t, z), NSM_T(bf16_t, pooled), nullptr);
   else
     hipLaunchKernelGGL(bn_act_pool_kernel<float>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,
-                       NSM_T(float, z), NSM_T(float, pooled));
+                       NSM_T(float, z), NSM_T(float, pooled), amax);
   NSM_LAUNCH_CHECK("bn_act_pool");
   return 0;
 }

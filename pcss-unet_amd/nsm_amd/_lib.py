@@ -36,6 +36,13 @@ _SIGS = {
     "nsm_wino_gemm": (I, [P, P, I, I, I, I, I, I, P, P]),
     "nsm_wino_gemm_s": (I, [P, P, I, I, I, I, I, I, P, P, P, P]),
     "nsm_absmax": (I, [P, L, P, P]),
+    "nsm_to_h2": (I, [P, L, I, P, F, P, P]),
+    "nsm_wino_gemm_h2": (I, [P, P, I, I, I, I, I, I, P, P, F, P, F, P]),
+    "nsm_wino_beta": (F, [I, I]),
+    "nsm_wino_input_h2": (I, [P, I, I, I, I, I, I, I, I, P, P, P]),
+    "nsm_wino_dual_input_h2": (I, [P, I, I, I, I, I, I, P, P, P, P]),
+    "nsm_wino_wgrad_h2_ws": (Z, [I, I, I, I, I, I]),
+    "nsm_conv3x3_wgrad_wino_h2": (I, [P, P, I, I, I, I, I, I, I, I, P, P, Z, P, P, P]),
     "nsm_set_f32_split": (I, [I]),
     "nsm_wino_output": (I, [P, I, I, I, I, I, P, P, I, P]),
     "nsm_wino_wgrad_ws": (Z, [I, I, I, I, I, I]),
@@ -55,7 +62,7 @@ _SIGS = {
     "nsm_sum_rows": (I, [P, I, I, I, P, P]),
     "nsm_resize_fwd_act": (I, [P, I, I, I, I, P, I, I, P, P, F, P, I, P]),
     "nsm_up2_resize_fwd_act": (I, [P, I, I, I, I, P, I, I, P, P, F, P, I, P]),
-    "nsm_bn_act_pool": (I, [P, I, I, I, I, P, P, F, P, P, I, P]),
+    "nsm_bn_act_pool": (I, [P, I, I, I, I, P, P, F, P, P, I, P, P]),
     "nsm_wino_dual_input": (I, [P, I, I, I, I, I, I, P, P, P, P, P]),
     "nsm_wino_dual_input_bn": (I, [P, I, P, I, I, I, I, I, I, P, P, F, P, P, P, P, P, P, P, P]),
     "nsm_conv3x3_wgrad_wino_dm": (I, [P, P, I, I, I, I, I, I, I, I, P, P, Z, P, P, P]),
@@ -70,7 +77,7 @@ _SIGS = {
     "nsm_wino_stat_slots": (I, [I, I, I, I, I]),
     "nsm_conv1x1_bnbwd_chunks": (I, [I, I, I, I, I]),
     "nsm_conv1x1_dgrad_bnbwd": (I, [P, I, I, I, I, I, P, I, P, I, P, P, P, P, P, F, I, P, P, P, I,
-                                    I, P, P, P]),
+                                    I, P, P, P, P]),
     "nsm_avgpool2_fwd": (I, [P, I, I, I, I, P, I, P]),
     "nsm_avgpool2_bwd_add": (I, [P, I, I, I, I, P, P, I, P]),
     "nsm_resize_fwd": (I, [P, I, I, I, I, P, I, I, I, P]),

@@ -259,17 +259,28 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     Mb = empty(nb * T * cout_p, device=x.device)
     y = empty(M, cout_p, device=x.device)
     st = stream()
+    h2 = U.dtype == H2   # pre-split operands (csrc/nsm_conv_h2.inc)
     ev_all = _probe(tag)  # the whole convolution: input transform + GEMM + output transform
     if v_in is not None:
         V = v_in
+    elif h2:
+        # amax_v: max|x| (x's producer), the scale source of the h2 V
+        V = torch.empty(nb * T * 2 * cin_p, dtype=H2, device=x.device)
+        call("nsm_wino_input_h2", ptr(x), x.stride(0), B, hi, wi, H, W, cin_p, tile, ptr(V),
+             ptr(amax_v), st)
     else:
         V = empty(nb * T * cin_p, device=x.device)    # kept alive for the wgrad
         call("nsm_wino_input_resize", ptr(x), x.stride(0), B, hi, wi, H, W, cin_p, tile,
              int(relu), ptr(V), ptr(amax_v), st)
     ev = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
-    both = amax_v is not None and amax_u is not None
-    call("nsm_wino_gemm_s", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb),
-         ptr(amax_v) if both else None, ptr(amax_u) if both else None, st)
+    if h2:
+        assert V.dtype == H2 and amax_v is not None and amax_u is not None
+        call("nsm_wino_gemm_h2", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb),
+             ptr(amax_v), wino_beta(tile, 0), ptr(amax_u), wino_beta(tile, 2), st)
+    else:
+        both = amax_v is not None and amax_u is not None
+        call("nsm_wino_gemm_s", ptr(V), ptr(U), B, H, W, cin_p, cout_p, tile, ptr(Mb),
+             ptr(amax_v) if both else None, ptr(amax_u) if both else None, st)
     if ev is not None:
         ev.record()
     part = None
@@ -298,6 +309,32 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     if stats:
         return y, (V if keep_v else None), part
     return (y, V) if keep_v else y
+
+
+H2 = torch.float16   # storage dtype of the pre-split (h2) Winograd operands
+_BETA = {}
+
+
+def wino_beta(tile, which):
+    """nsm_wino_beta: the bound of a Winograd transform (0 input, 1 output
+    gradient, 2 filter) between an h2 operand and its scale source."""
+    key = (tile, which)
+    if key not in _BETA:
+        from ._lib import lib
+        _BETA[key] = float(lib.nsm_wino_beta(tile, which))
+    return _BETA[key]
+
+
+def wino_dual_input_h2(dy, B, H, W, tile, amax_dy):
+    """wino_dual_input writing (Vd, dM) as h2 tensors; amax_dy: max|dy| slot
+    (filled by dy's producer), their scale source."""
+    c_p = dy.shape[1]
+    n = (tile + 2) ** 2 * wino_tiles(B, H, W, tile) * 2 * c_p
+    Vd = torch.empty(n, dtype=H2, device=dy.device)
+    dM = torch.empty(n, dtype=H2, device=dy.device)
+    call("nsm_wino_dual_input_h2", ptr(dy), dy.stride(0), B, H, W, c_p, tile, ptr(Vd), ptr(dM),
+         ptr(amax_dy), stream())
+    return Vd, dM
 
 
 def wino_dual_input(dy, B, H, W, tile=4, amax=(None, None)):
@@ -345,9 +382,20 @@ def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, d
     max|V|) slots: with both (and dM given) the GEMM runs the f16x2 split."""
     from ._lib import lib
     cout_p = dy.shape[1]
+    ev = _probe(tag)
+    if dM is not None and dM.dtype == H2:
+        # h2 dM / V (wino_dual_input_h2, conv3x3_wino's h2 V): amax = (max|dy|, max|x|),
+        # their scale sources
+        assert V.dtype == H2 and amax[0] is not None and amax[1] is not None
+        n = int(lib.nsm_wino_wgrad_h2_ws(B, H, W, cin_p, cout_p, tile))
+        ws = empty(n, device=dy.device)
+        call("nsm_conv3x3_wgrad_wino_h2", ptr(dM), ptr(V), B, H, W, cin_p, cout_p, cin, cout,
+             tile, ptr(dw), ptr(ws), n, ptr(amax[0]), ptr(amax[1]), stream())
+        if ev is not None:
+            ev.record()
+        return
     n = int(lib.nsm_wino_wgrad_ws(B, H, W, cin_p, cout_p, tile))
     ws = empty(n, device=dy.device)
-    ev = _probe(tag)
     if dM is None:
         call("nsm_conv3x3_wgrad_wino", ptr(dy), dy.stride(0), ptr(V), B, H, W, cin_p, cout_p, cin,
              cout, tile, ptr(dw), ptr(ws), n, stream())
@@ -537,7 +585,8 @@ SUM_ROWS_ABOVE = int(os.environ.get("NSM_SUM_ROWS_ABOVE", "512"))  # BN-backward
 
 
 def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
-                         recompute, slope=0.2, tag=None, defer=False, amax=(None, None)):
+                         recompute, slope=0.2, tag=None, defer=False, amax=(None, None),
+                         amax_out=None):
     """dY1 of a DoubleConv's first BN from dY2 (grad wrt the 1x1 conv output):
     the 1x1 input gradient dA1 = dY2 W2 with the BN + LeakyReLU + Dropout2d
     backward in its epilogue (nsm_conv1x1_dgrad_bnbwd) — the same values as
@@ -546,7 +595,8 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     (dA1 never stored); False: one pass storing dA1 + partials, then
     nsm_bn_bwd_apply. defer=True (with recompute=False): DeferredBnBwd(dA1,
     coef) instead of dy, the apply pass left to the consumer. amax = (max|dY2|,
-    max|w2d|) slots: the fp32 GEMM passes run the f16x2 split."""
+    max|w2d|) slots: the fp32 GEMM passes run the f16x2 split. amax_out: slot
+    receiving max|dY1| (fp32; the h2 scale source of its Winograd transforms)."""
     from ._lib import lib
     M, cop = dY2.shape
     C = y.shape[1]
@@ -561,7 +611,7 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     ev = _probe(tag)
     am = _pair(amax) if dtc == NSM_F32 else (None, None)
     call("nsm_conv1x1_dgrad_bnbwd", *args, 0 if recompute else 1, ptr(partial), None, ptr(dA1),
-         dA1.stride(0) if dA1 is not None else 0, dtc, *am, stream())
+         dA1.stride(0) if dA1 is not None else 0, dtc, *am, None, stream())
     if nchunk > SUM_ROWS_ABOVE:
         G = -(-nchunk // SUM_ROWS_ABOVE)
         n2 = -(-nchunk // G)
@@ -578,11 +628,11 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     dy = like(M, C, y)
     if recompute:
         call("nsm_conv1x1_dgrad_bnbwd", *args, 2, None, ptr(coef), ptr(dy), dy.stride(0), dtc,
-             *am, stream())
+             *am, ptr(amax_out) if dtc == NSM_F32 else None, stream())
     else:
         call("nsm_bn_bwd_apply", ptr(dA1), dA1.stride(0), ptr(y), y.stride(0), M, C, H * W,
              ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy),
-             dy.stride(0), dtc, None, stream())
+             dy.stride(0), dtc, ptr(amax_out) if dtc == NSM_F32 else None, stream())
     if ev is not None:
         ev.record()
     return dy
@@ -681,13 +731,14 @@ def up2_resize_act(z, B, h, w, th, tw, slope=0.2):
     return y
 
 
-def bn_act_pool(y, st, B, H, W, slope=0.2):
-    """(z, avgpool2(z)) with z = lrelu(y*scale+shift), one read of y."""
+def bn_act_pool(y, st, B, H, W, slope=0.2, amax=None):
+    """(z, avgpool2(z)) with z = lrelu(y*scale+shift), one read of y.
+    amax: operand-maximum slot receiving max|pooled| (fp32)."""
     C = y.shape[-1]
     z = like(B * H * W, C, y)
     pooled = like(B * (H // 2) * (W // 2), C, y)
     call("nsm_bn_act_pool", ptr(y), B, H, W, C, ptr(st.scale), ptr(st.shift), slope, ptr(z),
-         ptr(pooled), dt(y), stream())
+         ptr(pooled), dt(y), ptr(amax) if y.dtype == F32 else None, stream())
     return z, pooled
 
 

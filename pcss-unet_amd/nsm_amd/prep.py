@@ -12,6 +12,7 @@ parameter storage), instead of ~40 small launches. `LazyBlockWeights` is the
 per-call path (a standalone DoubleConv).
 """
 import ctypes
+import os
 
 import torch
 
@@ -24,7 +25,11 @@ class NsmPrepJob(ctypes.Structure):
                 ("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("amax", ctypes.c_void_p)]
 
 
-KIND_PACK_F32, KIND_PACK_BF16, KIND_WINO, KIND_PAD = 0, 1, 2, 3
+KIND_PACK_F32, KIND_PACK_BF16, KIND_WINO, KIND_PAD, KIND_WINO_H2 = 0, 1, 2, 3, 4
+# NSM_H2=0: the fp32 training step keeps fp32 Winograd operands (the GEMMs
+# split them in-kernel, nsm_conv_split16.inc) instead of the pre-split h2
+# tensors their producers write (nsm_conv_h2.inc)
+H2_WINO = os.environ.get("NSM_H2", "1") != "0"
 
 
 class LazyBlockWeights:
@@ -74,7 +79,8 @@ class _PreparedBlock:
         return self.t[("U1", flip)]
 
     def amax_U1(self, flip):
-        """max|U| of the step's Winograd weight (written by the prep launch)."""
+        """max|U| of the step's Winograd weight (written by the prep launch);
+        for an h2 U (float16 storage) max|w| of the filters, its scale source."""
         return self.t.get(("amaxU1", flip))
 
     def amax_w2(self, mode):
@@ -142,13 +148,19 @@ class StepWeights:
             modes = (ops.PACK_FWD, ops.PACK_DGRAD) if training else (ops.PACK_FWD,)
             if cip >= wino_min and dtype == torch.float32:
                 tile = wino_tile(cip, h, w)
+                h2 = training and H2_WINO
                 for flip in ((False, True) if training else (False,)):
                     am = ops.amax_slot(self.amax, n_am)
                     n_am += 1
                     pb.t[("amaxU1", flip)] = am
-                    pb.t[("U1", flip)] = add(KIND_WINO, (ci, ci, cip, cip, int(flip), tile),
-                                             c0.weight, (tile + 2) ** 2 * cip * cip, torch.float32,
-                                             amax=am)
+                    if h2:   # pre-split U [alpha^2][cip][2 cip] float16 (nsm_conv_h2.inc)
+                        pb.t[("U1", flip)] = add(KIND_WINO_H2, (ci, ci, cip, cip, int(flip), tile),
+                                                 c0.weight, (tile + 2) ** 2 * cip * 2 * cip,
+                                                 ops.H2, amax=am)
+                    else:
+                        pb.t[("U1", flip)] = add(KIND_WINO, (ci, ci, cip, cip, int(flip), tile),
+                                                 c0.weight, (tile + 2) ** 2 * cip * cip,
+                                                 torch.float32, amax=am)
             else:
                 for mode in modes:
                     pb.t[("w1", mode)] = add(pk, (ci, ci, 9, cip, cip, mode), c0.weight,

@@ -423,8 +423,10 @@ class _BlockSaved:
 
 
 # a block's operand-maximum slots (the f16x2 GEMMs' operand scales, filled by
-# the operands' producers): Winograd V, Vd, dM; the 1x1 conv's A1 and dY2
-AM_V, AM_VD, AM_DM, AM_A1, AM_DY2, AM_PER_BLOCK = 0, 1, 2, 3, 4, 5
+# the operands' producers): Winograd V, Vd, dM; the 1x1 conv's A1 and dY2; the
+# scale sources of the pre-split (h2) Winograd operands: the block input X
+# (written by the previous block's output pass) and dY1
+AM_V, AM_VD, AM_DM, AM_A1, AM_DY2, AM_X, AM_DY1, AM_PER_BLOCK = 0, 1, 2, 3, 4, 5, 6, 7
 
 
 def _slot(am, i):
@@ -436,6 +438,16 @@ def _block_slots(amax, k):
     """Block k's operand-maximum slots of the step's buffer, or None."""
     w = ops.AMAX_WORDS * AM_PER_BLOCK
     return None if amax is None else amax[k * w:(k + 1) * w]
+
+
+def _x_slot(amax, k):
+    """Block k's input-maximum slot (AM_X), filled by the pass that writes
+    block k's input (or the tensor it is resampled from), or None."""
+    return _slot(_block_slots(amax, k), AM_X)
+
+
+def _is_h2(U):
+    return U is not None and U.dtype == ops.H2
 
 
 def fuses_resize(blk, dtype):
@@ -501,17 +513,19 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         tile = wino_tile(cip, H, W)
         U1 = pw.U1(tile, False)
+        # h2 U: V is written pre-split, scaled from max|X| (AM_X)
+        am_v = _slot(am, AM_X if _is_h2(U1) else AM_V)
         part1 = None
         if training and WINO_BN_STATS:
             # the output transform also writes the BN batch-statistics partials
             Y1, V, part1 = ops.conv3x3_wino(xin, B, H, W, U1, b1, cip, tile=tile,
                                             tag=name + ".conv.0.fwd", keep_v=True, stats=True,
-                                            src_hw=src_hw, amax_v=_slot(am, AM_V),
+                                            src_hw=src_hw, amax_v=am_v,
                                             amax_u=pw.amax_U1(False))
         else:
             Y1, V = ops.conv3x3_wino(xin, B, H, W, U1, b1, cip, tile=tile,
                                      tag=name + ".conv.0.fwd", keep_v=True, src_hw=src_hw,
-                                     amax_v=_slot(am, AM_V), amax_u=pw.amax_U1(False))
+                                     amax_v=am_v, amax_u=pw.amax_U1(False))
         if training and part1 is None:
             part1 = ops.bn_partials(Y1)
     else:
@@ -573,19 +587,36 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
                        pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
     mode = bnb_mode(s.cip, s.cop, dtype)
+    # pre-split (h2) Winograd operands: dY1's producer records max|dY1|, the
+    # scale source of both its transforms (Vd, dM)
+    h2 = s.V is not None and s.V.dtype == ops.H2
+    am_dy1 = _slot(s.am, AM_DY1) if h2 else None
     # dY1 is consumed only by its two Winograd transforms: leave the BN apply
     # to the dual transform kernel, dY1 is never stored
-    lazy = s.V is not None and need_dx and DUAL_TRANSFORM and LAZY_DY1
+    lazy = s.V is not None and need_dx and DUAL_TRANSFORM and LAZY_DY1 and not h2
     if mode:
         dY1 = ops.conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
                                        g[bn1m.bias], g[c0.bias], mode == 2,
-                                       tag=name + ".conv.4.dgrad", defer=lazy, amax=am_w2d)
+                                       tag=name + ".conv.4.dgrad", defer=lazy, amax=am_w2d,
+                                       amax_out=am_dy1)
     else:
         dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad",
                            amax=am_w2d)
         dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias],
-                         g[c0.bias], defer=lazy)
+                         g[c0.bias], defer=lazy, amax=am_dy1)
     Vd = None
+    if h2:
+        tile = wino_tile(s.cip, H, W)
+        Vd, dM = ops.wino_dual_input_h2(dY1, B, H, W, tile, am_dy1)
+        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=tile,
+                               tag=name + ".conv.0.wgrad", dM=dM,
+                               amax=(am_dy1, _slot(s.am, AM_X)))
+        s.V = None
+        if not need_dx:
+            return None
+        return ops.conv3x3_wino(dY1, B, H, W, s.pw.U1(tile, True), None, s.cip, tile=tile,
+                                tag=name + ".conv.0.dgrad", v_in=Vd, amax_v=am_dy1,
+                                amax_u=s.pw.amax_U1(True))
     if s.V is not None:
         tile = wino_tile(s.cip, H, W)
         dM = None
@@ -682,11 +713,14 @@ class _UnetFn(torch.autograd.Function):
                     if k < 5:
                         inp = ops.avgpool2(c[k], B, h, w)
                 elif k < 5 and ACT_POOL:   # z and its pooling from one read of Y2
-                    c[k], inp = ops.bn_act_pool(s.Y2, s.bn2, B, h, w, SLOPE)
+                    c[k], inp = ops.bn_act_pool(s.Y2, s.bn2, B, h, w, SLOPE,
+                                                amax=_x_slot(amax, k + 1))
                 elif k == 5 and LAZY_DECODER and cdt == torch.bfloat16:
                     c[k] = ops.Lazy(s.Y2, s.bn2, None)   # sampled by conv6's upsample
                 else:
-                    c[k] = ops.bn_act(s.Y2, s.bn2, SLOPE)
+                    # max|c_k| bounds the next block's input (its pooling or
+                    # bilinear upsample), the scale source of an h2 V
+                    c[k] = ops.bn_act(s.Y2, s.bn2, SLOPE, amax=_x_slot(amax, k + 1))
                     if k < 5:
                         inp = ops.avgpool2(c[k], B, h, w)
                 if k < 5:
@@ -723,7 +757,8 @@ class _UnetFn(torch.autograd.Function):
                 elif k != 9 and LAZY_DECODER and cdt == torch.bfloat16:
                     cur = ops.Lazy(s.Y2, s.bn2, res)     # only the next upsample reads it
                 else:
-                    cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res)
+                    cur = ops.bn_act(s.Y2, s.bn2, SLOPE, res=res,
+                                     amax=_x_slot(amax, k + 1) if k < 9 else None)
                 h, w = th, tw
         z9 = cur
         with ops.stage("head.fwd"):
