@@ -272,10 +272,15 @@ def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
                   2: (3, BF16_PEAK_TFLOPS)}[mode]
     work = mult * ex_flops
     achieved = work / (gemm_ms * 1e-3) / 1e12
-    return {"kernel": f"conv6.conv.0.fwd Winograd F({m}x{m},3x3) batched GEMM nsm_wino_gemm "
+    from nsm_amd.prep import H2_WINO
+    f16 = ("gemm_h2_kernel<256,256> (fp32 via the f16x2 split: the two fp16 terms of each "
+           "power-of-two scaled operand written by its producer, LDS-DMA, 3 products on "
+           "v_mfma_f32_32x32x16_f16)" if H2_WINO else
+           "gemm_f32h_kernel (fp32 via the f16x2 split of power-of-two scaled operands, 3 "
+           "products on v_mfma_f32_32x32x16_f16)")
+    return {"kernel": f"conv6.conv.0.fwd Winograd F({m}x{m},3x3) batched GEMM "
                       f"({nb} x M={T6} N=1024 K=1024), B={B} at {h6}x{w6}: "
-                      + {2: "gemm_f32h_kernel (fp32 via the f16x2 split of power-of-two scaled "
-                            "operands, 3 products on v_mfma_f32_32x32x16_f16)",
+                      + {2: f16,
                          1: "gemm_f32s_kernel (fp32 via the exact 3-way bf16 split, 6 products on "
                             "v_mfma_f32_32x32x16_bf16)",
                          0: "gemm_f32_kernel (v_mfma_f32_32x32x2_f32)"}[mode],

@@ -47,6 +47,14 @@ def set_f32_split(mode):
     return int(lib.nsm_set_f32_split(int(mode)))
 
 
+def get_f32_split():
+    """The current fp32 GEMM arithmetic mode (set_f32_split / NSM_F32_SPLIT)."""
+    from ._lib import lib
+    m = int(lib.nsm_set_f32_split(-1))
+    lib.nsm_set_f32_split(m)
+    return m
+
+
 # ---- parameters ------------------------------------------------------------
 def pack_conv_weight(w, cout_p, cin_p, mode, dtype=F32):
     """MFMA operand layout of a conv weight, in the activations' dtype."""

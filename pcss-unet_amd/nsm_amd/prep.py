@@ -100,7 +100,7 @@ class StepWeights:
     layouts of DoubleConv k. Valid while the parameters keep their storage
     (`valid()` checks the pointers)."""
 
-    def __init__(self, mod, dtype, shapes, training, wino_min, wino_tile):
+    def __init__(self, mod, dtype, shapes, training, wino_min, wino_tile, h2=False):
         dev = mod.conv10.weight.device
         self.params = [p for p in mod.parameters()]
         self.ptrs = [p.data_ptr() for p in self.params]
@@ -148,12 +148,11 @@ class StepWeights:
             modes = (ops.PACK_FWD, ops.PACK_DGRAD) if training else (ops.PACK_FWD,)
             if cip >= wino_min and dtype == torch.float32:
                 tile = wino_tile(cip, h, w)
-                h2 = training and H2_WINO
                 for flip in ((False, True) if training else (False,)):
                     am = ops.amax_slot(self.amax, n_am)
                     n_am += 1
                     pb.t[("amaxU1", flip)] = am
-                    if h2:   # pre-split U [alpha^2][cip][2 cip] float16 (nsm_conv_h2.inc)
+                    if h2 and training:   # pre-split U [alpha^2][cip][2 cip] float16 (nsm_conv_h2.inc)
                         pb.t[("U1", flip)] = add(KIND_WINO_H2, (ci, ci, cip, cip, int(flip), tile),
                                                  c0.weight, (tile + 2) ** 2 * cip * 2 * cip,
                                                  ops.H2, amax=am)

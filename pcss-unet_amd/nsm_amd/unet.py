@@ -27,7 +27,7 @@ import torch.nn as nn
 
 from . import ops, optim
 from ._lib import call, ptr, require_gpu, stream
-from .prep import LazyBlockWeights, StepWeights
+from .prep import H2_WINO, LazyBlockWeights, StepWeights
 
 SLOPE = 0.2
 # 3x3 convolutions with at least this many (padded) input channels use the
@@ -665,12 +665,14 @@ def _step_weights(mod, dtype, Rh, Rw, training):
     NSM_PREP_BATCH=0: None (every block packs its own, one launch per layout)."""
     if not PREP_BATCH:
         return None
-    key = (dtype, Rh, Rw, bool(training), WINOGRAD_MIN_CHANNELS)
+    # pre-split (h2) Winograd operands in fp32 training with the f16x2 arithmetic
+    h2 = bool(training) and dtype == torch.float32 and H2_WINO and ops.get_f32_split() == 2
+    key = (dtype, Rh, Rw, bool(training), WINOGRAD_MIN_CHANNELS, h2)
     cache = mod.__dict__.setdefault("_step_weights", {})
     sw = cache.get(key)
     if sw is None or not sw.valid(mod):
         sw = cache[key] = StepWeights(mod, dtype, block_shapes(Rh, Rw), training,
-                                      WINOGRAD_MIN_CHANNELS, wino_tile)
+                                      WINOGRAD_MIN_CHANNELS, wino_tile, h2=h2)
     sw.run()
     return sw
 

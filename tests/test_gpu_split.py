@@ -151,3 +151,94 @@ def test_split_train_step_vs_oracle(ops, device):
     for mode in (1, 2):
         assert errs[mode][0] <= 2.0 * errs[0][0] + 1e-6
         assert errs[mode][1] <= 2.0 * errs[0][1] + 1e-6
+
+
+def _h2(ops, t, rows, C, amax, beta):
+    """fp32 [rows][C] -> h2 tensor (nsm_to_h2) with scale source (amax, beta)."""
+    from nsm_amd._lib import call, ptr, stream
+    out = torch.empty(rows * 2 * C, dtype=ops.H2, device=t.device)
+    call("nsm_to_h2", ptr(t), rows, C, ptr(amax), beta, ptr(out), stream())
+    return out
+
+
+@pytest.mark.parametrize("tile", [4, 6])
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 9, 11, 32, 64), (1, 16, 16, 256, 128), (2, 7, 5, 64, 32),
+                                        (2, 32, 32, 512, 256), (1, 40, 36, 128, 64), (2, 24, 30, 64, 128)])
+def test_h2_matches_fp32_accuracy(ops, device, B, H, W, ci, co, tile):
+    """The pre-split (h2) Winograd path (csrc/nsm_conv_h2.inc): the input / dual
+    transforms write the two fp16 terms scaled from max|x| / max|dy| times the
+    transform bound, U from max|w| times the filter bound, and the LDS-DMA f16
+    GEMMs run fwd, dgrad and wgrad. Against a float64 convolution the error
+    stays within that of the fp32-MFMA path (same bounds as the f16x2 split)."""
+    g = torch.Generator().manual_seed(ci * 5 + co + W + tile)
+    x = torch.randn(B, ci, H, W, generator=g, dtype=torch.float64, requires_grad=True)
+    w = (torch.randn(co, ci, 3, 3, generator=g, dtype=torch.float64) / (ci * 9) ** 0.5).requires_grad_(True)
+    dy = torch.randn(B, co, H, W, generator=g, dtype=torch.float64)
+    ref = F.conv2d(x, w, padding=1)
+    ref.backward(dy)
+    xs, ws, dys = x.detach().float(), w.detach().float(), dy.float()
+    xd, dyd, wd = nhwc(xs).to(device), nhwc(dys).to(device), ws.to(device)
+    nb = (tile + 2) ** 2
+    res = {}
+    for mode in ("fp32", "h2"):
+        ops.set_f32_split(0 if mode == "fp32" else 2)
+        U = ops.wino_weight(wd, co, ci, flip=False, tile=tile)
+        Ud = ops.wino_weight(wd, ci, co, flip=True, tile=tile)
+        dw = torch.empty(co, ci, 3, 3, device=device)
+        if mode == "fp32":
+            y, V = ops.conv3x3_wino(xd, B, H, W, U, None, co, tile=tile, keep_v=True)
+            Vd, dM = ops.wino_dual_input(dyd, B, H, W, tile=tile)
+            dx = ops.conv3x3_wino(dyd, B, H, W, Ud, None, ci, tile=tile, v_in=Vd)
+            ops.conv3x3_wgrad_wino(dyd, V, B, H, W, ci, ci, co, dw, tile=tile, dM=dM)
+        else:
+            aw, ax, ady = ops.absmax(wd), ops.absmax(xd), ops.absmax(dyd)
+            bg = ops.wino_beta(tile, 2)
+            Uh = _h2(ops, U, nb * co, ci, aw, bg)
+            Udh = _h2(ops, Ud, nb * ci, co, aw, bg)
+            y, V = ops.conv3x3_wino(xd, B, H, W, Uh, None, co, tile=tile, keep_v=True,
+                                    amax_v=ax, amax_u=aw)
+            assert V.dtype == ops.H2
+            Vd, dM = ops.wino_dual_input_h2(dyd, B, H, W, tile, ady)
+            dx = ops.conv3x3_wino(dyd, B, H, W, Udh, None, ci, tile=tile, v_in=Vd, amax_v=ady,
+                                  amax_u=aw)
+            ops.conv3x3_wgrad_wino(dyd, V, B, H, W, ci, ci, co, dw, tile=tile, dM=dM,
+                                   amax=(ady, ax))
+        res[mode] = (_errs(nchw(y.cpu(), B, H, W), ref.detach()),
+                     _errs(nchw(dx.cpu(), B, H, W), x.grad), _errs(dw.cpu(), w.grad))
+    ops.set_f32_split(2)
+    for i, name in enumerate(("fwd", "dgrad", "wgrad")):
+        (m0, r0), (m2, r2) = res["fp32"][i], res["h2"][i]
+        print(f"h2 F({tile}) {name}: fp32-MFMA max {m0:.2e} rms {r0:.2e} | h2 max {m2:.2e} rms {r2:.2e}")
+        assert r2 <= 1.5 * r0 + 1e-9, (name, r0, r2)
+        assert m2 <= 2.0 * m0 + 1e-8, (name, m0, m2)
+
+
+def test_h2_prep_matches_to_h2(ops, device):
+    """The step's weight preparation (prep kind 4: max|w| pass, then U written
+    pre-split) gives bitwise the h2 tensor of nsm_wino_weight's U scaled from
+    max|w| x the filter bound, for the forward and the input-gradient filters."""
+    from nsm_amd import Unet
+    from nsm_amd.prep import StepWeights
+    from nsm_amd.unet import WINOGRAD_MIN_CHANNELS, block_shapes, wino_tile
+    torch.manual_seed(3)
+    m = Unet(in_ch=7).to(device).train()
+    sw = StepWeights(m, torch.float32, block_shapes(64, 64), True, WINOGRAD_MIN_CHANNELS,
+                     wino_tile, h2=True)
+    sw.run()
+    for k in (3, 6, 9):
+        blk = m.block(k)
+        cip = ops.pad32(blk.conv[0].in_channels)
+        h, w_ = block_shapes(64, 64)[k]
+        tile = wino_tile(cip, h, w_)
+        pb = sw.block(k)
+        wt = blk.conv[0].weight.detach()
+        aw = ops.absmax(wt.contiguous())
+        nb = (tile + 2) ** 2
+        for flip in (False, True):
+            U = ops.wino_weight(wt, cip, cip, flip=flip, tile=tile)
+            ref = _h2(ops, U, nb * cip, cip, aw, ops.wino_beta(tile, 2))
+            got = pb.U1(tile, flip)
+            assert got.dtype == ops.H2
+            assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (k, flip)
+            # the slot the GEMMs read holds max|w|
+            assert torch.equal(pb.amax_U1(flip).max(), aw.max()), (k, flip)
