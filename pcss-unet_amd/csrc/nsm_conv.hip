@@ -2597,10 +2597,44 @@ extern "C" int nsm_wino_dual_input_h2(const float* dy, int lddy, int B, int H, i
   return 0;
 }
 
+// NSM_H2_WG256=0: the h2 weight gradients keep 128x128 tiles where 256x256 fit
+static bool h2_wg256() {
+  static bool v = [] {
+    const char* e = getenv("NSM_H2_WG256");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
+// the h2 weight-gradient plan: plan_wino_wgrad's, or 256x256 tiles (8 waves,
+// the forward's tile) where both channel counts are multiples of 256, with the
+// split count that brings the grid to ~1024 blocks (4 rounds of one block per CU)
+static WinoWgradPlan plan_wino_wgrad_h2(long long T, int cin_p, int cout_p, int nb) {
+  WinoWgradPlan p = plan_wino_wgrad(T, cin_p, cout_p, nb);
+  if (!h2_wg256() || cin_p % 256 || cout_p % 256) return p;
+  p.BM = p.BN = 256;
+  const long long tiles = (long long)(cout_p / 256) * (cin_p / 256) * nb;
+  long long sp = (1024 + tiles - 1) / tiles, maxs = (T + 255) / 256;
+  if (sp > maxs) sp = maxs;
+  if (sp > 64) sp = 64;
+  if (sp < 1) sp = 1;
+  long long kc = (T + sp - 1) / sp;
+  kc = (kc + BK - 1) / BK * BK;
+  sp = (T + kc - 1) / kc;
+  // (conv5's F(4x4) at 32x32: 144 tiles x 2 splits = 288 blocks, measured
+  // 52.5 -> 63.5 us: keep the 128x128 plan under three rounds of blocks)
+  if (tiles * sp < 768) return plan_wino_wgrad(T, cin_p, cout_p, nb);
+  p.splits = (int)sp;
+  p.kchunk = (int)kc;
+  p.slab_floats = (size_t)nb * sp * cout_p * cin_p;
+  if (sp > 1) p.slab_floats += (size_t)nb * cout_p * cin_p;
+  return p;
+}
+
 extern "C" size_t nsm_wino_wgrad_h2_ws(int B, int H, int W, int cin_p, int cout_p, int tile) {
   WinoGeom g;
   if (!wino_geom(tile, B, H, W, g)) return 0;
-  return plan_wino_wgrad(g.T, cin_p, cout_p, g.alpha2).slab_floats;
+  return plan_wino_wgrad_h2(g.T, cin_p, cout_p, g.alpha2).slab_floats;
 }
 
 extern "C" int nsm_conv3x3_wgrad_wino_h2(const void* dMh, const void* Vh, int B, int H, int W,
@@ -2616,7 +2650,7 @@ extern "C" int nsm_conv3x3_wgrad_wino_h2(const void* dMh, const void* Vh, int B,
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "conv3x3_wgrad_wino_h2: bad tile or shape");
   const int nb = g.alpha2;
-  WinoWgradPlan pl = plan_wino_wgrad(g.T, cin_p, cout_p, nb);
+  WinoWgradPlan pl = plan_wino_wgrad_h2(g.T, cin_p, cout_p, nb);
   if (ws_floats < pl.slab_floats) return fail(NSM_E_WS, "conv3x3_wgrad_wino_h2: workspace too small");
   NSM_CHECK_ARG(g.T * 2 * (long long)std::max(cin_p, cout_p) < (1ll << 30),
                 "conv3x3_wgrad_wino_h2: operand too large");
