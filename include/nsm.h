@@ -367,7 +367,8 @@ int nsm_up2_resize_bwd_bnred(const void* dy, int B, int h, int w, int C, void* d
 /* ---- model boundary ---------------------------------------------------------
  * pixel_unshuffle(2) + NCHW->NHWC + channel pad (Unetmodel.py:65-67,101) */
 int nsm_input_prep(const float* x, int B, int C, int H, int W, void* out, int cp, int dtype,
-                   void* stream);
+                   uint32_t* amax, void* stream);
+/* (amax: fp32, may be NULL — max|out|, conv2's f16x2 operand scale) */
 int nsm_input_grad(const void* dX, int B, int C, int H, int W, int cp, float* dx, int dtype,
                    void* stream);
 /* conv10 1x1 16->4 + pixel_shuffle(2) + sigmoid (Unetmodel.py:63,143-148) */

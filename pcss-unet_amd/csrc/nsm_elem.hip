@@ -1423,9 +1423,11 @@ static bool sep_resize() {
 template <typename T>
 __global__ void __launch_bounds__(256) input_prep_kernel(const float* __restrict__ x, int B, int C,
                                                          int H, int W, T* __restrict__ out, int cp,
-                                                         uint32_t npix, FastDiv fdRw, FastDiv fdRh) {
+                                                         uint32_t npix, FastDiv fdRw, FastDiv fdRh,
+                                                         uint32_t* __restrict__ amax) {
   const int Rh = H / 2, Rw = W / 2;
   const size_t plane = (size_t)H * W;
+  uint32_t am = 0;  // max|out| (conv2's f16x2 operand scale)
   for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < npix; p += gridDim.x * 256u) {
     const uint32_t t = fdiv(p, fdRw);
     const int rx = (int)(p - t * (uint32_t)Rw);
@@ -1439,10 +1441,15 @@ __global__ void __launch_bounds__(256) input_prep_kernel(const float* __restrict
         const int c = 2 * g + (q >> 1);
         r[q] = c < C ? *(const f32x2*)(src + (size_t)c * plane + (q & 1) * W) : f32x2{0.f, 0.f};
       }
-      st8(out + (size_t)p * cp + 8 * g,
-          F8{f32x4{r[0].x, r[0].y, r[1].x, r[1].y}, f32x4{r[2].x, r[2].y, r[3].x, r[3].y}});
+      const F8 v{f32x4{r[0].x, r[0].y, r[1].x, r[1].y}, f32x4{r[2].x, r[2].y, r[3].x, r[3].y}};
+      st8(out + (size_t)p * cp + 8 * g, v);
+      if (amax) {
+        amax_fold(am, v.a);
+        amax_fold(am, v.b);
+      }
     }
   }
+  amax_flush(am, amax);
 }
 
 template <typename T>
@@ -2325,7 +2332,7 @@ extern "C" int nsm_up2_resize_bwd_bnred(const void* dy, int B, int h, int w, int
 #undef NSM_DT
 
 extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, void* out, int cp,
-                              int dtype, void* stream) {
+                              int dtype, uint32_t* amax, void* stream) {
   NSM_CHECK_ARG(x && out && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C && cp % 8 == 0,
                 "input_prep: bad args");
   NSM_CHECK_ARG(((uintptr_t)x % 8) == 0, "input_prep: x must be 8-byte aligned");
@@ -2335,10 +2342,10 @@ extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, void* 
   const FastDiv fw = make_fastdiv(W / 2), fh = make_fastdiv(H / 2);
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(input_prep_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
-                       NSM_T(bf16_t, out), cp, (uint32_t)npix, fw, fh);
+                       NSM_T(bf16_t, out), cp, (uint32_t)npix, fw, fh, nullptr);
   else
     hipLaunchKernelGGL(input_prep_kernel<float>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
-                       NSM_T(float, out), cp, (uint32_t)npix, fw, fh);
+                       NSM_T(float, out), cp, (uint32_t)npix, fw, fh, amax);
   NSM_LAUNCH_CHECK("input_prep");
   return 0;
 }

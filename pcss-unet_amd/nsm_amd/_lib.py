@@ -84,7 +84,7 @@ _SIGS = {
     "nsm_resize_bwd": (I, [P, I, I, I, I, P, I, I, I, P]),
     "nsm_up2_resize_fwd": (I, [P, I, I, I, I, P, I, I, I, P]),
     "nsm_up2_resize_bwd": (I, [P, I, I, I, I, P, I, I, I, P]),
-    "nsm_input_prep": (I, [P, I, I, I, I, P, I, I, P]),
+    "nsm_input_prep": (I, [P, I, I, I, I, P, I, I, P, P]),
     "nsm_input_grad": (I, [P, I, I, I, I, I, P, I, P]),
     "nsm_head_fwd": (I, [P, I, I, I, I, P, P, P, I, P]),
     "nsm_head_bwd_blocks": (I, [I, I, I]),

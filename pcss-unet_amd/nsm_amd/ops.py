@@ -772,11 +772,13 @@ def up2_resize_bwd(dy, B, h, w, th, tw, bnred=None):
 
 
 # ---- boundary ----------------------------------------------------------------
-def input_prep(x, cp, dtype=F32):
-    """fp32 NCHW model input -> NHWC [B*H/2*W/2, cp] activations in `dtype`."""
+def input_prep(x, cp, dtype=F32, amax=None):
+    """fp32 NCHW model input -> NHWC [B*H/2*W/2, cp] activations in `dtype`.
+    amax: operand-maximum slot receiving max|out| (fp32)."""
     B, C, H, W = x.shape
     out = torch.empty(B * (H // 2) * (W // 2), cp, dtype=dtype, device=x.device)
-    call("nsm_input_prep", ptr(x), B, C, H, W, ptr(out), cp, dt(out), stream())
+    call("nsm_input_prep", ptr(x), B, C, H, W, ptr(out), cp, dt(out),
+         ptr(amax) if dtype == F32 else None, stream())
     return out
 
 

@@ -57,6 +57,9 @@ class LazyBlockWeights:
     def amax_w2(self, mode):
         return None
 
+    def amax_w1(self, mode):
+        return None
+
     def w1(self, mode):
         return ops.pack_conv_weight(self.blk.conv[0].weight.detach(), self.cip, self.cip, mode,
                                     self.dtype)
@@ -87,6 +90,10 @@ class _PreparedBlock:
         """max|packed 1x1 weight| (fp32 packs; written by the prep launch)."""
         return self.t.get(("amaxw2", mode))
 
+    def amax_w1(self, mode):
+        """max|packed direct 3x3 weight| (fp32 packs; written by the prep launch)."""
+        return self.t.get(("amaxw1", mode))
+
     def w1(self, mode):
         return self.t[("w1", mode)]
 
@@ -108,8 +115,8 @@ class StepWeights:
         jobs, keep = [], []
         base = 0
         # slots: Winograd U (fwd, dgrad) and the packed 1x1 weights (fwd, dgrad)
-        n_wino = (sum(1 for k in shapes if ops.pad32(mod.block(k).conv[0].in_channels) >= wino_min)
-                  * 2 + len(shapes) * 2) if dtype == torch.float32 else 0
+        # (fwd + dgrad of each block's 3x3 and 1x1 weight)
+        n_wino = len(shapes) * 4 if dtype == torch.float32 else 0
         # per-step maxima of the Winograd weights (the f16x2 GEMMs' operand
         # scales), zeroed by run() before the prep launch refills them
         self.amax = ops.amax_slots(max(n_wino, 1), dev)
@@ -162,8 +169,13 @@ class StepWeights:
                                                  torch.float32, amax=am)
             else:
                 for mode in modes:
+                    am = None
+                    if dtype == torch.float32:
+                        am = ops.amax_slot(self.amax, n_am)
+                        n_am += 1
+                        pb.t[("amaxw1", mode)] = am
                     pb.t[("w1", mode)] = add(pk, (ci, ci, 9, cip, cip, mode), c0.weight,
-                                             cip * 9 * cip, dtype)
+                                             cip * 9 * cip, dtype, amax=am)
             for mode in modes:
                 am = None
                 if dtype == torch.float32:

@@ -531,7 +531,8 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     else:
         w1 = pw.w1(ops.PACK_FWD)
         Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd",
-                                    stats=training)
+                                    stats=training,
+                                    amax=(_slot(am, AM_X), pw.amax_w1(ops.PACK_FWD)))
     eps1, eps2 = bn1m.eps, bn2m.eps
     if training:
         bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1, gamma=pw.vec("g1"),
@@ -590,7 +591,7 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
     # pre-split (h2) Winograd operands: dY1's producer records max|dY1|, the
     # scale source of both its transforms (Vd, dM)
     h2 = s.V is not None and s.V.dtype == ops.H2
-    am_dy1 = _slot(s.am, AM_DY1) if h2 else None
+    am_dy1 = _slot(s.am, AM_DY1)
     # dY1 is consumed only by its two Winograd transforms: leave the BN apply
     # to the dual transform kernel, dY1 is never stored
     lazy = s.V is not None and need_dx and DUAL_TRANSFORM and LAZY_DY1 and not h2
@@ -633,7 +634,8 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
                                amax=(_slot(s.am, AM_DM), _slot(s.am, AM_V)))
         s.V = None
     else:
-        ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad")
+        ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad",
+                       amax=(am_dy1, _slot(s.am, AM_X)))
     if not need_dx:
         return None
     if s.cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
@@ -643,7 +645,8 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
                                 tag=name + ".conv.0.dgrad", v_in=Vd, amax_v=_slot(s.am, AM_VD),
                                 amax_u=s.pw.amax_U1(True))
     w1d = s.pw.w1(ops.PACK_DGRAD)
-    return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad")
+    return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad",
+                        amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)))
 
 
 def block_shapes(Rh, Rw):
@@ -695,12 +698,12 @@ class _UnetFn(torch.autograd.Function):
         assert mod.conv2.conv[0].in_channels == 4 * C, (
             f"Unet expects {mod.conv2.conv[0].in_channels // 4} input channels, got {C}")
         cdt = mod.activation_dtype()
-        X = ops.input_prep(x32, cin_p, cdt)
         masks = _masks_for(mod, B, dev, training)
         sw = _step_weights(mod, cdt, Rh, Rw, training)
         # per-step maxima of the f16x2 GEMM operands of every block (their
         # producers fill them; zeroed here, one launch)
         amax = ops.amax_slots(AM_PER_BLOCK * 10, dev) if sw else None
+        X = ops.input_prep(x32, cin_p, cdt, amax=_x_slot(amax, 2))
 
         saved, c, shapes = {}, {}, {}
         inp, h, w = X, Rh, Rw
