@@ -1225,6 +1225,35 @@ __device__ __forceinline__ void wmat2(const T (&x)[NI][NI], T (&y)[NO][NO]) {
   for (int i = 0; i < NO; ++i) wmat<C>(s[i], y[i]);
 }
 
+// wmat2's column pass fed one input row at a time: s[i][e] accumulates
+// C(i, a) x[a][e] over the rows a in increasing order with wmat's exact
+// operation sequence (first nonzero term, then +, - or fma), so streaming a
+// tile's rows gives wmat2's bits while one row, not the tile, is live (the
+// F(6x6) input transform with the x2 upsample held 220 VGPRs = 2 waves / SIMD)
+template <class C, int NI>
+__device__ constexpr int wfirst(int i) {
+  for (int j = 0; j < NI; ++j)
+    if (C::c(i, j) != 0.f) return j;
+  return NI;
+}
+template <class C, int NO, int NI, typename T>
+__device__ __forceinline__ void wcol_row(T (&s)[NO][NI], const T (&row)[NI], int a) {
+#pragma clang fp contract(off)
+#pragma unroll
+  for (int i = 0; i < NO; ++i) {
+    const float c = C::c(i, a);
+    if (c == 0.f) continue;
+    const bool first = a == wfirst<C, NI>(i);
+#pragma unroll
+    for (int e = 0; e < NI; ++e) {
+      if (first) s[i][e] = c == 1.f ? row[e] : (c == -1.f ? -row[e] : c * row[e]);
+      else if (c == 1.f) s[i][e] = s[i][e] + row[e];
+      else if (c == -1.f) s[i][e] = s[i][e] - row[e];
+      else s[i][e] = vfma(c, row[e], s[i][e]);
+    }
+  }
+}
+
 template <int MT>
 __global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int cin, int n_p, int k_p,
                                    int flip, float* __restrict__ U) {
@@ -1250,6 +1279,22 @@ __global__ void wino_weight_kernel(const float* __restrict__ w, int cout, int ci
   for (int a = 0; a < A; ++a)
 #pragma unroll
     for (int b = 0; b < A; ++b) U[(a * A + b) * plane + (size_t)n * k_p + k] = u[a][b];
+}
+
+// components i*A .. i*A+A-1 (row i of the transform) of tile t, channel(s)
+// c.. of one thread into an h2 tensor [alpha^2][T][2C]
+template <int A, typename VT>
+__device__ __forceinline__ void h2_write_row(bf16_t* __restrict__ out, long long T, int C,
+                                             long long t, int c, int i, const VT (&v)[A], float s) {
+  const size_t plane2 = (size_t)T * 2 * C;
+  bf16_t* row = out + (size_t)t * 2 * C + (size_t)(i * A) * plane2;
+#pragma unroll
+  for (int e = 0; e < A; ++e) {
+    if constexpr (std::is_same<VT, float>::value)
+      *(uint32_t*)(row + e * plane2 + h2_pair_off(c)) = h2_pair_word(v[e], s);
+    else
+      h2_store4(row + e * plane2, c, v[e], s);
+  }
 }
 
 // the alpha x alpha transform values of tile t, channel(s) c.. of one thread
@@ -1279,14 +1324,18 @@ __device__ __forceinline__ void h2_write(bf16_t* __restrict__ out, long long T, 
 // resized activation is never written to HBM.
 // H2: V is written as an h2 tensor (nsm_conv_h2.inc) Vh [alpha^2][T][2C] with
 // the scale of hsc (max|x| recorded by x's producer, beta = the transform's bound)
-template <int MT, bool RELU, bool UP, bool H2 = false>
-__global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict__ x, int ld, int H,
-                                                         int W, int C, int TH, int TW, long long T,
-                                                         float* __restrict__ V, int hi, int wi,
-                                                         float sh, float sw,
-                                                         uint32_t* __restrict__ amax,
-                                                         bf16_t* __restrict__ Vh = nullptr,
-                                                         H2Scale hsc = H2Scale{}) {
+// UNI (with UP, host-checked: C / CW a multiple of 64): a wave covers 64
+// channels of ONE tile, so the tile, its source taps and rows are
+// wave-uniform and kept in scalar registers
+// OCC: minimum waves per SIMD the register allocation must allow (the F(6x6)
+// x2-upsample form with wave-uniform tiles: 3, i.e. <= 168 VGPRs instead of
+// 218 — no spills, tools/asm_audit.py)
+template <int MT, bool RELU, bool UP, bool H2 = false, bool UNI = false, int OCC = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC, 8)))
+    wino_input_kernel(const float* __restrict__ x, int ld, int H, int W, int C, int TH, int TW,
+                      long long T, float* __restrict__ V, int hi, int wi, float sh, float sw,
+                      uint32_t* __restrict__ amax, bf16_t* __restrict__ Vh = nullptr,
+                      H2Scale hsc = H2Scale{}) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   const int C4 = C / CW;
@@ -1297,12 +1346,18 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const int c = (int)(i % C4) * CW;
-    const long long t = i / C4;
+    long long t = i / C4;
+    if constexpr (UNI) t = __builtin_amdgcn_readfirstlane((int)t);
     const int tx = (int)(t % TW);
     const long long r = t / TW;
     const int ty = (int)(r % TH);
     const long long b = r / TH;
-    VT d[A][A];
+    // patch rows stream through the column pass (wcol_row): one row live
+    VT sc[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) sc[a][e] = VT{};
     if constexpr (UP) {
       int x0[A], x1[A];
       float lx0[A], lx1[A];
@@ -1349,41 +1404,47 @@ __global__ void __launch_bounds__(256) wino_input_kernel(const float* __restrict
           }
           yb = y1;
         }
+        VT d[A];
 #pragma unroll
         for (int e = 0; e < A; ++e) {
           const int xx = MT * tx - 1 + e;
           const VT v = ly0 * h0[e] + ly1 * h1[e];
-          d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) ? v : VT{};
+          d[e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) ? v : VT{};
         }
+        wcol_row<CBt<MT>>(sc, d, a);
       }
     } else {
 #pragma unroll
       for (int a = 0; a < A; ++a) {
         const int yy = MT * ty - 1 + a;
+        VT d[A];
 #pragma unroll
         for (int e = 0; e < A; ++e) {
           const int xx = MT * tx - 1 + e;
-          d[a][e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
-                        ? *(const VT*)(x + ((size_t)(b * H + yy) * W + xx) * ld + c)
-                        : VT{};
-          if (RELU) d[a][e] = vrelu(d[a][e]);
+          d[e] = ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W)
+                     ? *(const VT*)(x + ((size_t)(b * H + yy) * W + xx) * ld + c)
+                     : VT{};
+          if (RELU) d[e] = vrelu(d[e]);
         }
+        wcol_row<CBt<MT>>(sc, d, a);
       }
     }
-    VT v[A][A];
-    wmat2<CBt<MT>>(d, v);
-    if constexpr (H2) {
-      h2_write<A>(Vh, T, C, t, c, v, hs);
-    } else {
-      const size_t plane = (size_t)T * C;
-      float* out = V + (size_t)t * C + c;
+    // row pass, one output row at a time
 #pragma unroll
-      for (int a = 0; a < A; ++a)
+    for (int a = 0; a < A; ++a) {
+      VT v[A];
+      wmat<CBt<MT>>(sc[a], v);
+      if constexpr (H2) {
+        h2_write_row<A>(Vh, T, C, t, c, a, v, hs);
+      } else {
+        const size_t plane = (size_t)T * C;
+        float* out = V + (size_t)t * C + c;
 #pragma unroll
         for (int e = 0; e < A; ++e) {
-          *(VT*)(out + (a * A + e) * plane) = v[a][e];
-          if (amax) amax_fold(am, v[a][e]);
+          *(VT*)(out + (a * A + e) * plane) = v[e];
+          if (amax) amax_fold(am, v[e]);
         }
+      }
     }
   }
   if constexpr (!H2) amax_flush(am, amax);
@@ -2561,15 +2622,19 @@ extern "C" int nsm_wino_input_h2(const float* x, int ldx, int B, int hi, int wi,
   const float sh = ac_scale(hi, H), sw = ac_scale(wi, W);
   const H2Scale sc{amax_x, wino_beta(tile, 0)};
   bf16_t* V = (bf16_t*)Vh;
-#define NSM_WI(m, u)                                                                             \
-  hipLaunchKernelGGL((wino_input_kernel<m, false, u, true>), grid, dim3(256), 0, s, x, ldx, H, W, \
-                     cin_p, g.TH, g.TW, g.T, nullptr, hi, wi, sh, sw, nullptr, V, sc)
+  const bool uni = (cin_p / (tile == 6 ? 1 : 4)) % 64 == 0;
+#define NSM_WI(m, u, un)                                                                          \
+  hipLaunchKernelGGL((wino_input_kernel<m, false, u, true, un>), grid, dim3(256), 0, s, x, ldx, H, \
+                     W, cin_p, g.TH, g.TW, g.T, nullptr, hi, wi, sh, sw, nullptr, V, sc)
   if (tile == 2) {
-    if (up) NSM_WI(2, true); else NSM_WI(2, false);
+    if (up && uni) NSM_WI(2, true, true); else if (up) NSM_WI(2, true, false); else NSM_WI(2, false, false);
   } else if (tile == 4) {
-    if (up) NSM_WI(4, true); else NSM_WI(4, false);
+    if (up && uni) NSM_WI(4, true, true); else if (up) NSM_WI(4, true, false); else NSM_WI(4, false, false);
   } else {
-    if (up) NSM_WI(6, true); else NSM_WI(6, false);
+    if (up && uni)
+      hipLaunchKernelGGL((wino_input_kernel<6, false, true, true, true, 3>), grid, dim3(256), 0, s,
+                         x, ldx, H, W, cin_p, g.TH, g.TW, g.T, nullptr, hi, wi, sh, sw, nullptr, V, sc);
+    else if (up) NSM_WI(6, true, false); else NSM_WI(6, false, false);
   }
 #undef NSM_WI
   NSM_LAUNCH_CHECK("wino_input_h2");
