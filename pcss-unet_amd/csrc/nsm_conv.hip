@@ -925,9 +925,16 @@ static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksiz
   pl.BN = cin_p >= 128 || (ksize == 3 && wgrad_multitap_f32()) ? 128
                                                                 : (cin_p >= 64 ? 64 : 32);
   long long tiles = (long long)ceil_div(M, pl.BM) * ceil_div(N, pl.BN);
-  // ~4096 blocks (8 waves of 2 blocks/CU) keeps the tail under ~6 %; each
-  // split keeps >= 8 K-slabs, and the fp32 partial slabs stay <= 512 MB.
-  long long want = (4096 + tiles - 1) / tiles;
+  // ~512 blocks (one round of 2 blocks/CU; A/B 4096 / 1024 / 512: 657 / 663 / 665
+  // frames/s); each split keeps >= 8 K-slabs,
+  // and the fp32 partial slabs stay <= 512 MB. (4096 blocks, the round-1
+  // policy, made the 1x1 weight gradients of the wide layers write and re-read
+  // more partial slabs than operands: conv6.4 128 splits x 2 MB = 268 MB.)
+  static const long long target = [] {
+    const char* e = getenv("NSM_WGRAD_BLOCKS");
+    return e ? atoll(e) : 512ll;
+  }();
+  long long want = (target + tiles - 1) / tiles;
   long long maxs = (K + 255) / 256;
   long long slab_cap = (128ll << 20) / ((long long)M * N);
   if (slab_cap < 1) slab_cap = 1;
