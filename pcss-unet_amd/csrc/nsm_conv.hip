@@ -2681,8 +2681,33 @@ static bool h2_wg256() {
 // the h2 weight-gradient plan: plan_wino_wgrad's, or 256x256 tiles (8 waves,
 // the forward's tile) where both channel counts are multiples of 256, with the
 // split count that brings the grid to ~1024 blocks (4 rounds of one block per CU)
+// splits of a batched weight-gradient GEMM over T tiles for ~target blocks
+static void wino_wgrad_resplit(WinoWgradPlan& p, long long T, int cin_p, int cout_p, int nb,
+                               long long target) {
+  const long long tiles = (long long)ceil_div(cout_p, p.BM) * ceil_div(cin_p, p.BN) * nb;
+  long long sp = (target + tiles - 1) / tiles, maxs = (T + 255) / 256;
+  if (sp > maxs) sp = maxs;
+  if (sp > 64) sp = 64;
+  if (sp < 1) sp = 1;
+  long long kc = (T + sp - 1) / sp;
+  kc = (kc + BK - 1) / BK * BK;
+  sp = (T + kc - 1) / kc;
+  p.splits = (int)sp;
+  p.kchunk = (int)kc;
+  p.slab_floats = (size_t)nb * sp * cout_p * cin_p;
+  if (sp > 1) p.slab_floats += (size_t)nb * cout_p * cin_p;
+}
+
 static WinoWgradPlan plan_wino_wgrad_h2(long long T, int cin_p, int cout_p, int nb) {
   WinoWgradPlan p = plan_wino_wgrad(T, cin_p, cout_p, nb);
+  // the 128 / 64 tiles run two blocks per CU: one round of ~512 blocks
+  // (plan_wino_wgrad's ~4096 wrote 64 x 57 partial dU slabs at conv8; A/B
+  // 4096 / 1024 / 512: 658-659 / 661-663 / 664 frames/s)
+  static const long long target = [] {
+    const char* e = getenv("NSM_H2_WG_BLOCKS");
+    return e ? atoll(e) : 512ll;
+  }();
+  wino_wgrad_resplit(p, T, cin_p, cout_p, nb, target);
   if (!h2_wg256() || cin_p % 256 || cout_p % 256) return p;
   p.BM = p.BN = 256;
   const long long tiles = (long long)(cout_p / 256) * (cin_p / 256) * nb;
