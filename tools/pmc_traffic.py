@@ -22,20 +22,26 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from stage_pmc import CODES, is_mark, load_pmc  # noqa: E402
 
 B8_CONV6 = 8 * 64 * 64
-F32_GEMM = lambda n: (n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n  # noqa: E731
-                      and any(k in n for k in ("gemm_f32_kernel", "gemm_f32s_kernel", "gemm_f32h_kernel")))
+F32_GEMM = lambda n: ((n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n  # noqa: E731
+                       and any(k in n for k in ("gemm_f32_kernel", "gemm_f32s_kernel", "gemm_f32h_kernel")))
+                      or ("gemm_h2_kernel<256, 256" in n and n.count("H2RowsDma<256, 8") >= 2))
+# blocks x threads of conv6.conv.0's forward GEMM: the register-path kernels'
+# 8x8x64 blocks of 256 threads, or the h2 kernel's 4x4x64 blocks of 512
+F32_GRIDS = (8 * 8 * 64 * 256, 4 * 4 * 64 * 512)
 KINDS = {
-    "f32_gemm": dict(match=F32_GEMM, grid=8 * 8 * 64 * 256, triple=False,
+    "f32_gemm": dict(match=F32_GEMM, grid=F32_GRIDS, triple=False,
                      alg=64 * (2 * 968 * 1024 + 1024 * 1024) * 4,
-                     desc="conv6.conv.0 fwd Winograd F(6x6) batched GEMM, B=8: gemm_f32s_kernel"
-                          "<128,128,2,2,RowsKLoader<128,256>x2,EpiStore> grid 8x8x64 (64 x M=968 "
-                          "N=1024 K=1024); algorithmic bytes = V + U read + M written, fp32"),
-    "f32": dict(match=F32_GEMM, grid=8 * 8 * 64 * 256, triple=True,
+                     desc="conv6.conv.0 fwd Winograd F(6x6) batched GEMM, B=8 (64 x M=968 N=1024 "
+                          "K=1024): gemm_h2_kernel<256,256,2,4,H2RowsDma x2,EpiH2> grid 4x4x64 (the "
+                          "pre-split f16x2 operands, NSM_H2=1) or the register-path split kernel "
+                          "grid 8x8x64; algorithmic bytes = V + U read + M written (fp32 bytes; "
+                          "an h2 operand has the same)"),
+    "f32": dict(match=F32_GEMM, grid=F32_GRIDS, triple=True,
                 alg=(2 * B8_CONV6 * 1024 + 9 * 1024 * 1024 + 1024) * 4,
                 desc="conv6.conv.0 fwd as a whole, B=8: wino_input + the GEMM above + "
                      "wino_output; algorithmic bytes = x + y + weights (direct conv)"),
     "bf16": dict(match=lambda n: "gemm_bf16_dma_kernel<256, 256" in n and "ConvActDma" in n,
-                 grid=4 * 1024 * 512, triple=False,
+                 grid=(4 * 1024 * 512,), triple=False,
                  alg=(2 * 262144 * 1024 + 9 * 1024 * 1024) * 2,
                  desc="conv6.conv.0 fwd bf16 LDS-DMA implicit GEMM, B=64: gemm_bf16_dma_kernel"
                       "<256,256,...,ConvActDma,RowsKDma,EpiStoreB> grid 4x1024 (M=262144 N=1024 "
@@ -57,7 +63,7 @@ def launches(path, k):
         seq.append((name, grid, cnt, cur))
     out, names = [], set()
     for i, (name, grid, cnt, cur) in enumerate(seq):
-        if cur != FWD or not k["match"](name) or grid != k["grid"]:
+        if cur != FWD or not k["match"](name) or grid not in k["grid"]:
             continue
         if k["triple"]:
             tot = dict(cnt)
