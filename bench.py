@@ -273,9 +273,10 @@ def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
     work = mult * ex_flops
     achieved = work / (gemm_ms * 1e-3) / 1e12
     from nsm_amd.prep import H2_WINO
-    f16 = ("gemm_h2_kernel<256,256> (fp32 via the f16x2 split: the two fp16 terms of each "
+    f16 = ("gemm_h2p_kernel<256,256> (fp32 via the f16x2 split: the two fp16 terms of each "
            "power-of-two scaled operand written by its producer, LDS-DMA, 3 products on "
-           "v_mfma_f32_32x32x16_f16)" if H2_WINO else
+           "v_mfma_f32_16x16x32_f16; persistent, one block per CU over the 4x4x64 tiles)"
+           if H2_WINO else
            "gemm_f32h_kernel (fp32 via the f16x2 split of power-of-two scaled operands, 3 "
            "products on v_mfma_f32_32x32x16_f16)")
     return {"kernel": f"conv6.conv.0.fwd Winograd F({m}x{m},3x3) batched GEMM "

@@ -2711,7 +2711,14 @@ static WinoWgradPlan plan_wino_wgrad_h2(long long T, int cin_p, int cout_p, int 
   if (!h2_wg256() || cin_p % 256 || cout_p % 256) return p;
   p.BM = p.BN = 256;
   const long long tiles = (long long)(cout_p / 256) * (cin_p / 256) * nb;
-  long long sp = (1024 + tiles - 1) / tiles, maxs = (T + 255) / 256;
+  static const long long target256 = [] {
+    const char* e = getenv("NSM_H2_WG256_BLOCKS");
+    return e ? atoll(e) : 1024ll;
+  }();
+  long long sp = (target256 + tiles - 1) / tiles, maxs = (T + 255) / 256;
+  // a full round of unsplit blocks stays unsplit (conv7: 256 tiles x K = 3872,
+  // no partial slabs, no split sum; A/B 694 -> 698 frames/s against 4 splits)
+  if (tiles >= cu_count()) sp = 1;
   if (sp > maxs) sp = maxs;
   if (sp > 64) sp = 64;
   if (sp < 1) sp = 1;
@@ -2720,7 +2727,8 @@ static WinoWgradPlan plan_wino_wgrad_h2(long long T, int cin_p, int cout_p, int 
   sp = (T + kc - 1) / kc;
   // (conv5's F(4x4) at 32x32: 144 tiles x 2 splits = 288 blocks, measured
   // 52.5 -> 63.5 us: keep the 128x128 plan under three rounds of blocks)
-  if (tiles * sp < 768) return plan_wino_wgrad(T, cin_p, cout_p, nb);
+  if (tiles * sp < 768 && !(sp == 1 && tiles >= cu_count()))
+    return plan_wino_wgrad(T, cin_p, cout_p, nb);
   p.splits = (int)sp;
   p.kchunk = (int)kc;
   p.slab_floats = (size_t)nb * sp * cout_p * cin_p;

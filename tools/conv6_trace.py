@@ -23,13 +23,15 @@ def grid_blocks(r):
 # conv6.conv.0's Winograd GEMM at B=8, 64x64, 1024 channels: F(6x6) (the
 # default there) grid 8x8x64 blocks, F(4x4) 16x8x36
 CONV6_GRIDS = ((8, 8, 64), (16, 8, 36))
-H2_GRIDS = ((4, 4, 64),)   # gemm_h2_kernel<256, 256> (NSM_H2=1, default)
+H2_GRIDS = ((4, 4, 64), (256, 1, 1))   # gemm_h2{,q}_kernel<256, 256>; persistent gemm_h2p_kernel
 KINDS = {
     "f32": (lambda r: ((any(k in r["Kernel_Name"] for k in ("gemm_f32_kernel", "gemm_f32s_kernel",
                                                           "gemm_f32h_kernel"))
                         and r["Kernel_Name"].count("RowsKLoader<128, 256>") == 2
                         and grid_blocks(r) in CONV6_GRIDS)
-                       or ("gemm_h2_kernel<256, 256" in r["Kernel_Name"]
+                       or (any(k in r["Kernel_Name"] for k in ("gemm_h2_kernel<256, 256",
+                                                               "gemm_h2q_kernel<256, 256",
+                                                               "gemm_h2p_kernel<256, 256"))
                            and r["Kernel_Name"].count("H2RowsDma<256, 8") >= 2
                            and grid_blocks(r) in H2_GRIDS)), True),
     "bf16": (lambda r: "gemm_bf16_dma_kernel<256, 256" in r["Kernel_Name"]

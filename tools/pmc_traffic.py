@@ -24,16 +24,20 @@ from stage_pmc import CODES, is_mark, load_pmc  # noqa: E402
 B8_CONV6 = 8 * 64 * 64
 F32_GEMM = lambda n: ((n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n  # noqa: E731
                        and any(k in n for k in ("gemm_f32_kernel", "gemm_f32s_kernel", "gemm_f32h_kernel")))
-                      or ("gemm_h2_kernel<256, 256" in n and n.count("H2RowsDma<256, 8") >= 2))
+                      or (any(k in n for k in ("gemm_h2_kernel<256, 256", "gemm_h2q_kernel<256, 256",
+                                               "gemm_h2p_kernel<256, 256"))
+                          and n.count("H2RowsDma<256, 8") >= 2))
 # blocks x threads of conv6.conv.0's forward GEMM: the register-path kernels'
-# 8x8x64 blocks of 256 threads, or the h2 kernel's 4x4x64 blocks of 512
-F32_GRIDS = (8 * 8 * 64 * 256, 4 * 4 * 64 * 512)
+# 8x8x64 blocks of 256 threads, the h2 kernels' 4x4x64 blocks of 512, or the
+# persistent h2 kernel's one block of 512 per CU (256 CUs)
+F32_GRIDS = (8 * 8 * 64 * 256, 4 * 4 * 64 * 512, 256 * 512)
 KINDS = {
     "f32_gemm": dict(match=F32_GEMM, grid=F32_GRIDS, triple=False,
                      alg=64 * (2 * 968 * 1024 + 1024 * 1024) * 4,
                      desc="conv6.conv.0 fwd Winograd F(6x6) batched GEMM, B=8 (64 x M=968 N=1024 "
-                          "K=1024): gemm_h2_kernel<256,256,2,4,H2RowsDma x2,EpiH2> grid 4x4x64 (the "
-                          "pre-split f16x2 operands, NSM_H2=1) or the register-path split kernel "
+                          "K=1024): gemm_h2p_kernel<256,256,2,4,H2RowsDma x2> (persistent, one block "
+                          "per CU over the 4x4x64 tiles; gemm_h2q/h2_kernel grid 4x4x64 without it) "
+                          "on the pre-split f16x2 operands (NSM_H2=1), or the register-path split kernel "
                           "grid 8x8x64; algorithmic bytes = V + U read + M written (fp32 bytes; "
                           "an h2 operand has the same)"),
     "f32": dict(match=F32_GEMM, grid=F32_GRIDS, triple=True,
