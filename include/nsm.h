@@ -65,7 +65,8 @@ int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
  * vector, a = {n, n_p}; kind 4: Winograd U as an h2 tensor [alpha^2][n_p][2 k_p]
  * (nsm_to_h2's layout), a as kind 2, amax (required) = the slot the launch first
  * fills with max|w| of the filters, the scale source of U (beta =
- * nsm_wino_beta(tile, 2)). `base` = the job's first item in the launch (jobs in
+ * nsm_wino_beta(tile, 2)); a[6] = 1: the slot is shared with an earlier kind-4
+ * job over the same filters, which fills it (this job only reads it). `base` = the job's first item in the launch (jobs in
  * ascending base order, consecutive); nsm_prep_items() = the job's extent in
  * the launch (its item count rounded up to whole 2048-item blocks: add it to
  * get the next base; total_items = the sum). jobs_dev: a device copy. */

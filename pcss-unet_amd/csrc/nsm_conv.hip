@@ -934,7 +934,10 @@ static WgradPlan plan_wgrad(int B, int H, int W, int cin_p, int cout_p, int ksiz
     const char* e = getenv("NSM_WGRAD_BLOCKS");
     return e ? atoll(e) : 512ll;
   }();
-  long long want = (target + tiles - 1) / tiles;
+  // rounded DOWN: a grid just past the resident slots runs a second round for
+  // its last few blocks (conv2.0's 3 N tiles x 171 = 513 blocks took 151.6 us)
+  long long want = target / tiles;
+  if (want < 1) want = 1;
   long long maxs = (K + 255) / 256;
   long long slab_cap = (128ll << 20) / ((long long)M * N);
   if (slab_cap < 1) slab_cap = 1;
@@ -1863,6 +1866,7 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
   if (j.kind == 4) {  // uniform per block
     const int cout = j.a[0], cin = j.a[1], n_p = j.a[2], k_p = j.a[3], flip = j.a[4];
     if (phase == 0) {
+      if (j.a[6]) return;  // its slot is filled by the un-flipped job over the same filters
       for (int r = 0; r < PREP_ITEMS / 256; ++r) {
         const long long li = blk0 - j.base + r * 256 + threadIdx.x;
         if (li >= items) break;

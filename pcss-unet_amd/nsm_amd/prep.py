@@ -156,11 +156,17 @@ class StepWeights:
             if cip >= wino_min and dtype == torch.float32:
                 tile = wino_tile(cip, h, w)
                 for flip in ((False, True) if training else (False,)):
-                    am = ops.amax_slot(self.amax, n_am)
-                    n_am += 1
+                    if h2 and training and flip:
+                        # max|w| of the same filters: the un-flipped job's slot,
+                        # filled once (a[6] = 1: phase 0 skips this job)
+                        am = pb.t[("amaxU1", False)]
+                    else:
+                        am = ops.amax_slot(self.amax, n_am)
+                        n_am += 1
                     pb.t[("amaxU1", flip)] = am
                     if h2 and training:   # pre-split U [alpha^2][cip][2 cip] float16 (nsm_conv_h2.inc)
-                        pb.t[("U1", flip)] = add(KIND_WINO_H2, (ci, ci, cip, cip, int(flip), tile),
+                        pb.t[("U1", flip)] = add(KIND_WINO_H2, (ci, ci, cip, cip, int(flip), tile,
+                                                                int(flip)),
                                                  c0.weight, (tile + 2) ** 2 * cip * 2 * cip,
                                                  ops.H2, amax=am)
                     else:
