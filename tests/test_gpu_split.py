@@ -242,3 +242,40 @@ def test_h2_prep_matches_to_h2(ops, device):
             assert torch.equal(got.view(torch.int16), ref.view(torch.int16)), (k, flip)
             # the slot the GEMMs read holds max|w|
             assert torch.equal(pb.amax_U1(flip).max(), aw.max()), (k, flip)
+
+
+@pytest.mark.parametrize("B,H,W,ci,co", [(8, 64, 64, 1024, 1024), (8, 128, 128, 512, 512),
+                                        (8, 128, 128, 512, 128)])
+def test_h2_persistent_gemm_full_shapes(ops, device, B, H, W, ci, co):
+    """The persistent h2 GEMM (gemm_h2p_kernel: one block per CU walking the
+    tiles, the K-tile stream running across tiles, buffer-store epilogue) at the
+    train step's conv6 / conv7 shapes (256x256 tiles; the last one 256x128):
+    components against float64, and the rows past T (outside the epilogue's
+    buffer descriptor) never written."""
+    from nsm_amd._lib import call, ptr, stream
+    t = 6
+    T = ops.wino_tiles(B, H, W, t)
+    nb = (t + 2) ** 2
+    g = torch.Generator(device=device).manual_seed(ci + co)
+    cs = (2.0 ** torch.linspace(-3, 3, nb, device=device)).view(nb, 1, 1)
+    V = (torch.randn(nb, T, ci, device=device, generator=g) * cs).reshape(-1).contiguous()
+    U = (torch.randn(nb, co, ci, device=device, generator=g) * 0.03).reshape(-1).contiguous()
+    amax = ops.amax_slots(2, device)
+    av, au = ops.absmax(V, ops.amax_slot(amax, 0)), ops.absmax(U, ops.amax_slot(amax, 1))
+    Vh = _h2(ops, V, nb * T, ci, av, 100.0)
+    Uh = _h2(ops, U, nb * co, ci, au, 1.0)
+    guard = 4096
+    Mb = torch.full((nb * T * co + guard,), float("nan"), device=device)
+    call("nsm_wino_gemm_h2", ptr(Vh), ptr(Uh), B, H, W, ci, co, t, ptr(Mb), ptr(av), 100.0,
+         ptr(au), 1.0, stream())
+    torch.cuda.synchronize()
+    assert torch.isnan(Mb[nb * T * co:]).all()
+    for c in (0, nb // 2, nb - 1):
+        v = V.view(nb, T, ci)[c].double()
+        u = U.view(nb, co, ci)[c].double()
+        ref = v @ u.t()
+        got = Mb[:nb * T * co].view(nb, T, co)[c].double()
+        assert torch.isfinite(got).all(), c
+        rms = ref.pow(2).mean().sqrt()
+        assert ((got - ref).pow(2).mean().sqrt() / rms).item() < 2e-6, c
+        assert ((got - ref).abs().max() / rms).item() < 3e-5, c
