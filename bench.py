@@ -81,8 +81,11 @@ STAGES = ["conv2", "conv3", "conv4", "conv5", "conv6", "conv7", "conv8", "conv9"
 
 
 def f32_split_mode():
-    """NSM_F32_SPLIT as libnsm reads it: 2 (default) f16x2 for the Winograd
-    GEMMs + bf16x3 for the direct ones, 1 bf16x3 everywhere, 0 fp32 MFMA."""
+    """NSM_F32_SPLIT as libnsm reads it: 2 (default) the f16x2 split (3 f16
+    products) for every GEMM of the train step (all operand maxima are recorded
+    by their producers; only a fused BN-prologue operand, NSM_F32_ACT=0, falls
+    back to the bf16 three-way split), 1 bf16 split (6 bf16 products)
+    everywhere, 0 fp32 MFMA."""
     v = int(os.environ.get("NSM_F32_SPLIT", "2"))
     return min(max(v, 0), 2)
 
@@ -95,7 +98,7 @@ def pipe_products(bf16):
     m = f32_split_mode()
     if m == 0:
         return (1, 1), FP32_PEAK_TFLOPS
-    return ((3, 6) if m == 2 else (6, 6)), BF16_PEAK_TFLOPS
+    return ((3, 3) if m == 2 else (6, 6)), BF16_PEAK_TFLOPS
 
 
 def stage_work(in_ch, H, W, B, bytes_per=4, wino_min=128, tile=4, passes=3):

@@ -66,10 +66,16 @@ int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
  * (nsm_to_h2's layout), a as kind 2, amax (required) = the slot the launch first
  * fills with max|w| of the filters, the scale source of U (beta =
  * nsm_wino_beta(tile, 2)); a[6] = 1: the slot is shared with an earlier kind-4
- * job over the same filters, which fills it (this job only reads it). `base` = the job's first item in the launch (jobs in
+ * job over the same filters, which fills it (this job only reads it); kind 5:
+ * pack as an h2 tensor (a as kind 0; FWD [cout_p][2 taps cin_p], DGRAD
+ * [cin_p][2 taps cout_p] float16), amax (required) = the slot the launch first
+ * fills with max|w| (beta 1), a[6] = 1: shared with the FWD job of the same
+ * weight. `base` = the job's first item in the launch (jobs in
  * ascending base order, consecutive); nsm_prep_items() = the job's extent in
  * the launch (its item count rounded up to whole 2048-item blocks: add it to
- * get the next base; total_items = the sum). jobs_dev: a device copy. */
+ * get the next base; total_items = the sum). jobs_dev: a device copy.
+ * max_pass: the table holds kind-4 / kind-5 jobs (their max|w| pass runs
+ * first; 0 skips that launch). */
 typedef struct {
   int kind;
   int a[7];
@@ -78,10 +84,11 @@ typedef struct {
   void* dst;
   uint32_t* amax; /* kinds 0, 2 (may be NULL): atomic max of |written| as fp32
                      bits (zeroed beforehand): the f16x2 GEMM operand scale;
-                     kind 4: max|w| (see above) */
+                     kinds 4, 5: max|w| (see above) */
 } NsmPrepJob;
 long long nsm_prep_items(const NsmPrepJob* job);
-int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items, void* stream);
+int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items, int max_pass,
+                     void* stream);
 
 /* ---- convolution as MFMA implicit GEMM (fp32 in, fp32 accumulate) ----------
  * nsm_conv_fwd: y[p][co] = bias[co] + sum_{tap,ci} pro(x[p+off(tap)][ci]) * W
@@ -189,6 +196,33 @@ int nsm_conv3x3_wgrad_wino_h2(const void* dMh, const void* Vh, int B, int H, int
 int nsm_wino_gemm_h2(const void* V, const void* U, int B, int H, int W, int cin_p, int cout_p,
                      int tile, float* Mb, const uint32_t* amax_v, float beta_v,
                      const uint32_t* amax_u, float beta_u, void* stream);
+/* ---- the DoubleConv's 1x1 convolution on h2 operands (csrc/nsm_conv_h2d.inc)
+ * Replaces nn.Conv2d(in, out, 1) (Unetmodel.py:26), its input gradient with
+ * the first BN's backward fused (as nsm_conv1x1_dgrad_bnbwd) and its weight
+ * gradient, for the fp32 train step: xh / dy2h / dyh are h2 tensors (the
+ * activated operand from nsm_bn_act_h2, the output-BN gradient from
+ * nsm_to_h2), wh / w2dh the FWD / DGRAD h2 packs of prep kind 5, each with its
+ * scale source slot (beta 1). nsm_conv1x1_h2: y [M][ldy] fp32 = x W^T + bias,
+ * stats (may be NULL) = BN partials [ceil(M/R)][2][cout_p] with R =
+ * nsm_conv1x1_h2_rows(M, cout_p, 2 cin_p, 0). nsm_conv1x1_dgrad_bnbwd_h2: modes
+ * and outputs as nsm_conv1x1_dgrad_bnbwd, partial rows of R =
+ * nsm_conv1x1_h2_rows(M, cip, 2 cop, 1) pixels, HW = pixels per image (mask row).
+ * nsm_conv1x1_wgrad_h2: dw [cout][cin] (reference layout) with ws >=
+ * nsm_conv1x1_wgrad_h2_ws floats. M = pixels. */
+int nsm_conv1x1_h2_rows(int M, int N, int K, int bnbwd);
+int nsm_conv1x1_h2(const void* xh, int M, int cin_p, const void* wh, const float* bias, int cout_p,
+                   float* y, int ldy, float* stats, const uint32_t* amax_x,
+                   const uint32_t* amax_w, void* stream);
+int nsm_conv1x1_dgrad_bnbwd_h2(const void* dy2h, int M, int cop, const void* w2dh, int cip,
+                               const float* y1, int ldy1, const float* scale, const float* shift,
+                               const float* mean, const float* invstd, const float* mask, int HW,
+                               float slope, int mode, float* partial, const float* coef,
+                               float* out, int ldo, const uint32_t* amax_dy2,
+                               const uint32_t* amax_w, uint32_t* amax_out, void* stream);
+size_t nsm_conv1x1_wgrad_h2_ws(int M, int cin_p, int cout_p);
+int nsm_conv1x1_wgrad_h2(const void* dyh, const void* xh, int M, int cin_p, int cout_p, int cin,
+                         int cout, float* dw, float* ws, size_t ws_floats, const uint32_t* amax_dy,
+                         const uint32_t* amax_x, void* stream);
 /* fp32 GEMM arithmetic of every fp32 convolution (the batched GEMMs of
  * nsm_wino_gemm / nsm_conv3x3_wino, the weight gradient of
  * nsm_conv3x3_wgrad_wino, the direct implicit GEMMs): 2 (default, env
@@ -270,7 +304,12 @@ int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_per_chunk, 
                           int c_real,
                           const float* gamma, const float* beta, float* run_mean, float* run_var,
                           int64_t* num_batches, float momentum, float eps, int n_updates,
-                          float* mean, float* invstd, float* scale, float* shift, void* stream);
+                          float* mean, float* invstd, float* scale, float* shift, uint32_t* bound,
+                          float bound_mul, void* stream);
+/* bound (may be NULL): operand-maximum slot receiving, as the atomic max of its
+ * channels, bound_mul * (|scale| sqrt(var (M - 1)) + |beta|) >= max|lrelu(BN(y))|
+ * * bound_mul over the batch (train-mode BN of M values; bound_mul = the
+ * Dropout2d mask's maximum): the scale source of nsm_bn_act_h2 */
 /* merge groups of `group` consecutive partial chunks ({sum, M2} rows of
  * rows_per_chunk rows) into ceil(nchunk/group) rows of rows_per_chunk*group
  * rows (Chan, fixed order): keeps nsm_bn_finalize_train short on huge grids */
@@ -285,17 +324,28 @@ int nsm_bn_finalize_eval(const float* run_mean, const float* run_var, const floa
 int nsm_bn_act(const void* y, int ldy, int M, int C, const float* scale, const float* shift,
                float slope, const float* mask, int HW, const void* res, int ldres, void* out,
                int ldo, int dtype, uint32_t* amax, void* stream);
+/* nsm_bn_act (fp32, no skip) writing an h2 tensor out [M][2C] (float16; see
+ * the pre-split operands above) with scale source `bound` (beta 1): the
+ * activated 1x1 operand A1 of the fp32 train step (Unetmodel.py:22-24) */
+int nsm_bn_act_h2(const float* y, int ldy, int M, int C, const float* scale, const float* shift,
+                  float slope, const float* mask, int HW, void* out, const uint32_t* bound,
+                  void* stream);
 /* backward of  z = lrelu(mask * ... ) chains around a train-mode BN:
  *   dz = g * mask[b][c] * lrelu'(y*scale+shift); partial {sum dz, sum dz*xhat}. */
 int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy, int M, int C, int HW,
                       const float* scale, const float* shift, float slope, const float* mask,
                       const float* mean, const float* invstd, float* partial, int nchunk,
-                      int dtype, void* stream);
+                      int dtype, uint32_t* amax_k1dz, void* stream);
 /* dgamma, dbeta (real channels), bias grad of the producing conv
- * (analytically 0 in train mode), coef[3][C] for nsm_bn_bwd_apply. */
+ * (analytically 0 in train mode), coef[3][C] for nsm_bn_bwd_apply.
+ * amax_k1dz (the reductions' optional slot: max|scale * dz| over the tensor)
+ * and bound (may be NULL): the slot receiving max_c (max|k1 dz| + |k2|
+ * sqrt(M - 1) / invstd + |k3|) >= max|dy| (Samuelson), the scale source of
+ * nsm_bn_bwd_apply_h2. */
 int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int C, int c_real,
                         const float* gamma, const float* invstd, float* dgamma, float* dbeta,
-                        float* dbias_prev, float* coef, void* stream);
+                        float* dbias_prev, float* coef, const uint32_t* amax_k1dz,
+                        uint32_t* bound, void* stream);
 /* plain-sum merge: out[g][j] = sum of rows [g*group, (g+1)*group) of part[nrows][width]
  * (fixed order): the BN-backward partials of nsm_conv1x1_dgrad_bnbwd before
  * nsm_bn_bwd_finalize */
@@ -305,6 +355,14 @@ int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, int M, int 
                      const float* scale, const float* shift, float slope, const float* mask,
                      const float* mean, const float* coef, void* dy, int lddy, int dtype,
                      uint32_t* amax, void* stream);
+/* nsm_bn_bwd_apply (fp32) writing dy as an h2 tensor [M][2C] float16 with the
+ * scale source bound (nsm_bn_bwd_finalize's): the 1x1 conv's output gradient
+ * for its h2 weight / input gradients (nsm_conv1x1_wgrad_h2,
+ * nsm_conv1x1_dgrad_bnbwd_h2) */
+int nsm_bn_bwd_apply_h2(const float* g, int ldg, const float* y, int ldy, int M, int C, int HW,
+                        const float* scale, const float* shift, float slope, const float* mask,
+                        const float* mean, const float* coef, void* dy, const uint32_t* bound,
+                        void* stream);
 /* amax (bn_act, bn_bwd_apply; fp32 only, may be NULL): the operand-maximum
  * slot receiving max|out| / max|dy| for the f16x2 GEMM that consumes it. */
 
@@ -355,15 +413,16 @@ int nsm_bnred_chunks(int kind, int B, int H, int W, int C);
 int nsm_avgpool2_bwd_add_bnred(const void* dy, int B, int H, int W, int C, const void* skip,
                                void* dx, int dtype, const void* y2, const float* scale,
                                const float* shift, const float* mean, const float* invstd,
-                               float slope, float* partial, void* stream);
+                               float slope, float* partial, uint32_t* amax_k1dz, void* stream);
 int nsm_resize_bwd_bnred(const void* dy, int B, int Hi, int Wi, int C, void* dx, int Ho, int Wo,
                          int dtype, const void* y2, const float* scale, const float* shift,
                          const float* mean, const float* invstd, float slope, float* partial,
-                         void* stream);
+                         uint32_t* amax_k1dz, void* stream);
 int nsm_up2_resize_bwd_bnred(const void* dy, int B, int h, int w, int C, void* dx, int th, int tw,
                              int dtype, const void* y2, const float* scale, const float* shift,
                              const float* mean, const float* invstd, float slope, float* partial,
-                             void* stream);
+                             uint32_t* amax_k1dz, void* stream);
+/* amax_k1dz (may be NULL): slot receiving max|scale * dz| (nsm_bn_bwd_finalize's bound) */
 
 /* ---- model boundary ---------------------------------------------------------
  * pixel_unshuffle(2) + NCHW->NHWC + channel pad (Unetmodel.py:65-67,101) */

@@ -181,6 +181,73 @@ __device__ __forceinline__ uint32_t amax_read(const uint32_t* p) {
   return m;
 }
 
+// ---- the f16x2 split of power-of-two scaled fp32 operands (h2 tensors) ------
+// (nsm_conv_split16.inc, nsm_conv_h2.inc): shared by the GEMM TU and the
+// elementwise TU, whose producers write h2 operands
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// s = 2^(15 - ceil(log2 m)) from the bits of m = max|X| (0, Inf, NaN -> 1).
+// Clamped to [-126, 126] so that s and the epilogue's undo factor 2^-se are
+// both normal floats (exp2i(-127) would be the bit pattern 0): an operand
+// whose maximum is below 2^-111 is scaled by 2^126 only, i.e. represented with
+// fewer significand bits, but never flushed to an all-zero GEMM.
+__device__ __forceinline__ int pow2_scale_exp(uint32_t u) {
+  if (u == 0u || u >= 0x7f800000u) return 0;
+  int e = (int)(u >> 23) - 127;  // floor(log2 m) (subnormal m: -127)
+  if (u & 0x7fffffu) e += 1;     // ceil
+  int se = 15 - e;
+  return se < -126 ? -126 : (se > 126 ? 126 : se);
+}
+__device__ __forceinline__ float exp2i(int e) { return __int_as_float((e + 127) << 23); }
+
+__device__ __forceinline__ uint32_t pack_h2(f32x2 v) {
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
+}
+__device__ __forceinline__ f32x2 unpack_h2(uint32_t w) {
+  return __builtin_convertvector(__builtin_bit_cast(f16x2, w), f32x2);
+}
+
+__device__ __forceinline__ void split4h(f32x4 v, float s, u32x2& h, u32x2& l) {
+  const f32x2 a = f32x2{v.x, v.y} * s, b = f32x2{v.z, v.w} * s;
+  h = u32x2{pack_h2(a), pack_h2(b)};
+  l = u32x2{pack_h2(a - unpack_h2(h.x)), pack_h2(b - unpack_h2(h.y))};
+}
+
+// ---- pre-split (h2) operands: scale source and writers (nsm_conv_h2.inc) ----
+struct H2Scale {
+  const uint32_t* amax;  // max|source| slot (NSM_AMAX_WORDS)
+  float beta;            // max|operand| <= beta * max|source|
+};
+// beta * max can overflow fp32 for a finite max (beta is 3969 for the F(6x6)
+// output-gradient transform): that saturates at FLT_MAX (s = 2^-113, every
+// finite operand value fits f16) instead of reading as Inf (s = 1, values
+// above 65504 would turn Inf). A non-finite max keeps s = 1 (NaN propagates).
+__device__ __forceinline__ int h2_exp(const H2Scale& s) {
+  const uint32_t m = amax_read(s.amax);
+  uint32_t b = __float_as_uint(__uint_as_float(m) * s.beta);
+  if (m < 0x7f800000u && b >= 0x7f800000u) b = 0x7f7fffffu;
+  return pow2_scale_exp(b);
+}
+
+// 4 consecutive channels c..c+3 (c % 4 == 0) of one lane: h and l as 8-B words
+__device__ __forceinline__ void h2_store4(bf16_t* row, int c, f32x4 v, float s) {
+  u32x2 h, l;
+  split4h(v, s, h, l);
+  const int o = 16 * (c >> 3) + (c & 7);
+  *(u32x2*)(row + o) = h;
+  *(u32x2*)(row + o + 8) = l;
+}
+// 8 consecutive channels c..c+7 (c % 8 == 0) of one lane: h and l as one
+// 16-B word each (row = the h2 row of the pixel)
+__device__ __forceinline__ void h2_store8(bf16_t* row, int c, F8 v, float s) {
+  u32x2 ha, la, hb, lb;
+  split4h(v.a, s, ha, la);
+  split4h(v.b, s, hb, lb);
+  *(u32x4*)(row + 2 * c) = u32x4{ha.x, ha.y, hb.x, hb.y};
+  *(u32x4*)(row + 2 * c + 8) = u32x4{la.x, la.y, lb.x, lb.y};
+}
+
 inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace nsm

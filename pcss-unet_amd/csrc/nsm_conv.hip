@@ -517,6 +517,13 @@ __device__ __forceinline__ f32x4 shfl_xor_v4(f32x4 v, int o) {
 // the epilogue adds no register pressure to the GEMM loop.
 struct EpiBnBwd {
   using P = BnBwdEpiP;
+  // LDS of the h2 GEMMs' epilogue (gemm_h2_kernel): the staged wave tiles, then
+  // the [WM][2][BNT] partial rows
+  template <int TM, int TN, int WM, int WN>
+  static constexpr int lds_bytes() {
+    constexpr int a = WM * WN * TM * 32 * (TN * 32 + 4) * 4, b = WM * 2 * WN * TN * 32 * 4;
+    return a > b ? a : b;
+  }
   template <int TM, int TN, int WM, int WN>
   __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
                                int) {
@@ -1786,7 +1793,8 @@ __global__ void __launch_bounds__(256) wino_wgrad_out_kernel(const float* __rest
 __host__ __device__ inline long long nsm_prep_items_dev(const NsmPrepJob& j) {
   switch (j.kind) {
     case 0:
-    case 1: return (long long)j.a[3] * j.a[4] * j.a[2];
+    case 1:
+    case 5: return (long long)j.a[3] * j.a[4] * j.a[2];
     case 2:
     case 4: return (long long)j.a[2] * j.a[3];
     case 3: return j.a[1];
@@ -1850,8 +1858,9 @@ constexpr int PREP_ITEMS = 2048;  // items per block: 8 per thread
 // (job.base / PREP_ITEMS: every job starts on a block boundary, see
 // nsm_prep_items), then the block's items of that job, coalesced
 // phase 0: the h2 Winograd jobs (kind 4) record max|w| of their filters into
-// j.amax (the scale source of the U they write in phase 1, beta = wino_beta G);
-// every other job waits for phase 1
+// j.amax (the scale source of the U they write in phase 1, beta = wino_beta G),
+// the h2 packs (kind 5) max|w| of theirs (beta 1); every other job waits for
+// phase 1
 __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __restrict__ jobs,
                                                            int njobs, int phase) {
   const long long blk0 = (long long)blockIdx.x * PREP_ITEMS;
@@ -1863,6 +1872,39 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
   const NsmPrepJob& j = jobs[lo];
   const long long items = nsm_prep_items_dev(j);
   uint32_t am = 0;  // max|written| (the f16x2 GEMMs' operand scale, j.amax)
+  if (j.kind == 5) {  // h2 pack (uniform per block): max|w| (phase 0), then h + l (phase 1)
+    const int cout = j.a[0], cin = j.a[1], taps = j.a[2], cout_p = j.a[3], cin_p = j.a[4];
+    const bool fwd = j.a[5] == NSM_PACK_FWD;
+    if (phase == 0 && j.a[6]) return;  // the FWD job over the same weight fills the slot
+    const float s = phase ? exp2i(h2_exp(H2Scale{j.amax, 1.f})) : 0.f;
+    const int K = taps * (fwd ? cin_p : cout_p);  // row length (fp32 elements)
+    bf16_t* out = (bf16_t*)j.dst;
+    for (int r = 0; r < PREP_ITEMS / 256; ++r) {
+      const long long li = blk0 - j.base + r * 256 + threadIdx.x;
+      if (li >= items) break;
+      const int idx = (int)li;
+      float v;
+      if (fwd) {
+        const int ci = idx % cin_p, t = idx / cin_p, tap = t % taps, co = t / taps;
+        v = (co < cout && ci < cin) ? j.src[((size_t)co * cin + ci) * taps + tap] : 0.f;
+      } else {
+        const int co = idx % cout_p, t = idx / cout_p, tap = t % taps, ci = t / taps;
+        v = (co < cout && ci < cin) ? j.src[((size_t)co * cin + ci) * taps + (taps - 1 - tap)] : 0.f;
+      }
+      if (phase == 0) {
+        amax_fold(am, v);
+      } else {
+        const int row = idx / K, k = idx - row * K;
+        const float a = v * s;
+        const _Float16 h = (_Float16)a;
+        bf16_t* o = out + (size_t)row * 2 * K + 16 * (k >> 3) + (k & 7);
+        o[0] = __builtin_bit_cast(unsigned short, h);
+        o[8] = __builtin_bit_cast(unsigned short, (_Float16)(a - (float)h));
+      }
+    }
+    if (phase == 0) amax_flush(am, j.amax);
+    return;
+  }
   if (j.kind == 4) {  // uniform per block
     const int cout = j.a[0], cin = j.a[1], n_p = j.a[2], k_p = j.a[3], flip = j.a[4];
     if (phase == 0) {
@@ -1989,11 +2031,13 @@ extern "C" long long nsm_prep_items(const NsmPrepJob* j) {
 }
 
 extern "C" int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items,
-                                void* stream) {
+                                int max_pass, void* stream) {
   NSM_CHECK_ARG(jobs_dev && njobs > 0 && total_items > 0 && total_items % PREP_ITEMS == 0,
                 "prep_weights: bad args");
   NSM_CHECK_ARG(total_items / PREP_ITEMS < (1ll << 31), "prep_weights: too many items");
-  for (int phase = 0; phase < 2; ++phase)
+  // phase 0 (the max|w| pass of the h2 jobs, kinds 4 and 5) only where the
+  // table holds such jobs (max_pass): otherwise every block of it would return
+  for (int phase = max_pass ? 0 : 1; phase < 2; ++phase)
     hipLaunchKernelGGL(prep_weights_kernel, dim3((unsigned)(total_items / PREP_ITEMS)), dim3(256), 0,
                        as_stream(stream), jobs_dev, njobs, phase);
   NSM_LAUNCH_CHECK("prep_weights");
@@ -2613,6 +2657,7 @@ static int wgrad_wino_finish(float* slab, const WinoWgradPlan& pl, int nb, int M
 namespace nsm {
 #include "nsm_conv_bf16.inc"
 #include "nsm_conv_h2.inc"
+#include "nsm_conv_h2d.inc"
 
 extern "C" float nsm_wino_beta(int tile, int which) {
   return (tile == 2 || tile == 4 || tile == 6) && which >= 0 && which <= 2 ? wino_beta(tile, which)

@@ -114,7 +114,7 @@ __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
     const float* __restrict__ partial, int nchunk, int rpc, int M, int C, int c_real,
     const float* __restrict__ gamma, const float* __restrict__ beta, float* run_mean,
     float* run_var, int64_t* num_batches, float momentum, float eps, int n_updates, float* mean_o,
-    float* invstd_o, float* scale_o, float* shift_o) {
+    float* invstd_o, float* scale_o, float* shift_o, uint32_t* bound, float bound_mul) {
   __shared__ double red[4];
   const int tid = threadIdx.x;
   const int c = blockIdx.x;
@@ -159,6 +159,17 @@ __global__ void __launch_bounds__(256) bn_finalize_train_kernel(
   invstd_o[c] = inv;
   scale_o[c] = sc;
   shift_o[c] = beta[c] - mf * sc;
+  if (bound) {
+    // max over the batch of |lrelu(y*scale+shift)| * mask_max, the scale source
+    // of the h2 activated operand (nsm_bn_act_h2) known before it is written:
+    // y*scale + shift = scale (y - mean) + beta and, for n values with biased
+    // variance var, max|y - mean| <= sqrt(var (n - 1)) (Samuelson), so
+    // |BN(y)| <= |scale| sqrt(var (n - 1)) + |beta|; LeakyReLU does not grow
+    // it. In double, 1e-6 up (the fp32 apply rounds within the s headroom).
+    const double b = ((double)fabsf(sc) * sqrt((double)var_b * (double)(M - 1)) +
+                      (double)fabsf(beta[c])) * (double)bound_mul * (1.0 + 1e-6);
+    atomicMax(bound + (c & (AMAX_LINES - 1)) * AMAX_STRIDE, __float_as_uint((float)b) & 0x7fffffffu);
+  }
   if (c < c_real && run_mean) {
     float rm = run_mean[c], rv = run_var[c];
     for (int u = 0; u < n_updates; ++u) {
@@ -275,6 +286,28 @@ __global__ void __launch_bounds__(256) bn_act_kernel(const T* __restrict__ y, in
   amax_flush(am, amax);
 }
 
+// bn_act's activated operand written as an h2 tensor out [M][2C] (fp32 in):
+// the 1x1 conv's A1 (nsm_conv_h2d.inc), scale from the bound slot its BN
+// finalize filled (nsm_bn_finalize_train `bound`)
+__global__ void __launch_bounds__(256) bn_act_h2_kernel(const float* __restrict__ y, int ldy, int M,
+                                                        int C8, FastDiv fdHW,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift,
+                                                        float slope,
+                                                        const float* __restrict__ mask,
+                                                        bf16_t* __restrict__ out, H2Scale hs) {
+  const float s = exp2i(h2_exp(hs));  // every lane: amax_read is a wave reduction
+  const int ppb = blockDim.x / C8, tp = threadIdx.x / C8;
+  const int c = (threadIdx.x - tp * C8) * 8;
+  const F8 sc = ldf8(scale + c), sh = ldf8(shift + c);
+  const int pstep = gridDim.x * ppb;
+  for (int p = blockIdx.x * ppb + tp; p < M; p += pstep) {
+    F8 o = lrelu8(ld8(y + (size_t)p * ldy + c) * sc + sh, slope);
+    if (mask) o = o * ld8(mask + (size_t)fdiv((uint32_t)p, fdHW) * (C8 * 8) + c);
+    h2_store8(out + (size_t)p * 16 * C8, c, o, s);
+  }
+}
+
 // dz = g * mask[b][c] * lrelu'(y*scale+shift)
 __device__ __forceinline__ f32x4 lrelu_grad4(f32x4 z, float slope) {
   return f32x4{lrelu_grad(z.x, slope), lrelu_grad(z.y, slope), lrelu_grad(z.z, slope),
@@ -295,7 +328,8 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const T* __restrict__ g, int ldg, const T* __restrict__ y, int ldy, int M, int C,
     FastDiv fdHW, const float* __restrict__ scale, const float* __restrict__ shift, float slope,
     const float* __restrict__ mask, const float* __restrict__ mean,
-    const float* __restrict__ invstd, int cl, int rl, int rpc, float* __restrict__ partial) {
+    const float* __restrict__ invstd, int cl, int rl, int rpc, float* __restrict__ partial,
+    uint32_t* __restrict__ amax) {
   __shared__ F8 red[256];
   const int tid = threadIdx.x, tc = tid % cl, tr = tid / cl;
   const int c = (blockIdx.x * cl + tc) * 8;
@@ -303,6 +337,7 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
   const F8 sc = ldf8(scale + c), sh = ldf8(shift + c);
   const F8 mu = ldf8(mean + c), is = ldf8(invstd + c);
   F8 s1 = f8zero(), s2 = f8zero();
+  uint32_t am = 0;  // max|scale * dz| (scale = gamma * invstd = k1 of the finalize)
 #pragma unroll 2
   for (int r = r0 + tr; r < r1; r += rl) {
     const F8 v = ld8(y + (size_t)r * ldy + c);
@@ -311,7 +346,12 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
     const F8 dz = bn_dz8(gg, v, sc, sh, slope, mask, b, C, c);
     s1 += dz;
     s2 += dz * ((v - mu) * is);
+    if (amax) {
+      amax_fold(am, sc.a * dz.a);
+      amax_fold(am, sc.b * dz.b);
+    }
   }
+  amax_flush(am, amax);
   red[tid] = s1;
   col_tree_reduce(red, cl, rl, tid);
   const F8 t1 = red[tc];
@@ -328,10 +368,14 @@ __global__ void __launch_bounds__(256) bn_bwd_reduce_kernel(
 __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
     const float* __restrict__ partial, int nchunk, int M, int C, int c_real,
     const float* __restrict__ gamma, const float* __restrict__ invstd, float* dgamma,
-    float* dbeta, float* dbias_prev, float* coef) {
+    float* dbeta, float* dbias_prev, float* coef, const uint32_t* __restrict__ amax_k1dz,
+    uint32_t* __restrict__ bound) {
   __shared__ double red[4];
   const int tid = threadIdx.x;
   const int c = blockIdx.x;  // one block per channel (see bn_finalize_train_kernel)
+  // max over the tensor of |k1 dz| (recorded by the reduction's producer): every
+  // lane of the block's waves (amax_read is a wave reduction)
+  const float a_k1dz = bound ? __uint_as_float(amax_read(amax_k1dz)) : 0.f;
   const size_t st = (size_t)2 * C;
   double a0 = 0.0, a1 = 0.0, b0 = 0.0, b1 = 0.0;
   int k = tid;
@@ -355,6 +399,14 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(
   coef[c] = k1;
   coef[C + c] = k2;
   coef[2 * C + c] = k3;
+  if (bound) {
+    // dy = k1 dz + k2 (y - mean) + k3 with max|y - mean| <= sqrt(var (M - 1))
+    // <= sqrt(M - 1) / invstd (Samuelson, biased var): a bound of max|dy| known
+    // before nsm_bn_bwd_apply_h2 writes dy, the scale source of that h2 tensor
+    const double b = ((double)a_k1dz + fabs((double)k2) * sqrt((double)(M - 1)) / (double)is +
+                      fabs((double)k3)) * (1.0 + 1e-6);
+    atomicMax(bound + (c & (AMAX_LINES - 1)) * AMAX_STRIDE, __float_as_uint((float)b) & 0x7fffffffu);
+  }
   if (c < c_real) {
     if (dgamma) dgamma[c] = (float)S2;
     if (dbeta) dbeta[c] = (float)S1;
@@ -390,6 +442,29 @@ __global__ void __launch_bounds__(256) bn_bwd_apply_kernel(
   amax_flush(am, amax);
 }
 
+// nsm_bn_bwd_apply (fp32) writing dy as an h2 tensor [M][2C] with the scale
+// source `bound` (nsm_bn_bwd_finalize's): the 1x1 conv's output gradient dY2
+// read by its h2 weight and input gradients (nsm_conv_h2d.inc)
+__global__ void __launch_bounds__(256) bn_bwd_apply_h2_kernel(
+    const float* __restrict__ g, int ldg, const float* __restrict__ y, int ldy, int M, int C,
+    int C8, FastDiv fdHW, const float* __restrict__ scale, const float* __restrict__ shift,
+    float slope, const float* __restrict__ mask, const float* __restrict__ mean,
+    const float* __restrict__ coef, bf16_t* __restrict__ dy, H2Scale hs) {
+  const float s = exp2i(h2_exp(hs));  // every lane: amax_read is a wave reduction
+  const int ppb = blockDim.x / C8, tp = threadIdx.x / C8;
+  const int c = (threadIdx.x - tp * C8) * 8;
+  const F8 sc = ldf8(scale + c), sh = ldf8(shift + c), mu = ldf8(mean + c);
+  const F8 k1 = ldf8(coef + c), k2 = ldf8(coef + C + c), k3 = ldf8(coef + 2 * C + c);
+  const int pstep = gridDim.x * ppb;
+  for (int p = blockIdx.x * ppb + tp; p < M; p += pstep) {
+    const F8 v = ld8(y + (size_t)p * ldy + c);
+    const F8 gg = ld8(g + (size_t)p * ldg + c);
+    const int b = mask ? (int)fdiv((uint32_t)p, fdHW) : 0;
+    const F8 dz = bn_dz8(gg, v, sc, sh, slope, mask, b, C, c);
+    h2_store8(dy + (size_t)p * 2 * C, c, k1 * dz + k2 * (v - mu) + k3, s);
+  }
+}
+
 // BN-backward reduction fused into the kernel that PRODUCES a block output's
 // gradient g (the pooling / resize backward): with y = that block's BN input
 // Y2, {sum dz, sum dz*xhat} per channel of dz = g * lrelu'(y*scale+shift)
@@ -405,6 +480,7 @@ struct BnRedP {
   const float* invstd;
   float slope;
   float* partial;
+  uint32_t* amax;  // max|scale * dz| (may be NULL): the k1 term of the dy bound (finalize)
 };
 template <typename T>
 __device__ __forceinline__ F8 as_stored8(F8 v);
@@ -419,6 +495,7 @@ __device__ __forceinline__ F8 as_stored8<bf16_t>(F8 v) {
 }
 struct BnRedAcc {
   F8 sc, sh, mu, is, s1, s2;
+  uint32_t am;
   __device__ void init(const BnRedP& r, int c) {
     sc = ldf8(r.scale + c);
     sh = ldf8(r.shift + c);
@@ -426,6 +503,7 @@ struct BnRedAcc {
     is = ldf8(r.invstd + c);
     s1 = f8zero();
     s2 = f8zero();
+    am = 0;
   }
   // g: the value as written (T-rounded); p: its pixel row in y
   template <typename T>
@@ -434,6 +512,10 @@ struct BnRedAcc {
     const F8 dz = bn_dz8(g, v, sc, sh, r.slope, nullptr, 0, C, c);
     s1 += dz;
     s2 += dz * ((v - mu) * is);
+    if (r.amax) {
+      amax_fold(am, sc.a * dz.a);
+      amax_fold(am, sc.b * dz.b);
+    }
   }
   // whole block (256 threads, group = tid % C8) -> partial row blockIdx.x
   __device__ void write(const BnRedP& r, int C8) {
@@ -450,6 +532,7 @@ struct BnRedAcc {
       st8(pr + tc * 8, t1);
       st8(pr + C + tc * 8, red[tc]);
     }
+    amax_flush(am, r.amax);
   }
   // a block covering channels [c0, c0 + 8 G) of a C-channel tensor (group =
   // tid % G): its slice of partial row `row`
@@ -467,6 +550,7 @@ struct BnRedAcc {
       st8(pr + tc * 8, t1);
       st8(pr + C + tc * 8, red[tc]);
     }
+    amax_flush(am, r.amax);
   }
 };
 
@@ -1828,7 +1912,8 @@ extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_
                                      int C, int c_real, const float* gamma, const float* beta,
                                      float* run_mean, float* run_var, int64_t* num_batches,
                                      float momentum, float eps, int n_updates, float* mean,
-                                     float* invstd, float* scale, float* shift, void* stream) {
+                                     float* invstd, float* scale, float* shift, uint32_t* bound,
+                                     float bound_mul, void* stream) {
   NSM_CHECK_ARG(partial && gamma && beta && mean && invstd && scale && shift, "bn_finalize: null");
   NSM_CHECK_ARG(M > 1, "bn_finalize: Expected more than 1 value per channel when training");
   NSM_CHECK_ARG(nchunk >= 1 && (rows_per_chunk == 0 ||
@@ -1837,7 +1922,8 @@ extern "C" int nsm_bn_finalize_train(const float* partial, int nchunk, int rows_
   hipLaunchKernelGGL(bn_finalize_train_kernel, dim3(C), dim3(256), 0,
                      as_stream(stream), partial, nchunk, rows_per_chunk, M, C, c_real, gamma, beta,
                      run_mean,
-                     run_var, num_batches, momentum, eps, n_updates, mean, invstd, scale, shift);
+                     run_var, num_batches, momentum, eps, n_updates, mean, invstd, scale, shift,
+                     bound, bound_mul);
   NSM_LAUNCH_CHECK("bn_finalize_train");
   return 0;
 }
@@ -1910,10 +1996,28 @@ extern "C" int nsm_bn_act(const void* y, int ldy, int M, int C, const float* sca
   return 0;
 }
 
+extern "C" int nsm_bn_act_h2(const float* y, int ldy, int M, int C, const float* scale,
+                             const float* shift, float slope, const float* mask, int HW, void* out,
+                             const uint32_t* bound, void* stream) {
+  NSM_CHECK_ARG(y && scale && shift && out && bound && C % 8 == 0 && C <= 2048 && ldy % 8 == 0 &&
+                    (!mask || HW > 0) && ((uintptr_t)out % 16) == 0,
+                "bn_act_h2: bad args");
+  NSM_CHECK_ARG(M >= 0 && M < (1 << 30), "bn_act_h2: too large");
+  if (M == 0) return 0;
+  dim3 g, b;
+  pix_launch(M, C / 8, g, b);
+  hipLaunchKernelGGL(bn_act_h2_kernel, g, b, 0, as_stream(stream), y, ldy, M, C / 8,
+                     make_fastdiv(mask ? HW : 1), scale, shift, slope, mask, (bf16_t*)out,
+                     H2Scale{bound, 1.f});
+  NSM_LAUNCH_CHECK("bn_act_h2");
+  return 0;
+}
+
 extern "C" int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy, int M, int C,
                                  int HW, const float* scale, const float* shift, float slope,
                                  const float* mask, const float* mean, const float* invstd,
-                                 float* partial, int nchunk, int dtype, void* stream) {
+                                 float* partial, int nchunk, int dtype, uint32_t* amax_k1dz,
+                                 void* stream) {
   NSM_CHECK_ARG(g && y && scale && shift && mean && invstd && partial && C % 8 == 0 &&
                     ldg % 8 == 0 && ldy % 8 == 0, "bn_bwd_reduce: bad args");
   ColRed r = colred_plan(M, C);
@@ -1922,22 +2026,26 @@ extern "C" int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy,
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<bf16_t>, gr, dim3(256), 0, as_stream(stream),
                        NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, make_fastdiv(HW),
-                       scale, shift, slope, mask, mean, invstd, r.cl, r.rl, r.rpc, partial);
+                       scale, shift, slope, mask, mean, invstd, r.cl, r.rl, r.rpc, partial,
+                       amax_k1dz);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, gr, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, make_fastdiv(HW), scale,
-                       shift, slope, mask, mean, invstd, r.cl, r.rl, r.rpc, partial);
+                       shift, slope, mask, mean, invstd, r.cl, r.rl, r.rpc, partial, amax_k1dz);
   NSM_LAUNCH_CHECK("bn_bwd_reduce");
   return 0;
 }
 
 extern "C" int nsm_bn_bwd_finalize(const float* partial, int nchunk, int M, int C, int c_real,
                                    const float* gamma, const float* invstd, float* dgamma,
-                                   float* dbeta, float* dbias_prev, float* coef, void* stream) {
+                                   float* dbeta, float* dbias_prev, float* coef,
+                                   const uint32_t* amax_k1dz, uint32_t* bound, void* stream) {
   NSM_CHECK_ARG(partial && gamma && invstd && coef, "bn_bwd_finalize: bad args");
+  NSM_CHECK_ARG(!bound || amax_k1dz, "bn_bwd_finalize: a bound needs the max|k1 dz| slot");
+  NSM_CHECK_ARG(M > 1 || !bound, "bn_bwd_finalize: M");
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0,
                      as_stream(stream), partial, nchunk, M, C, c_real, gamma, invstd, dgamma, dbeta,
-                     dbias_prev, coef);
+                     dbias_prev, coef, amax_k1dz, bound);
   NSM_LAUNCH_CHECK("bn_bwd_finalize");
   return 0;
 }
@@ -1963,6 +2071,25 @@ extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, 
                        NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, C / 8, fh, scale,
                        shift, slope, mask, mean, coef, NSM_T(float, dy), lddy, amax);
   NSM_LAUNCH_CHECK("bn_bwd_apply");
+  return 0;
+}
+
+extern "C" int nsm_bn_bwd_apply_h2(const float* g, int ldg, const float* y, int ldy, int M, int C,
+                                   int HW, const float* scale, const float* shift, float slope,
+                                   const float* mask, const float* mean, const float* coef,
+                                   void* dy, const uint32_t* bound, void* stream) {
+  NSM_CHECK_ARG(g && y && scale && shift && mean && coef && dy && bound && C % 8 == 0 &&
+                    C <= 2048 && ldg % 8 == 0 && ldy % 8 == 0 && (!mask || HW > 0) &&
+                    ((uintptr_t)dy % 16) == 0,
+                "bn_bwd_apply_h2: bad args");
+  NSM_CHECK_ARG(M >= 0 && M < (1 << 30), "bn_bwd_apply_h2: too large");
+  if (M == 0) return 0;
+  dim3 gr, b;
+  pix_launch(M, C / 8, gr, b);
+  hipLaunchKernelGGL(bn_bwd_apply_h2_kernel, gr, b, 0, as_stream(stream), g, ldg, y, ldy, M, C,
+                     C / 8, make_fastdiv(mask ? HW : 1), scale, shift, slope, mask, mean, coef,
+                     (bf16_t*)dy, H2Scale{bound, 1.f});
+  NSM_LAUNCH_CHECK("bn_bwd_apply_h2");
   return 0;
 }
 
@@ -2306,10 +2433,10 @@ extern "C" int nsm_bnred_chunks(int kind, int B, int H, int W, int C) {
 
 #define NSM_BNRED_ARGS                                                                  \
   const void *y2, const float *scale, const float *shift, const float *mean,            \
-      const float *invstd, float slope, float *partial
+      const float *invstd, float slope, float *partial, uint32_t *amax_k1dz
 #define NSM_BNRED_CHECK(what)                                                           \
   NSM_CHECK_ARG(y2 && scale && shift && mean && invstd && partial, what ": null BN args"); \
-  const BnRedP rp{y2, scale, shift, mean, invstd, slope, partial}
+  const BnRedP rp{y2, scale, shift, mean, invstd, slope, partial, amax_k1dz}
 
 extern "C" int nsm_avgpool2_bwd_add_bnred(const void* dy, int B, int H, int W, int C,
                                           const void* skip, void* dx, int dtype, NSM_BNRED_ARGS,

@@ -325,9 +325,15 @@ __global__ void __launch_bounds__(1024) tail_finalize_kernel(
       // main.py:368 unscale_ (x 1/scale), then :371-397 on the unscaled grad
       const float inv_s = (float)(1.0 / (double)scale);
       float n2 = (n1 * f1) * inv_s;
-      // an overflowed norm (finite values, sum of squares > FLT_MAX): the
-      // reference's factor 1/max(1, inf) = 0 zeroes the gradient, whose norm
-      // is then 0 and the step goes on (main.py:361-365); inf * 0 is NaN here
+      // The tail follows the arithmetic of the reference's CPU path, the
+      // oracle of this port (scale 1, main.py:175): torch.norm of an fp32
+      // tensor sums the squares in double there, so the fp32 norm is +inf only
+      // when the norm itself exceeds FLT_MAX (finite values, |g| > 3.4e38).
+      // Then the reference's factor 1/max(1, inf) = 0 zeroes the gradient,
+      // whose norm is 0 and the step goes on (main.py:361-365); inf * 0 is NaN
+      // here. (On CUDA torch sums the squares in fp32 and a norm above ~1.8e19
+      // already reads inf; a norm between the two is rescaled to 1000 here, as
+      // on the CPU: tests/test_gpu_tail.py::test_large_finite_norm_rescales_like_cpu.)
       if (n1 == __builtin_inff()) n2 = 0.f;
       // a non-finite survivor of the repair (:374-381) is impossible once
       // zeroed; only an infinite norm (overflowed sum of squares) is left

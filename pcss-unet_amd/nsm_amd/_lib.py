@@ -52,12 +52,20 @@ _SIGS = {
     "nsm_reduce_chunks": (I, [I, I]),
     "nsm_reduce_rows": (I, [I, I]),
     "nsm_bn_stats": (I, [P, I, I, I, P, I, I, P]),
-    "nsm_bn_finalize_train": (I, [P, I, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P]),
+    "nsm_bn_finalize_train": (I, [P, I, I, I, I, I, P, P, P, P, P, F, F, I, P, P, P, P, P, F, P]),
+    "nsm_bn_act_h2": (I, [P, I, I, I, P, P, F, P, I, P, P, P]),
+    "nsm_conv1x1_h2_rows": (I, [I, I, I, I]),
+    "nsm_conv1x1_h2": (I, [P, I, I, P, P, I, P, I, P, P, P, P]),
+    "nsm_conv1x1_dgrad_bnbwd_h2": (I, [P, I, I, P, I, P, I, P, P, P, P, P, I, F, I, P, P, P, I, P,
+                                       P, P, P]),
+    "nsm_conv1x1_wgrad_h2_ws": (Z, [I, I, I]),
+    "nsm_conv1x1_wgrad_h2": (I, [P, P, I, I, I, I, I, P, P, Z, P, P, P]),
     "nsm_bn_partials_merge": (I, [P, I, I, I, I, I, P, P]),
     "nsm_bn_finalize_eval": (I, [P, P, P, P, I, I, F, P, P, P, P, P]),
     "nsm_bn_act": (I, [P, I, I, I, P, P, F, P, I, P, I, P, I, I, P, P]),
-    "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P]),
-    "nsm_bn_bwd_finalize": (I, [P, I, I, I, I, P, P, P, P, P, P, P]),
+    "nsm_bn_bwd_reduce": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P, P]),
+    "nsm_bn_bwd_finalize": (I, [P, I, I, I, I, P, P, P, P, P, P, P, P, P]),
+    "nsm_bn_bwd_apply_h2": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, P, P]),
     "nsm_bn_bwd_apply": (I, [P, I, P, I, I, I, I, P, P, F, P, P, P, P, I, I, P, P]),
     "nsm_sum_rows": (I, [P, I, I, I, P, P]),
     "nsm_resize_fwd_act": (I, [P, I, I, I, I, P, I, I, P, P, F, P, I, P]),
@@ -69,9 +77,9 @@ _SIGS = {
     "nsm_conv_fwd_act": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, F, P, I, I, P]),
     "nsm_wino_output_act": (I, [P, I, I, I, I, I, P, P, I, P, P, F, P, I, P]),
     "nsm_bnred_chunks": (I, [I, I, I, I, I]),
-    "nsm_avgpool2_bwd_add_bnred": (I, [P, I, I, I, I, P, P, I, P, P, P, P, P, F, P, P]),
-    "nsm_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P]),
-    "nsm_up2_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P]),
+    "nsm_avgpool2_bwd_add_bnred": (I, [P, I, I, I, I, P, P, I, P, P, P, P, P, F, P, P, P]),
+    "nsm_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P, P]),
+    "nsm_up2_resize_bwd_bnred": (I, [P, I, I, I, I, P, I, I, I, P, P, P, P, P, F, P, P, P]),
     "nsm_wino_input_resize": (I, [P, I, I, I, I, I, I, I, I, I, P, P, P]),
     "nsm_wino_output_stats": (I, [P, I, I, I, I, I, P, P, I, P, I, P]),
     "nsm_wino_stat_slots": (I, [I, I, I, I, I]),
@@ -123,7 +131,7 @@ _SIGS = {
     "nsm_dropout_masks": (I, [P, I, I, U64, P, P]),
     "nsm_stage_mark": (I, [I, P]),
     "nsm_prep_items": (L, [P]),
-    "nsm_prep_weights": (I, [P, I, L, P]),
+    "nsm_prep_weights": (I, [P, I, L, I, P]),
 }
 
 

@@ -494,23 +494,30 @@ def merged(part, M, C):
     return part._merged
 
 
-def _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, gamma, beta=None):
+def _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, gamma, beta=None,
+              bound=None):
     part = merged(part, M, C)
     if beta is None:
         beta = pad_vec(bn_mod.bias.detach(), C)
     track = bn_mod.track_running_stats
+    slot, mul = bound if bound is not None else (None, 1.0)
     call("nsm_bn_finalize_train", ptr(part.buf), part.nchunk, part.rpc, M, C, c_real, ptr(gamma),
          ptr(beta), ptr(bn_mod.running_mean if track else None),
          ptr(bn_mod.running_var if track else None),
          ptr(bn_mod.num_batches_tracked if track else None), momentum, eps, n_updates,
-         ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift), stream())
+         ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift), ptr(slot), float(mul),
+         stream())
 
 
-def bn_train(y, bn_mod, c_real, momentum, eps, n_updates=1, part=None, gamma=None, beta=None):
+def bn_train(y, bn_mod, c_real, momentum, eps, n_updates=1, part=None, gamma=None, beta=None,
+             bound=None):
     """Train-mode BN: batch statistics of y [M, C] (given as fused GEMM
     partials, or computed here) + running-stat update in place on the module's
     buffers -> BNState with scale/shift for the fused apply. gamma / beta: the
-    affine parameters padded to C (pad_vec'd here when not given)."""
+    affine parameters padded to C (pad_vec'd here when not given).
+    bound=(slot, mask_max): the zeroed operand-maximum slot receiving a bound
+    of max|lrelu(BN(y))| * mask_max (nsm_bn_finalize_train), the scale source
+    of bn_act_h2."""
     M, C = y.shape
     if part is None:
         part = bn_partials(y)
@@ -518,7 +525,8 @@ def bn_train(y, bn_mod, c_real, momentum, eps, n_updates=1, part=None, gamma=Non
     st.part, st.nchunk = part, part.nchunk
     st.gamma = gamma if gamma is not None else pad_vec(bn_mod.weight.detach(), C)
     st.beta = beta if beta is not None else pad_vec(bn_mod.bias.detach(), C)
-    _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, st.gamma, st.beta)
+    _finalize(part, M, C, bn_mod, c_real, momentum, eps, n_updates, st, st.gamma, st.beta,
+              bound=bound)
     return st
 
 
@@ -553,22 +561,86 @@ def bn_act(y, st, slope=0.2, res=None, out=None, mask=None, HW=0, amax=None):
     return o
 
 
+def bn_act_h2(y, st, slope=0.2, mask=None, HW=0, bound=None):
+    """bn_act (fp32, no skip) written as an h2 tensor [M, 2C] float16
+    (nsm_bn_act_h2); bound: the slot bn_train(bound=...) filled, its scale
+    source."""
+    M, C = y.shape
+    assert y.dtype == F32 and bound is not None and (mask is None or HW > 0)
+    o = torch.empty(M, 2 * C, dtype=H2, device=y.device)
+    call("nsm_bn_act_h2", ptr(y), y.stride(0), M, C, ptr(st.scale), ptr(st.shift), slope,
+         ptr(mask), HW, ptr(o), ptr(bound), stream())
+    return o
+
+
+def to_h2(x, amax, beta=1.0):
+    """fp32 [rows, C] -> h2 tensor [rows, 2C] float16 (nsm_to_h2), scale source
+    (amax slot, beta)."""
+    rows, C = x.shape
+    assert x.is_contiguous() and x.dtype == F32
+    o = torch.empty(rows, 2 * C, dtype=H2, device=x.device)
+    call("nsm_to_h2", ptr(x), rows, C, ptr(amax), float(beta), ptr(o), stream())
+    return o
+
+
+def conv1x1_h2(xh, wh, bias, cout_p, stats=True, amax=(None, None), tag=None):
+    """1x1 conv on h2 operands (nsm_conv1x1_h2): xh [M, 2 cin_p] (bn_act_h2),
+    wh the FWD h2 pack; amax = (scale source of xh, of wh). Returns (y fp32
+    [M, cout_p], Partials|None)."""
+    from ._lib import lib
+    M, cin2 = xh.shape
+    assert xh.dtype == H2 and wh.dtype == H2 and amax[0] is not None and amax[1] is not None
+    y = empty(M, cout_p, device=xh.device)
+    part = None
+    if stats:
+        rpc = int(lib.nsm_conv1x1_h2_rows(M, cout_p, cin2, 0))
+        nchunk = -(-M // rpc)
+        part = Partials(empty(nchunk * 2 * cout_p, device=xh.device), nchunk, rpc)
+    ev = _probe(tag)
+    call("nsm_conv1x1_h2", ptr(xh), M, cin2 // 2, ptr(wh), ptr(bias), cout_p, ptr(y), y.stride(0),
+         ptr(part.buf) if part is not None else None, ptr(amax[0]), ptr(amax[1]), stream())
+    if ev is not None:
+        ev.record()
+    return y, part
+
+
+def conv1x1_wgrad_h2(dyh, xh, cin, cout, dw, amax=(None, None), tag=None):
+    """dw [cout, cin, 1, 1] <- sum_p dy (x) x over h2 pixel rows
+    (nsm_conv1x1_wgrad_h2); amax = (scale source of dyh, of xh)."""
+    from ._lib import lib
+    M, cout2 = dyh.shape
+    cin_p, cout_p = xh.shape[1] // 2, cout2 // 2
+    assert xh.shape[0] == M and dyh.dtype == H2 and xh.dtype == H2
+    n = int(lib.nsm_conv1x1_wgrad_h2_ws(M, cin_p, cout_p))
+    ws = empty(max(n, 1), device=dyh.device)
+    ev = _probe(tag)
+    call("nsm_conv1x1_wgrad_h2", ptr(dyh), ptr(xh), M, cin_p, cout_p, cin, cout, ptr(dw), ptr(ws),
+         n, ptr(amax[0]), ptr(amax[1]), stream())
+    if ev is not None:
+        ev.record()
+
+
 def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, part=None,
-           defer=False, amax=None):
+           defer=False, amax=None, h2=None):
     """Backward through lrelu(.)*mask after a train-mode BN: returns dy
     (grad wrt the BN input) and writes dgamma/dbeta/dbias_prev (real chans).
     part=(partial, nchunk): the {sum dz, sum dz*xhat} partials already written
     by g's producer (GradPart), so the reduce pass is skipped. defer=True:
     DeferredBnBwd(g, coef) instead of dy (its consumer forms dy itself).
-    amax: operand-maximum slot receiving max|dy| (fp32)."""
+    amax: operand-maximum slot receiving max|dy| (fp32).
+    h2=(k1dz slot, bound slot), both zeroed (fp32): dy is returned as an h2
+    tensor [M, 2C] (nsm_bn_bwd_apply_h2) scaled from the bound the finalize
+    derives from max|k1 dz| (recorded by the reduce pass, or by g's producer
+    when part is given: pass it the same k1dz slot)."""
     M, C = y.shape
     assert g.dtype == y.dtype
+    k1dz, bound = h2 if h2 is not None else (None, None)
     if part is None:
         nchunk = reduce_chunks(M, C)
         partial = empty(nchunk * 2 * C, device=y.device)
         call("nsm_bn_bwd_reduce", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW,
              ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(st.invstd),
-             ptr(partial), nchunk, dt(y), stream())
+             ptr(partial), nchunk, dt(y), ptr(k1dz), stream())
     else:
         partial, nchunk = part
         if nchunk > SUM_ROWS_ABOVE:
@@ -579,9 +651,16 @@ def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, par
             partial, nchunk = buf, n2
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
-         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
+         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), ptr(k1dz), ptr(bound), stream())
     if defer:
         return DeferredBnBwd(g, coef)
+    if h2 is not None:
+        assert y.dtype == F32
+        dyh = torch.empty(M, 2 * C, dtype=H2, device=y.device)
+        call("nsm_bn_bwd_apply_h2", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW,
+             ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dyh),
+             ptr(bound), stream())
+        return dyh
     dy = like(M, C, y)
     call("nsm_bn_bwd_apply", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
          ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy), dy.stride(0), dt(y),
@@ -628,7 +707,7 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
         partial, nchunk = buf, n2
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
-         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), stream())
+         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), None, None, stream())
     if defer and not recompute:
         if ev is not None:
             ev.record()
@@ -646,6 +725,45 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     return dy
 
 
+def conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2dh, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
+                            recompute, slope=0.2, tag=None, amax=(None, None), amax_out=None):
+    """conv1x1_dgrad_bn_bwd on h2 operands (nsm_conv1x1_dgrad_bnbwd_h2): dY2h
+    [M, 2 cop] (to_h2 of dY2), w2dh the DGRAD h2 pack; amax = (scale source of
+    dY2h, of w2dh). HW: pixels per image (the Dropout2d mask row)."""
+    from ._lib import lib
+    M, cop2 = dY2h.shape
+    C = y.shape[1]
+    assert dY2h.dtype == H2 and w2dh.dtype == H2 and y.dtype == F32
+    nchunk = -(-M // int(lib.nsm_conv1x1_h2_rows(M, C, cop2, 1)))
+    partial = empty(nchunk * 2 * C, device=y.device)
+    dA1 = None if recompute else like(M, C, y)
+    args = (ptr(dY2h), M, cop2 // 2, ptr(w2dh), C, ptr(y), y.stride(0), ptr(st.scale),
+            ptr(st.shift), ptr(st.mean), ptr(st.invstd), ptr(mask), HW, slope)
+    ev = _probe(tag)
+    call("nsm_conv1x1_dgrad_bnbwd_h2", *args, 0 if recompute else 1, ptr(partial), None, ptr(dA1),
+         dA1.stride(0) if dA1 is not None else 0, ptr(amax[0]), ptr(amax[1]), None, stream())
+    if nchunk > SUM_ROWS_ABOVE:
+        G = -(-nchunk // SUM_ROWS_ABOVE)
+        n2 = -(-nchunk // G)
+        buf = empty(n2 * 2 * C, device=y.device)
+        call("nsm_sum_rows", ptr(partial), nchunk, 2 * C, G, ptr(buf), stream())
+        partial, nchunk = buf, n2
+    coef = empty(3 * C, device=y.device)
+    call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
+         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), None, None, stream())
+    dy = like(M, C, y)
+    if recompute:
+        call("nsm_conv1x1_dgrad_bnbwd_h2", *args, 2, None, ptr(coef), ptr(dy), dy.stride(0),
+             ptr(amax[0]), ptr(amax[1]), ptr(amax_out), stream())
+    else:
+        call("nsm_bn_bwd_apply", ptr(dA1), dA1.stride(0), ptr(y), y.stride(0), M, C, HW,
+             ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy),
+             dy.stride(0), NSM_F32, ptr(amax_out), stream())
+    if ev is not None:
+        ev.record()
+    return dy
+
+
 # ---- resampling --------------------------------------------------------------
 def avgpool2(x, B, H, W):
     C = x.shape[1]
@@ -656,18 +774,20 @@ def avgpool2(x, B, H, W):
 
 def _bnred(kind, B, H, W, C, bnred, device, slope=0.2):
     """(extra C-ABI args, (partial, nchunk)) for a gradient producer that also
-    reduces the BN backward of bnred = (y2, BNState); (None, None) when the
-    fused form does not apply to this shape."""
+    reduces the BN backward of bnred = (y2, BNState[, k1dz slot]); (None, None)
+    when the fused form does not apply to this shape. The k1dz slot receives
+    max|scale * dz| (bn_bwd(h2=...))."""
     from ._lib import lib
     if bnred is None:
         return None, None
     n = int(lib.nsm_bnred_chunks(kind, B, H, W, C))
     if n <= 0:
         return None, None
-    y2, st = bnred
+    y2, st = bnred[:2]
+    k1dz = bnred[2] if len(bnred) > 2 else None
     partial = empty(n * 2 * C, device=device)
     return ((ptr(y2), ptr(st.scale), ptr(st.shift), ptr(st.mean), ptr(st.invstd), slope,
-             ptr(partial)), (partial, n))
+             ptr(partial), ptr(k1dz)), (partial, n))
 
 
 def avgpool2_bwd_add(dy, B, H, W, skip, bnred=None):

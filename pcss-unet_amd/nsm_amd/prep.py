@@ -25,11 +25,15 @@ class NsmPrepJob(ctypes.Structure):
                 ("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("amax", ctypes.c_void_p)]
 
 
-KIND_PACK_F32, KIND_PACK_BF16, KIND_WINO, KIND_PAD, KIND_WINO_H2 = 0, 1, 2, 3, 4
+KIND_PACK_F32, KIND_PACK_BF16, KIND_WINO, KIND_PAD, KIND_WINO_H2, KIND_PACK_H2 = 0, 1, 2, 3, 4, 5
 # NSM_H2=0: the fp32 training step keeps fp32 Winograd operands (the GEMMs
 # split them in-kernel, nsm_conv_split16.inc) instead of the pre-split h2
 # tensors their producers write (nsm_conv_h2.inc)
 H2_WINO = os.environ.get("NSM_H2", "1") != "0"
+# NSM_H2_1X1=0: the DoubleConv 1x1 convolutions of the fp32 training step keep
+# fp32 operands (register-path f16x2 split) instead of h2 operands written by
+# their producers (csrc/nsm_conv_h2d.inc); on with the h2 Winograd operands
+H2_1X1 = os.environ.get("NSM_H2_1X1", "1") != "0"
 
 
 class LazyBlockWeights:
@@ -182,17 +186,28 @@ class StepWeights:
                         pb.t[("amaxw1", mode)] = am
                     pb.t[("w1", mode)] = add(pk, (ci, ci, 9, cip, cip, mode), c0.weight,
                                              cip * 9 * cip, dtype, amax=am)
+            h2_1x1 = h2 and training and H2_1X1
             for mode in modes:
                 am = None
-                if dtype == torch.float32:
+                if h2_1x1 and mode != ops.PACK_FWD:
+                    am = pb.t[("amaxw2", ops.PACK_FWD)]   # max|w| of the same weight
+                elif dtype == torch.float32:
                     am = ops.amax_slot(self.amax, n_am)
                     n_am += 1
+                if am is not None:
                     pb.t[("amaxw2", mode)] = am
-                pb.t[("w2", mode)] = add(pk, (co, ci, 1, cop, cip, mode), c4.weight, cop * cip, dtype,
-                                         amax=am)
+                if h2_1x1:   # h2 packs [rows][2 K] float16 (prep kind 5, nsm_conv_h2d.inc)
+                    pb.t[("w2", mode)] = add(KIND_PACK_H2, (co, ci, 1, cop, cip, mode,
+                                                            int(mode != ops.PACK_FWD)),
+                                             c4.weight, 2 * cop * cip, ops.H2, amax=am)
+                else:
+                    pb.t[("w2", mode)] = add(pk, (co, ci, 1, cop, cip, mode), c4.weight, cop * cip,
+                                             dtype, amax=am)
             self.blocks[k] = pb
         self.total = base
         self.njobs = len(jobs)
+        # the max|w| pass (phase 0) runs only for the h2 jobs' scale sources
+        self.max_pass = int(any(j.kind in (KIND_WINO_H2, KIND_PACK_H2) for j in jobs))
         raw = (NsmPrepJob * len(jobs))(*jobs)
         host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
         self.table = host.to(dev)
@@ -204,7 +219,7 @@ class StepWeights:
 
     def run(self):
         self.amax.zero_()
-        call("nsm_prep_weights", ptr(self.table), self.njobs, self.total, stream())
+        call("nsm_prep_weights", ptr(self.table), self.njobs, self.total, self.max_pass, stream())
 
     def block(self, k):
         return self.blocks[k]

@@ -104,7 +104,7 @@ BNB_MODE = int(os.environ.get("NSM_BNB", "2"))
 GRAD_BNRED = os.environ.get("NSM_GRAD_BNRED", "1") != "0"
 
 
-def bnb_mode(cip, cop, dtype):
+def bnb_mode(cip, cop, dtype, h2=False):
     """0: conv_fwd + bn_bwd; 1: fused epilogue storing dA1, then bn_bwd_apply;
     2: fused epilogue twice (partials, then dY1; dA1 never stored) where the
     HBM bytes saved, (2*cip - cop) elements per pixel, outweigh the second
@@ -119,7 +119,10 @@ def bnb_mode(cip, cop, dtype):
         return 0 if BNB_MODE == 2 else 1
     if BNB_MODE == 1:
         return 1
-    s, rate = (2, 6e14) if dtype == torch.bfloat16 else (4, 1.2e14)
+    # fp32-product rate of the pass: bf16 ~0.6 PF; fp32 register-path f16x2
+    # split ~0.12 PF; fp32 on h2 operands (nsm_conv_h2d.inc) ~1 PF of f16 MFMA
+    # work = ~0.3 PF of fp32 products
+    s, rate = (2, 6e14) if dtype == torch.bfloat16 else (4, 3e14 if h2 else 1.2e14)
     return 2 if (2 * cip - cop) * s / 5e12 > 2 * cip * cop / rate else 1
 ENCODER = (2, 3, 4, 5)
 DECODER = (6, 7, 8, 9)
@@ -374,8 +377,10 @@ class Unet(nn.Module):
 def _masks_for(mod, B, device, training):
     """[B, C_in_padded] Dropout2d masks of the blocks with p > 0: injected ones
     (parity), else all drawn in ONE nsm_dropout_masks launch seeded from torch's
-    default CPU generator (so torch.manual_seed makes them reproducible)."""
-    masks = {}
+    default CPU generator (so torch.manual_seed makes them reproducible).
+    Returns (masks, their maxima) — a mask's maximum bounds the activated 1x1
+    operand (bn_train(bound=...)): 1/(1-p) for drawn masks."""
+    masks, mmax = {}, {}
     inj = mod._inject_masks
     mod._inject_masks = None
     jobs = []
@@ -387,6 +392,7 @@ def _masks_for(mod, B, device, training):
         ci = blk.conv[0].in_channels
         cp = ops.pad32(ci)
         if inj is not None and k in inj:
+            mmax[k] = float(inj[k].abs().max())   # parity hook (tests): host value
             m = inj[k].to(device=device, dtype=torch.float32).reshape(B, ci)
             if cp != ci:
                 m = torch.nn.functional.pad(m, (0, cp - ci))
@@ -413,8 +419,9 @@ def _masks_for(mod, B, device, training):
         off = 0
         for k, ci, cp, keep in jobs:
             masks[k] = flat[off:off + B * cp].view(B, cp)
+            mmax[k] = 1.0 / keep
             off += B * cp
-    return masks
+    return masks, mmax
 
 
 class _BlockSaved:
@@ -426,7 +433,10 @@ class _BlockSaved:
 # the operands' producers): Winograd V, Vd, dM; the 1x1 conv's A1 and dY2; the
 # scale sources of the pre-split (h2) Winograd operands: the block input X
 # (written by the previous block's output pass) and dY1
-AM_V, AM_VD, AM_DM, AM_A1, AM_DY2, AM_X, AM_DY1, AM_PER_BLOCK = 0, 1, 2, 3, 4, 5, 6, 7
+# (h2 1x1 operands: AM_A1 holds the bound of A1 from its BN finalize, AM_K1DZ
+# max|k1 dz| of the output BN's backward, AM_DY2B the bound of dY2 derived from it)
+AM_V, AM_VD, AM_DM, AM_A1, AM_DY2, AM_X, AM_DY1, AM_K1DZ, AM_DY2B = range(9)
+AM_PER_BLOCK = 9
 
 
 def _slot(am, i):
@@ -487,7 +497,7 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
 
 
 def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse_out=False,
-               res=None, am=None):
+               res=None, am=None, mask_max=1.0):
     """pw: the block's weight layouts (prep.StepWeights.block, all written by the
     step's single preparation launch), or None to build them here per call.
     src=(x_low, hi, wi): X is the bilinear resize of x_low to H x W, sampled
@@ -495,7 +505,8 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     fuse_out (eval, EVAL_FUSED): the block output lrelu(bn2(Y2)) (+ res) is
     produced by the convs' epilogues, returned as s.Z (Y1/Y2 not stored).
     am: the block's zeroed operand-maximum slots (AM_*: the f16x2 GEMMs'
-    operand scales), or None (bf16 split)."""
+    operand scales), or None (bf16 split). mask_max: the maximum of `mask` (the
+    bound of the h2 activated operand, bn_train(bound=...))."""
     c0, bn1m, c4, bn2m = blk.conv[0], blk.conv[1], blk.conv[4], blk.conv[5]
     ci, co = c0.in_channels, c4.out_channels
     cip, cop = ops.pad32(ci), ops.pad32(co)
@@ -534,15 +545,25 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
                                     stats=training,
                                     amax=(_slot(am, AM_X), pw.amax_w1(ops.PACK_FWD)))
     eps1, eps2 = bn1m.eps, bn2m.eps
-    if training:
-        bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1, gamma=pw.vec("g1"),
-                           beta=pw.vec("be1"))
-    else:
-        bn1 = ops.bn_eval(bn1m, cip, ci, eps1, xin.device, gamma=pw.vec("g1"), beta=pw.vec("be1"))
     w2 = pw.w2(ops.PACK_FWD)
     b2 = pw.vec("b2")
+    # h2 1x1 operands (fp32 training, csrc/nsm_conv_h2d.inc): A1 written by
+    # bn_act_h2, scaled from the bound the BN finalize records in AM_A1
+    h2x = training and w2.dtype == ops.H2
+    if training:
+        bn1 = ops.bn_train(Y1, bn1m, ci, bn1m.momentum, eps1, part=part1, gamma=pw.vec("g1"),
+                           beta=pw.vec("be1"),
+                           bound=(_slot(am, AM_A1), mask_max if mask is not None else 1.0)
+                           if h2x else None)
+    else:
+        bn1 = ops.bn_eval(bn1m, cip, ci, eps1, xin.device, gamma=pw.vec("g1"), beta=pw.vec("be1"))
     A1 = None
-    if BF16_MATERIALIZE_ACT if dtype == torch.bfloat16 else F32_MATERIALIZE_ACT:
+    if h2x:
+        A1 = ops.bn_act_h2(Y1, bn1, SLOPE, mask=mask, HW=H * W, bound=_slot(am, AM_A1))
+        Y2, part2 = ops.conv1x1_h2(A1, w2, b2, cop, stats=True,
+                                   amax=(_slot(am, AM_A1), pw.amax_w2(ops.PACK_FWD)),
+                                   tag=name + ".conv.4.fwd")
+    elif BF16_MATERIALIZE_ACT if dtype == torch.bfloat16 else F32_MATERIALIZE_ACT:
         # the same fp32 arithmetic and bf16 rounding as the fused operand prologue
         A1 = ops.bn_act(Y1, bn1, SLOPE, mask=mask, HW=H * W, amax=_slot(am, AM_A1))
         Y2, part2 = ops.conv_fwd_bn(A1, B, H, W, w2, b2, cop, 1, tag=name + ".conv.4.fwd",
@@ -575,10 +596,29 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
     B, H, W = s.B, s.H, s.W
     HW = H * W
     g = grads
-    dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias],
-                     part=gpart, amax=_slot(s.am, AM_DY2))
     dtype = G.dtype
     w2d = s.pw.w2(ops.PACK_DGRAD)
+    h2 = s.V is not None and s.V.dtype == ops.H2
+    am_dy1 = _slot(s.am, AM_DY1)
+    if s.A1 is not None and s.A1.dtype == ops.H2:
+        # h2 1x1 operands (csrc/nsm_conv_h2d.inc): the BN backward writes dY2
+        # pre-split, scaled from the bound its finalize derives (AM_DY2B); the
+        # weight and input gradients read it by LDS-DMA
+        am_dy2 = _slot(s.am, AM_DY2B)
+        dY2h = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias],
+                          part=gpart, h2=(_slot(s.am, AM_K1DZ), am_dy2))
+        ops.conv1x1_wgrad_h2(dY2h, s.A1, ci, co, g[c4.weight], amax=(am_dy2, _slot(s.am, AM_A1)),
+                             tag=name + ".conv.4.wgrad")
+        s.A1 = None
+        dY1 = ops.conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
+                                          g[bn1m.bias], g[c0.bias],
+                                          bnb_mode(s.cip, s.cop, dtype, h2=True) == 2,
+                                          tag=name + ".conv.4.dgrad",
+                                          amax=(am_dy2, s.pw.amax_w2(ops.PACK_DGRAD)),
+                                          amax_out=am_dy1)
+        return _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1)
+    dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias],
+                     part=gpart, amax=_slot(s.am, AM_DY2))
     am_w2d = (_slot(s.am, AM_DY2), s.pw.amax_w2(ops.PACK_DGRAD))
     if s.A1 is not None:
         ops.conv_wgrad(dY2, s.A1, B, H, W, 1, ci, co, g[c4.weight], tag=name + ".conv.4.wgrad",
@@ -590,8 +630,6 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
     mode = bnb_mode(s.cip, s.cop, dtype)
     # pre-split (h2) Winograd operands: dY1's producer records max|dY1|, the
     # scale source of both its transforms (Vd, dM)
-    h2 = s.V is not None and s.V.dtype == ops.H2
-    am_dy1 = _slot(s.am, AM_DY1)
     # dY1 is consumed only by its two Winograd transforms: leave the BN apply
     # to the dual transform kernel, dY1 is never stored
     lazy = s.V is not None and need_dx and DUAL_TRANSFORM and LAZY_DY1 and not h2
@@ -605,6 +643,18 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
                            amax=am_w2d)
         dY1 = ops.bn_bwd(dA1, s.Y1, s.bn1, HW, s.mask, ci, g[bn1m.weight], g[bn1m.bias],
                          g[c0.bias], defer=lazy, amax=am_dy1)
+    return _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1)
+
+
+def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
+    """The 3x3 conv's weight and input gradients of a DoubleConv from dY1 (the
+    gradient wrt its output Y1; a DeferredBnBwd where the dual transform forms
+    it). h2: the forward kept an h2 V (pre-split Winograd operands)."""
+    c0 = blk.conv[0]
+    ci = c0.in_channels
+    B, H, W = s.B, s.H, s.W
+    g = grads
+    dtype = s.Y1.dtype
     Vd = None
     if h2:
         tile = wino_tile(s.cip, H, W)
@@ -647,6 +697,15 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
     w1d = s.pw.w1(ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad",
                         amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)))
+
+
+def _bnred_of(s):
+    """bnred= of a gradient producer reducing block s's output-BN backward:
+    (Y2, bn2) and, where the block's 1x1 runs on h2 operands, its max|k1 dz|
+    slot (the dY2 bound, bn_bwd(h2=...))."""
+    if s.A1 is not None and s.A1.dtype == ops.H2:
+        return s.Y2, s.bn2, _slot(s.am, AM_K1DZ)
+    return s.Y2, s.bn2
 
 
 def block_shapes(Rh, Rw):
@@ -698,7 +757,7 @@ class _UnetFn(torch.autograd.Function):
         assert mod.conv2.conv[0].in_channels == 4 * C, (
             f"Unet expects {mod.conv2.conv[0].in_channels // 4} input channels, got {C}")
         cdt = mod.activation_dtype()
-        masks = _masks_for(mod, B, dev, training)
+        masks, mask_max = _masks_for(mod, B, dev, training)
         sw = _step_weights(mod, cdt, Rh, Rw, training)
         # per-step maxima of the f16x2 GEMM operands of every block (their
         # producers fill them; zeroed here, one launch)
@@ -711,7 +770,7 @@ class _UnetFn(torch.autograd.Function):
             with ops.stage(f"conv{k}.fwd"):
                 s = _block_fwd(mod.block(k), inp, B, h, w, training, masks.get(k), f"conv{k}",
                                pw=sw.block(k) if sw else None, fuse_out=True,
-                               am=_block_slots(amax, k))
+                               am=_block_slots(amax, k), mask_max=mask_max.get(k, 1.0))
                 saved[k], shapes[k] = s, (h, w)
                 if s.Z is not None:
                     c[k] = s.Z
@@ -755,7 +814,7 @@ class _UnetFn(torch.autograd.Function):
                 res = c[SKIP_OF[k]] if k in SKIP_OF else None
                 s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}",
                                pw=sw.block(k) if sw else None, src=src, fuse_out=True, res=res,
-                               am=_block_slots(amax, k))
+                               am=_block_slots(amax, k), mask_max=mask_max.get(k, 1.0))
                 saved[k] = s
                 if s.Z is not None:
                     cur = s.Z
@@ -820,8 +879,7 @@ class _UnetFn(torch.autograd.Function):
                 if (th, tw) != (h2, w2):
                     dprev, gpart = ops.up2_resize_bwd(dX, B, h, w, th, tw), None
                 elif GRAD_BNRED:
-                    dprev, gpart = ops.resize_bwd(dX, B, h, w, h2, w2,
-                                                  bnred=(sb[k - 1].Y2, sb[k - 1].bn2))
+                    dprev, gpart = ops.resize_bwd(dX, B, h, w, h2, w2, bnred=_bnred_of(sb[k - 1]))
                 else:
                     dprev, gpart = ops.resize_bwd(dX, B, h, w, h2, w2), None
             # the previous merge / c5 receives dprev; merge_{k-1} = conv + c_skip
@@ -850,7 +908,7 @@ class _UnetFn(torch.autograd.Function):
                 ph, pw = sb[k - 1].H, sb[k - 1].W
                 if GRAD_BNRED:
                     G, gpart = ops.avgpool2_bwd_add(dX, B, ph, pw, skip_grad.get(k - 1),
-                                                    bnred=(sb[k - 1].Y2, sb[k - 1].bn2))
+                                                    bnred=_bnred_of(sb[k - 1]))
                 else:
                     G = ops.avgpool2_bwd_add(dX, B, ph, pw, skip_grad.get(k - 1))
             else:

@@ -279,3 +279,38 @@ def test_h2_persistent_gemm_full_shapes(ops, device, B, H, W, ci, co):
         rms = ref.pow(2).mean().sqrt()
         assert ((got - ref).pow(2).mean().sqrt() / rms).item() < 2e-6, c
         assert ((got - ref).abs().max() / rms).item() < 3e-5, c
+
+
+def _scale_exp(m, beta):
+    """Host mirror of h2_exp / pow2_scale_exp (nsm_conv_split16.inc)."""
+    import numpy as np
+    b = np.float32(m) * np.float32(beta)
+    if np.isfinite(np.float32(m)) and not np.isfinite(b):
+        b = np.finfo(np.float32).max
+    u = int(np.array(b, dtype=np.float32).view(np.uint32))
+    if u == 0 or u >= 0x7f800000:
+        return 0
+    e = (u >> 23) - 127
+    if u & 0x7fffff:
+        e += 1
+    return max(-126, min(126, 15 - e))
+
+
+@pytest.mark.parametrize("mx,beta", [(2.0 ** -120, 1.0), (1e36, 3969.0), (3.0e38, 225.0), (1.0, 1.0)])
+def test_h2_scale_edges(ops, device, mx, beta):
+    """Scale edges of the h2 writers: a maximum below 2^-111 keeps a
+    normal undo factor (the data is represented, not flushed to zero), and a
+    bound beta * max above FLT_MAX saturates instead of falling back to s = 1
+    (which would turn values above 65504 into Inf). Decoding (h + l) / s gives
+    back x within the f16x2 bound relative to the maximum."""
+    g = torch.Generator().manual_seed(5)
+    x = (torch.rand(64, 32, generator=g) * 2 - 1) * mx
+    x[0, 0] = mx
+    xd = x.to(device)
+    am = ops.absmax(xd)
+    h2 = _h2(ops, xd, 64, 32, am, beta).view(64, 4, 2, 8).float().cpu()
+    e = _scale_exp(mx, beta)
+    dec = (h2[:, :, 0, :].double() + h2[:, :, 1, :].double()).reshape(64, 32) * 2.0 ** (-e)
+    assert torch.isfinite(dec).all()
+    err = (dec - x.double()).abs().max().item()
+    assert err <= mx * 2.0 ** -20, (err, mx)

@@ -141,6 +141,38 @@ def test_overflowing_norm_steps_like_reference():
         torch.testing.assert_close(p.detach().cpu(), r.detach(), rtol=1e-6, atol=1e-7)
 
 
+def test_large_finite_norm_rescales_like_cpu():
+    """A gradient norm of ~1.4e20: above the ~1.8e19 where an fp32 sum of
+    squares (torch.norm on CUDA) overflows, below FLT_MAX. The tail follows
+    the reference's CPU arithmetic (the oracle; squares summed in double): the
+    norm is finite, the pre-unscale clip (main.py:361-365) rescales it to 1000
+    and the step is taken, exactly as the CPU oracle decides."""
+    import nsm_amd
+    from oracle.step_tail_ref import sanitize_and_clip
+    g0 = torch.tensor([1e20, -1e20, 1.0, -2.0])
+    g1 = torch.tensor([0.5, -0.25, 0.125])
+    assert torch.isfinite(g0.norm()) and g0.norm().item() > 1.8e19
+    init = [torch.tensor([0.1, -0.2, 0.3, 0.4]), torch.tensor([1.0, 2.0, -1.0])]
+    ref = [torch.nn.Parameter(t.clone()) for t in init]
+    for p, g in zip(ref, (g0, g1)):
+        p.grad = g.clone()
+    assert not sanitize_and_clip(ref, 0, 200)
+    assert ref[0].grad.abs().max().item() > 0      # rescaled, not zeroed
+    ropt = torch.optim.AdamW(ref, lr=1e-3, weight_decay=1e-3)
+    ropt.step()
+    ps = [torch.nn.Parameter(t.clone().to(DEV)) for t in init]
+    opt = nsm_amd.FlatAdamW(ps, lr=1e-3, weight_decay=1e-3, max_grad_norm=1.0, sanitize=True,
+                            seed=1)
+    for p, g in zip(ps, (g0, g1)):
+        p.grad = g.clone().to(DEV)
+    opt.step()
+    fl = opt.last_flags()
+    assert fl["skip"] == 0 and fl["nonfinite"] == 0, fl
+    assert opt.steps_taken() == 1
+    for p, r in zip(ps, ref):
+        torch.testing.assert_close(p.detach().cpu(), r.detach(), rtol=1e-6, atol=1e-7)
+
+
 def test_repair_noise_fresh_after_skipped_step():
     """The repair noise is keyed by the tail-call counter: a repaired step that
     is then skipped (post-clip norm > 10, main.py:408-418) does not advance
