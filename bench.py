@@ -176,14 +176,39 @@ def stage_table(work, times_ms, pipe_mult, peak, measured=None):
     return rows
 
 
+_LIB_SHA = []
+
+
+def loaded_lib_sha256():
+    """sha256 of the libnsm.so this process loaded (the profile stamps' key)."""
+    if not _LIB_SHA:
+        import hashlib
+        import nsm_amd
+        with open(nsm_amd.LIB_PATH, "rb") as f:
+            _LIB_SHA.append(hashlib.sha256(f.read()).hexdigest())
+    return _LIB_SHA[0]
+
+
+def _stamped(doc, rel):
+    """(doc, source) when the summary was measured on the loaded library,
+    else (None, "<file> (stale: ...)") — a profile of another build never
+    feeds the driver line (tools/stage_pmc.py stamp)."""
+    st = (doc or {}).get("stamp") or {}
+    if st.get("libnsm_sha256") != loaded_lib_sha256():
+        return None, f"{rel} (stale: measured on libnsm {str(st.get('libnsm_sha256'))[:12]}, " \
+                     f"loaded {loaded_lib_sha256()[:12]})"
+    return doc, rel
+
+
 def load_stage_pmc(tag):
-    """The newest committed per-stage PMC summary of this configuration."""
+    """The newest committed per-stage PMC summary of this configuration, if it
+    was measured on the loaded library."""
     import glob
     files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", f"stage_pmc_{tag}.json")))
     if not files:
         return None, None
     with open(files[-1]) as f:
-        return json.load(f), os.path.relpath(files[-1], ROOT)
+        return _stamped(json.load(f), os.path.relpath(files[-1], ROOT))
 
 
 def mean_ms(evs):
@@ -199,8 +224,8 @@ def load_traffic(name):
     if not files:
         return None, None
     with open(files[-1]) as f:
-        t = json.load(f)
-    return t.get("traffic_bytes_per_launch"), os.path.relpath(files[-1], ROOT)
+        t, src = _stamped(json.load(f), os.path.relpath(files[-1], ROOT))
+    return (t.get("traffic_bytes_per_launch") if t else None), src
 
 
 def cpu_baseline(in_ch, H, W, frames=8, reps=3, train=True, bf16_autocast=False):

@@ -121,3 +121,102 @@ def test_repaired_step_keeps_replicas_identical():
     assert res[0][0] == res[1][0]                     # shared seed
     assert res[0][1] == 1 and res[0][2] == 0          # repaired, step taken
     assert (res[0][3] == res[1][3]).all()
+
+
+def _dp_steps_worker(rank, world, port, q, steps):
+    """`Unet.data_parallel()` (rank 0's BN buffers broadcast at every forward,
+    the overlapped bucket all-reduce) + FlatAdamW(world_size=2) for `steps`
+    steps; rank 0 then replays the same steps in ONE process (two replicas,
+    rank 0's buffers copied to the other before each forward, their gradients
+    summed) as the reference."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pcss-unet_amd"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import nsm_amd
+    from nsm_amd.optim import flat_grad
+    from oracle.weights import make_state, synthetic_batch
+    dev = torch.device("cuda", 0)
+    sd0 = {k: torch.from_numpy(v.copy()) for k, v in make_state(7, 42).items()}
+
+    def model():
+        m = nsm_amd.Unet(in_ch=7, dropout_rate=0.0).to(dev).train()
+        m.load_state_dict(sd0)
+        return m
+
+    x_np, y_np = synthetic_batch(2 * world, 7, 64, 64)
+    shard = lambda a, r: torch.from_numpy(a[2 * r:2 * r + 2]).to(dev)  # noqa: E731
+    crit = nsm_amd.CustomLoss(dev, 0.9, vgg_weights=False)
+    bufs = lambda m: torch.cat([b.detach().reshape(-1).double().cpu()  # noqa: E731
+                                for n, b in m.named_buffers()])
+    m = model().data_parallel()
+    opt = nsm_amd.FlatAdamW(m.parameters(), lr=1e-3, weight_decay=1e-3, max_grad_norm=1.0,
+                            world_size=world, sanitize=True)
+    x, y = shard(x_np, rank), shard(y_np, rank)
+    trace = []
+    for _ in range(steps):
+        opt.zero_grad()
+        crit(m(x), y, x).backward()
+        nsm_amd.allreduce_grads(m.parameters())
+        opt.step()
+        torch.cuda.synchronize()
+        trace.append((opt.flat.cpu().numpy().copy(), bufs(m).numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+    emu = None
+    if rank == 0:
+        a, b = model(), model()
+        opt_e = nsm_amd.FlatAdamW(a.parameters(), lr=1e-3, weight_decay=1e-3, max_grad_norm=1.0,
+                                  world_size=world, sanitize=True, seed=opt.seed)
+        emu = []
+        for _ in range(steps):
+            with torch.no_grad():
+                for (_, pa), (_, pb) in zip(a.named_parameters(), b.named_parameters()):
+                    pb.copy_(pa)
+                for ba, bb in zip(a.buffers(), b.buffers()):
+                    bb.copy_(ba)                    # rank 0's buffers, broadcast
+            opt_e.zero_grad()
+            for p in b.parameters():
+                p.grad = None
+            crit(a(shard(x_np, 0)), shard(y_np, 0), shard(x_np, 0)).backward()
+            crit(b(shard(x_np, 1)), shard(y_np, 1), shard(x_np, 1)).backward()
+            g = flat_grad(list(a.parameters()))
+            g += flat_grad(list(b.parameters()))     # the all-reduce's sum
+            opt_e.step()
+            torch.cuda.synchronize()
+            emu.append((opt_e.flat.cpu().numpy().copy(), bufs(a).numpy().copy(),
+                        bufs(b).numpy().copy()))
+    q.put((rank, trace, emu))
+
+
+@pytest.mark.timeout(900)
+def test_data_parallel_steps_match_single_process():
+    """three DP steps at B=2 per rank, 7x64^2, through
+    Unet.data_parallel() + FlatAdamW(world_size=2): parameters stay bitwise
+    identical across the ranks after every step and match a single-process
+    emulation (per-shard gradients summed, the tail's 1/world mean) within the
+    fp32 bounds; each rank's BN buffers match the emulation's replica of that
+    rank (DDP broadcast_buffers semantics: rank 0's buffers are broadcast at
+    every forward, then each rank's forward updates them from its own shard)."""
+    import numpy as np
+    steps = 3
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dp_steps_worker, args=(r, 2, port, q, steps)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=800) for _ in range(2)))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    t0, t1, emu = res[0][0], res[1][0], res[0][1]
+    for s in range(steps):
+        assert np.array_equal(t0[s][0], t1[s][0]), f"step {s}: parameters differ across ranks"
+        pd, pe = t0[s][0].astype(np.float64), emu[s][0].astype(np.float64)
+        # parameters: within fp32 rounding of the emulation (sum order of the
+        # two shards' gradients differs: gloo vs one add)
+        assert np.abs(pd - pe).max() <= 1e-5 * (1 + np.abs(pe).max()), s
+        for r, t in ((0, t0), (1, t1)):
+            bd, be = t[s][1], emu[s][1 + r]
+            assert np.abs(bd - be).max() <= 1e-4 * (1 + np.abs(be).max()), (s, r)

@@ -36,7 +36,11 @@ def _write(tmp, steps=3):
                        "TCC_EA0_RDREQ_64B_sum": 20, "TCC_EA0_RDREQ_128B_sum": 60,
                        "WRITE_SIZE": 2.0, "SQ_VALU_MFMA_BUSY_CYCLES": 1024 * 100,
                        "GRBM_GUI_ACTIVE": 8 * 200, "SQ_INSTS_VALU_MFMA_MOPS_BF16": 1000,
-                       "SQ_INSTS_VALU_MFMA_MOPS_F32": 0}}
+                       "SQ_INSTS_VALU_MFMA_MOPS_F32": 0},
+            # a short dispatch (< 0.3 ms): its busy fraction is not reported
+            "bwd_b": {"WRITE_SIZE": 1.0, "SQ_VALU_MFMA_BUSY_CYCLES": 1024 * 50,
+                      "GRBM_GUI_ACTIVE": 8 * 100}}
+    dur_ns = {"gemm_a": 400000}
     pm = tmp / "pmc.csv"
     with open(pm, "w", newline="") as f:
         w = csv.writer(f)
@@ -44,7 +48,7 @@ def _write(tmp, steps=3):
                     "Counter_Value", "Start_Timestamp", "End_Timestamp"])
         for i, (n, g) in enumerate(disp):
             for c, v in vals.get(n, {"WRITE_SIZE": 1.0, "GRBM_GUI_ACTIVE": 8}).items():
-                w.writerow([i + 1, i + 1, g, n, c, v, 0, 4000])
+                w.writerow([i + 1, i + 1, g, n, c, v, 0, dur_ns.get(n, 4000)])
     return tr, pm
 
 
@@ -65,6 +69,9 @@ def test_stage_attribution_and_counters(tmp_path):
     assert st["conv2.fwd"]["read_bytes"] == 32 * 10 + 64 * (20 + 10) + 128 * 60
     assert st["conv2.fwd"]["write_bytes"] == 2048
     assert st["conv2.fwd"]["mfma_busy"] == 0.5
+    assert abs(st["conv2.fwd"]["eff_clock_ghz"] - 200 / 0.4e-3 / 1e9) <= 1e-3  # rounded to MHz
+    assert "mfma_busy" not in st["conv2.bwd"]       # 0.004 ms dispatch: no clock / busy
+    assert len(d["stamp"]["libnsm_sha256"]) == 64
     assert st["conv2.fwd"]["bf16_mfma_flops"] == 512 * 1000
     # fwd + bwd rolled up
     assert st["conv2"]["kernel_ms"] == 0.003

@@ -110,6 +110,9 @@ def main():
         out["traffic_over_algorithmic"] = round(out["traffic_bytes_per_launch"] / k["alg"], 3)
     out["note"] = ("reads from the sized fabric read requests (FETCH_SIZE x 2 beside them as the "
                    "guide's cross-check); Infinity-Cache hits are counted, not excluded")
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from stage_pmc import stamp
+    out["stamp"] = stamp()
     json.dump(out, open(outp, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

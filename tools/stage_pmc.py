@@ -24,7 +24,9 @@ outside every stage go to "other": input prep, weight prep, loss, tail):
   hbm_gbs        hbm_bytes / kernel_ms
   mfma_busy      SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8):
                  the fraction of SIMD-cycles the matrix pipe was busy, at the
-                 clock the chip held
+                 clock the chip held — over the stage's dispatches of >= 0.3 ms
+                 only (MI355X_MICROARCH.md: GRBM_GUI_ACTIVE / 8 / time reads
+                 high on shorter dispatches); absent when it has none
   bf16_mfma_flops, f32_mfma_flops
                  512 x SQ_INSTS_VALU_MFMA_MOPS_{BF16+F16, F32}: the matrix-core
                  work actually issued, per pipe (16-bit: bf16 and f16 MFMAs run
@@ -33,8 +35,13 @@ outside every stage go to "other": input prep, weight prep, loss, tail):
   mfma_pipe_frac bf16 work / kernel_ms / 2516.6 TFLOP/s + f32 work / kernel_ms
                  / 157.3 TFLOP/s: the fraction of the dense peak of the pipe
                  that ran it (at the 2.4 GHz peak clock)
-  eff_clock_ghz  GRBM_GUI_ACTIVE / 8 / profiled kernel time
+  eff_clock_ghz  GRBM_GUI_ACTIVE / 8 / profiled kernel time, same dispatches
+The output carries `stamp` = {libnsm_sha256 of the library the runs loaded,
+git_head (env GIT_HEAD, the box has no .git)}: bench.py uses the measured
+columns only when the stamp's library is the one it loaded.
 """
+import hashlib
+import os
 import collections
 import csv
 import json
@@ -47,6 +54,7 @@ CODES = {1 + 2 * i + j: f"{n}.{d}" for i, n in enumerate(STAGE_NAMES)
 CODES.update({40: "dp.bn_broadcast", 41: "dp.allreduce_wait"})
 FIRST = 1   # conv2.fwd: a new step
 N_SIMD = 256 * 4
+LONG_MS = 0.3   # dispatches shorter than this read a high clock (MI355X_MICROARCH.md, DVFS)
 BF16_PEAK = 2516.6e12   # dense bf16 MFMA: 1024 SIMD x 1024 FLOP/clk x 2.4 GHz
 F32_PEAK = 157.3e12
 SUMS = ("kernel_ms", "read_bytes", "fetch_bytes_x2", "write_bytes", "hbm_bytes",
@@ -107,6 +115,21 @@ def load_pmc(path):
     return [(n, g, (c, t)) for _, (n, g, c, t) in sorted(d.items())]
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "pcss-unet_amd", "nsm_amd", "libnsm.so")
+
+
+def lib_sha256(path=LIB):
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def stamp():
+    """What a profile summary was measured on: the library's sha256 and the git
+    head (env GIT_HEAD: the GPU box's copy of the tree has no .git)."""
+    return {"libnsm_sha256": lib_sha256(), "git_head": os.environ.get("GIT_HEAD")}
+
+
 def main():
     out_path, trace, pmcs = sys.argv[1], sys.argv[2], sys.argv[3:]
     res = collections.defaultdict(dict)
@@ -125,7 +148,14 @@ def main():
             for st, v in m.items():
                 res[st][cname] = v
         if "GRBM_GUI_ACTIVE" in names:
-            m, _ = mean_steps(att, lambda ps: sum(x[1] for x in ps))
+            # busy cycles / clock over the dispatches of >= LONG_MS only
+            for cname in ("SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"):
+                if cname in names:
+                    m, _ = mean_steps(att, lambda ps, c=cname: sum(x[0].get(c, 0.0) for x in ps
+                                                                   if x[1] >= LONG_MS))
+                    for st, v in m.items():
+                        res[st][cname + "_long"] = v
+            m, _ = mean_steps(att, lambda ps: sum(x[1] for x in ps if x[1] >= LONG_MS))
             prof_ms.update(m)
     stages = {}
     for st, r in res.items():
@@ -141,9 +171,9 @@ def main():
         rd = row.get("read_bytes", row.get("fetch_bytes_x2"))
         if rd is not None and "write_bytes" in row:
             row["hbm_bytes"] = rd + row["write_bytes"]
-        if r.get("SQ_VALU_MFMA_BUSY_CYCLES") is not None and r.get("GRBM_GUI_ACTIVE"):
-            row["mfma_busy_cycles"] = r["SQ_VALU_MFMA_BUSY_CYCLES"]
-            row["grbm"] = r["GRBM_GUI_ACTIVE"]
+        if r.get("SQ_VALU_MFMA_BUSY_CYCLES_long") and r.get("GRBM_GUI_ACTIVE_long"):
+            row["mfma_busy_cycles"] = r["SQ_VALU_MFMA_BUSY_CYCLES_long"]
+            row["grbm"] = r["GRBM_GUI_ACTIVE_long"]
             row["prof_ms"] = prof_ms.get(st, 0.0)
         for k, c in (("bf16_mfma_flops", "SQ_INSTS_VALU_MFMA_MOPS_BF16"),
                      ("f16_mfma_flops", "SQ_INSTS_VALU_MFMA_MOPS_F16"),
@@ -170,7 +200,7 @@ def main():
                                           + row.get("f32_mfma_flops", 0.0) / t / F32_PEAK, 4)
             row["bf16_mfma_tflops"] = round(row["bf16_mfma_flops"] / t / 1e12, 2)
         row["kernel_ms"] = round(row["kernel_ms"], 4)
-    doc = {"source": {"trace": trace, "pmc": pmcs}, "steps_averaged": nsteps,
+    doc = {"stamp": stamp(), "source": {"trace": trace, "pmc": pmcs}, "steps_averaged": nsteps,
            "counters": sorted(counters),
            "method": __doc__.split("Per stage", 1)[1].strip(), "stages": stages}
     json.dump(doc, open(out_path, "w"), indent=1)
