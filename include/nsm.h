@@ -218,11 +218,28 @@ int nsm_conv1x1_dgrad_bnbwd_h2(const void* dy2h, int M, int cop, const void* w2d
                                const float* mean, const float* invstd, const float* mask, int HW,
                                float slope, int mode, float* partial, const float* coef,
                                float* out, int ldo, const uint32_t* amax_dy2,
-                               const uint32_t* amax_w, uint32_t* amax_out, void* stream);
+                               const uint32_t* amax_w, uint32_t* amax_out, uint32_t* amax_k1dz,
+                               void* stream);
 size_t nsm_conv1x1_wgrad_h2_ws(int M, int cin_p, int cout_p);
+/* (amax_k1dz, modes 0 / 1, may be NULL: the slot receiving max|scale * dz|,
+ * nsm_bn_bwd_finalize's bound term for an h2 dY1 from nsm_bn_bwd_apply_h2) */
 int nsm_conv1x1_wgrad_h2(const void* dyh, const void* xh, int M, int cin_p, int cout_p, int cin,
                          int cout, float* dw, float* ws, size_t ws_floats, const uint32_t* amax_dy,
                          const uint32_t* amax_x, void* stream);
+/* The direct 3x3 convolution (conv2's, Cin < 64: Unetmodel.py:21) of the
+ * fp32 train step on h2 operands: nsm_conv3x3_h2 y = conv3x3(x) + bias (pad 1)
+ * from xh [B*H*W][2 cin_p] (nsm_input_prep_h2; for the input gradient the h2
+ * dY1 with the DGRAD pack and bias NULL), wh the prep-kind-5 pack [cout_p][9]
+ * [2 cin_p], stats = BN partials of nsm_conv3x3_h2_rows(M, cout_p) rows;
+ * nsm_conv3x3_wgrad_h2 dw [cout][cin][3][3] from the h2 dY and X (cout_p 32). */
+int nsm_conv3x3_h2_rows(int M, int N);
+int nsm_conv3x3_h2(const void* xh, int B, int H, int W, int cin_p, const void* wh,
+                   const float* bias, int cout_p, float* y, int ldy, float* stats,
+                   const uint32_t* amax_x, const uint32_t* amax_w, void* stream);
+size_t nsm_conv3x3_wgrad_h2_ws(int B, int H, int W, int cin_p, int cout_p);
+int nsm_conv3x3_wgrad_h2(const void* dyh, const void* xh, int B, int H, int W, int cin_p,
+                         int cout_p, int cin, int cout, float* dw, float* ws, size_t ws_floats,
+                         const uint32_t* amax_dy, const uint32_t* amax_x, void* stream);
 /* fp32 GEMM arithmetic of every fp32 convolution (the batched GEMMs of
  * nsm_wino_gemm / nsm_conv3x3_wino, the weight gradient of
  * nsm_conv3x3_wgrad_wino, the direct implicit GEMMs): 2 (default, env
@@ -429,6 +446,11 @@ int nsm_up2_resize_bwd_bnred(const void* dy, int B, int h, int w, int C, void* d
 int nsm_input_prep(const float* x, int B, int C, int H, int W, void* out, int cp, int dtype,
                    uint32_t* amax, void* stream);
 /* (amax: fp32, may be NULL — max|out|, conv2's f16x2 operand scale) */
+/* nsm_input_prep (fp32) writing X as an h2 tensor [B*H/2*W/2][2 cp]: its
+ * scale source `amax` (zeroed by the caller) is first filled with max|x| over
+ * the whole input by this call (X holds the same values) */
+int nsm_input_prep_h2(const float* x, int B, int C, int H, int W, void* out, int cp, uint32_t* amax,
+                      void* stream);
 int nsm_input_grad(const void* dX, int B, int C, int H, int W, int cp, float* dx, int dtype,
                    void* stream);
 /* conv10 1x1 16->4 + pixel_shuffle(2) + sigmoid (Unetmodel.py:63,143-148) */

@@ -499,6 +499,7 @@ struct BnBwdEpiP {
   float* partial;  // [nchunk][2][N]
   int mode;
   uint32_t* amax = nullptr;  // mode 2 (fp32): max|dy| written (an h2 scale source)
+  uint32_t* k1dz = nullptr;  // modes 0/1 (fp32): max|scale * dz| (the dy bound's k1 term)
 };
 
 __device__ __forceinline__ f32x4 lrelu_grad_v4(f32x4 z, float slope) {
@@ -517,6 +518,28 @@ __device__ __forceinline__ f32x4 shfl_xor_v4(f32x4 v, int o) {
 // the epilogue adds no register pressure to the GEMM loop.
 struct EpiBnBwd {
   using P = BnBwdEpiP;
+  // Y1 rows of the wave tile, loaded before the GEMM's K loop (gemm_h2_kernel:
+  // with the short K of most 1x1 input gradients the epilogue's Y1 read is the
+  // kernel's main traffic; issued first, it overlaps the operand DMA instead of
+  // following the MFMAs). Lane layout of apply's loop: one 4-column group
+  // (lane % CPR) per lane, rows (it * 64 + lane) / CPR.
+  template <int TM, int TN>
+  struct PreT {
+    static constexpr int NIT = TM * 32 * (TN * 32 / 4) / 64;
+    f32x4 yv[NIT];
+  };
+  template <int TM, int TN, int WM, int WN>
+  __device__ static void prefetch(const P& e, PreT<TM, TN>& pre, int mb, int nb, int lane, int M,
+                                  int N) {
+    constexpr int CPR = TN * 32 / 4;
+    const int n = nb + (lane % CPR) * 4, nc = n < N ? n : 0;
+    const float* __restrict__ Y = (const float*)e.y;
+#pragma unroll
+    for (int it = 0; it < PreT<TM, TN>::NIT; ++it) {
+      const int m = min(mb + (it * 64 + lane) / CPR, M - 1);
+      pre.yv[it] = *(const f32x4*)(Y + (size_t)m * e.ldy + nc);
+    }
+  }
   // LDS of the h2 GEMMs' epilogue (gemm_h2_kernel): the staged wave tiles, then
   // the [WM][2][BNT] partial rows
   template <int TM, int TN, int WM, int WN>
@@ -527,6 +550,16 @@ struct EpiBnBwd {
   template <int TM, int TN, int WM, int WN>
   __device__ static void apply(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M, int N,
                                int) {
+    apply_impl<TM, TN, WM, WN>(e, acc, cx, M, N, nullptr);
+  }
+  template <int TM, int TN, int WM, int WN>
+  __device__ static void apply_pre(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M,
+                                   int N, const PreT<TM, TN>& pre) {
+    apply_impl<TM, TN, WM, WN>(e, acc, cx, M, N, &pre);
+  }
+  template <int TM, int TN, int WM, int WN>
+  __device__ static void apply_impl(const P& e, f32x16 (&acc)[TM][TN], const EpiCtx& cx, int M,
+                                    int N, const PreT<TM, TN>* pre) {
     const int col = cx.lane & 31, h = cx.lane >> 5;
     constexpr int BNT = WN * TN * 32, WR = TM * 32, WC = TN * 32, WCP = WC + 4;
     constexpr int CPR = WC / 4;  // 16-B chunks per row
@@ -554,8 +587,12 @@ struct EpiBnBwd {
     f32x4 yv[NIT];
 #pragma unroll
     for (int it = 0; it < NIT; ++it) {
-      const int m = min(cx.mb + (it * 64 + cx.lane) / CPR, M - 1);
-      yv[it] = *(const f32x4*)(Y + (size_t)m * e.ldy + nc);
+      if (pre) {
+        yv[it] = pre->yv[it];
+      } else {
+        const int m = min(cx.mb + (it * 64 + cx.lane) / CPR, M - 1);
+        yv[it] = *(const f32x4*)(Y + (size_t)m * e.ldy + nc);
+      }
     }
     const f32x4 sc = *(const f32x4*)(e.scale + nc), sh = *(const f32x4*)(e.shift + nc),
                 mu = *(const f32x4*)(e.mean + nc);
@@ -583,12 +620,14 @@ struct EpiBnBwd {
         s1 += dz;
         s2 += dz * ((v - mu) * is);
         if (e.mode == 1) *(f32x4*)(O + (size_t)m * e.ldo + n) = g;
+        if (e.k1dz) amax_fold(am, sc * dz);
       }
     }
     if (!red) {
       amax_flush(am, e.amax);
       return;
     }
+    amax_flush(am, e.k1dz);
 #pragma unroll
     for (int o = CPR; o < 64; o <<= 1) {
       s1 += shfl_xor_v4(s1, o);

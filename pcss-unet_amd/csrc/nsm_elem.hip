@@ -1504,13 +1504,17 @@ static bool sep_resize() {
 // thread per output pixel: each group of 8 output channels = 2 input planes x
 // 2 rows x 2 columns (channel 4c + 2i + j, F.pixel_unshuffle), read as float2
 // pairs coalesced along x and written as one 16-B (bf16) / 32-B (fp32) vector
-template <typename T>
+// H2: out is an h2 tensor [npix][2 cp] scaled from the slot `amax` holds
+// (max|x|, filled beforehand), T = bf16_t (16-bit storage)
+template <typename T, bool H2 = false>
 __global__ void __launch_bounds__(256) input_prep_kernel(const float* __restrict__ x, int B, int C,
                                                          int H, int W, T* __restrict__ out, int cp,
                                                          uint32_t npix, FastDiv fdRw, FastDiv fdRh,
                                                          uint32_t* __restrict__ amax) {
   const int Rh = H / 2, Rw = W / 2;
   const size_t plane = (size_t)H * W;
+  float hs = 0.f;
+  if constexpr (H2) hs = exp2i(h2_exp(H2Scale{amax, 1.f}));
   uint32_t am = 0;  // max|out| (conv2's f16x2 operand scale)
   for (uint32_t p = blockIdx.x * 256u + threadIdx.x; p < npix; p += gridDim.x * 256u) {
     const uint32_t t = fdiv(p, fdRw);
@@ -1526,14 +1530,18 @@ __global__ void __launch_bounds__(256) input_prep_kernel(const float* __restrict
         r[q] = c < C ? *(const f32x2*)(src + (size_t)c * plane + (q & 1) * W) : f32x2{0.f, 0.f};
       }
       const F8 v{f32x4{r[0].x, r[0].y, r[1].x, r[1].y}, f32x4{r[2].x, r[2].y, r[3].x, r[3].y}};
-      st8(out + (size_t)p * cp + 8 * g, v);
-      if (amax) {
-        amax_fold(am, v.a);
-        amax_fold(am, v.b);
+      if constexpr (H2) {
+        h2_store8((bf16_t*)out + (size_t)p * 2 * cp, 8 * g, v, hs);
+      } else {
+        st8(out + (size_t)p * cp + 8 * g, v);
+        if (amax) {
+          amax_fold(am, v.a);
+          amax_fold(am, v.b);
+        }
       }
     }
   }
-  amax_flush(am, amax);
+  if constexpr (!H2) amax_flush(am, amax);
 }
 
 template <typename T>
@@ -2474,6 +2482,23 @@ extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, void* 
     hipLaunchKernelGGL(input_prep_kernel<float>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
                        NSM_T(float, out), cp, (uint32_t)npix, fw, fh, amax);
   NSM_LAUNCH_CHECK("input_prep");
+  return 0;
+}
+
+extern "C" int nsm_input_prep_h2(const float* x, int B, int C, int H, int W, void* out, int cp,
+                                 uint32_t* amax, void* stream) {
+  NSM_CHECK_ARG(x && out && amax && H % 2 == 0 && W % 2 == 0 && cp >= 4 * C && cp % 8 == 0,
+                "input_prep_h2: bad args");
+  NSM_CHECK_ARG(((uintptr_t)x % 8) == 0 && ((uintptr_t)out % 16) == 0, "input_prep_h2: alignment");
+  const long long npix = (long long)B * (H / 2) * (W / 2);
+  NSM_CHECK_ARG(npix < (1ll << 31), "input_prep_h2: too large");
+  const int rc = nsm_absmax(x, (int64_t)B * C * H * W, amax, stream);  // the scale source
+  if (rc) return rc;
+  dim3 g(grid_for(npix, 256, 2048));
+  hipLaunchKernelGGL((input_prep_kernel<bf16_t, true>), g, dim3(256), 0, as_stream(stream), x, B, C,
+                     H, W, (bf16_t*)out, cp, (uint32_t)npix, make_fastdiv(W / 2),
+                     make_fastdiv(H / 2), amax);
+  NSM_LAUNCH_CHECK("input_prep_h2");
   return 0;
 }
 

@@ -57,7 +57,12 @@ _SIGS = {
     "nsm_conv1x1_h2_rows": (I, [I, I, I, I]),
     "nsm_conv1x1_h2": (I, [P, I, I, P, P, I, P, I, P, P, P, P]),
     "nsm_conv1x1_dgrad_bnbwd_h2": (I, [P, I, I, P, I, P, I, P, P, P, P, P, I, F, I, P, P, P, I, P,
-                                       P, P, P]),
+                                       P, P, P, P]),
+    "nsm_conv3x3_h2_rows": (I, [I, I]),
+    "nsm_conv3x3_h2": (I, [P, I, I, I, I, P, P, I, P, I, P, P, P, P]),
+    "nsm_conv3x3_wgrad_h2_ws": (Z, [I, I, I, I, I]),
+    "nsm_conv3x3_wgrad_h2": (I, [P, P, I, I, I, I, I, I, I, P, P, Z, P, P, P]),
+    "nsm_input_prep_h2": (I, [P, I, I, I, I, P, I, P, P]),
     "nsm_conv1x1_wgrad_h2_ws": (Z, [I, I, I]),
     "nsm_conv1x1_wgrad_h2": (I, [P, P, I, I, I, I, I, P, P, Z, P, P, P]),
     "nsm_bn_partials_merge": (I, [P, I, I, I, I, I, P, P]),

@@ -726,10 +726,16 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
 
 
 def conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2dh, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
-                            recompute, slope=0.2, tag=None, amax=(None, None), amax_out=None):
+                            recompute, slope=0.2, tag=None, amax=(None, None), amax_out=None,
+                            h2_out=None):
     """conv1x1_dgrad_bn_bwd on h2 operands (nsm_conv1x1_dgrad_bnbwd_h2): dY2h
-    [M, 2 cop] (to_h2 of dY2), w2dh the DGRAD h2 pack; amax = (scale source of
-    dY2h, of w2dh). HW: pixels per image (the Dropout2d mask row)."""
+    [M, 2 cop] (bn_bwd(h2=...)), w2dh the DGRAD h2 pack; amax = (scale source
+    of dY2h, of w2dh). HW: pixels per image (the Dropout2d mask row).
+    h2_out=(k1dz slot, bound slot), zeroed (recompute=False only): dY1 is
+    returned as an h2 tensor (nsm_bn_bwd_apply_h2) for the direct 3x3's h2
+    gradients."""
+    assert h2_out is None or not recompute
+    k1dz, bound = h2_out if h2_out is not None else (None, None)
     from ._lib import lib
     M, cop2 = dY2h.shape
     C = y.shape[1]
@@ -741,7 +747,8 @@ def conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2dh, y, st, mask, c_real, dgamma, dbeta, 
             ptr(st.shift), ptr(st.mean), ptr(st.invstd), ptr(mask), HW, slope)
     ev = _probe(tag)
     call("nsm_conv1x1_dgrad_bnbwd_h2", *args, 0 if recompute else 1, ptr(partial), None, ptr(dA1),
-         dA1.stride(0) if dA1 is not None else 0, ptr(amax[0]), ptr(amax[1]), None, stream())
+         dA1.stride(0) if dA1 is not None else 0, ptr(amax[0]), ptr(amax[1]), None, ptr(k1dz),
+         stream())
     if nchunk > SUM_ROWS_ABOVE:
         G = -(-nchunk // SUM_ROWS_ABOVE)
         n2 = -(-nchunk // G)
@@ -750,11 +757,19 @@ def conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2dh, y, st, mask, c_real, dgamma, dbeta, 
         partial, nchunk = buf, n2
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
-         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), None, None, stream())
+         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), ptr(k1dz), ptr(bound), stream())
+    if h2_out is not None:
+        dyh = torch.empty(M, 2 * C, dtype=H2, device=y.device)
+        call("nsm_bn_bwd_apply_h2", ptr(dA1), dA1.stride(0), ptr(y), y.stride(0), M, C, HW,
+             ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dyh),
+             ptr(bound), stream())
+        if ev is not None:
+            ev.record()
+        return dyh
     dy = like(M, C, y)
     if recompute:
         call("nsm_conv1x1_dgrad_bnbwd_h2", *args, 2, None, ptr(coef), ptr(dy), dy.stride(0),
-             ptr(amax[0]), ptr(amax[1]), ptr(amax_out), stream())
+             ptr(amax[0]), ptr(amax[1]), ptr(amax_out), None, stream())
     else:
         call("nsm_bn_bwd_apply", ptr(dA1), dA1.stride(0), ptr(y), y.stride(0), M, C, HW,
              ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy),
@@ -900,6 +915,50 @@ def input_prep(x, cp, dtype=F32, amax=None):
     call("nsm_input_prep", ptr(x), B, C, H, W, ptr(out), cp, dt(out),
          ptr(amax) if dtype == F32 else None, stream())
     return out
+
+
+def input_prep_h2(x, cp, amax):
+    """input_prep written as an h2 tensor [B*H/2*W/2, 2 cp] (nsm_input_prep_h2);
+    amax: a zeroed slot the call fills with max|x|, its scale source."""
+    B, C, H, W = x.shape
+    out = torch.empty(B * (H // 2) * (W // 2), 2 * cp, dtype=H2, device=x.device)
+    call("nsm_input_prep_h2", ptr(x), B, C, H, W, ptr(out), cp, ptr(amax), stream())
+    return out
+
+
+def conv3x3_h2(xh, B, H, W, wh, bias, cout_p, stats=True, amax=(None, None), tag=None):
+    """Direct 3x3 conv (pad 1) on h2 operands (nsm_conv3x3_h2): xh [B*H*W,
+    2 cin_p], wh a kind-5 3x3 pack (FWD; DGRAD with bias None for the input
+    gradient); amax = (scale source of xh, of wh). Returns (y fp32, Partials|None)."""
+    from ._lib import lib
+    M, cin2 = xh.shape
+    assert xh.dtype == H2 and wh.dtype == H2 and M == B * H * W
+    y = empty(M, cout_p, device=xh.device)
+    part = None
+    if stats:
+        rpc = int(lib.nsm_conv3x3_h2_rows(M, cout_p))
+        part = Partials(empty(-(-M // rpc) * 2 * cout_p, device=xh.device), -(-M // rpc), rpc)
+    ev = _probe(tag)
+    call("nsm_conv3x3_h2", ptr(xh), B, H, W, cin2 // 2, ptr(wh), ptr(bias), cout_p, ptr(y),
+         y.stride(0), ptr(part.buf) if part is not None else None, ptr(amax[0]), ptr(amax[1]),
+         stream())
+    if ev is not None:
+        ev.record()
+    return y, part
+
+
+def conv3x3_wgrad_h2(dyh, xh, B, H, W, cin, cout, dw, amax=(None, None), tag=None):
+    """dw [cout, cin, 3, 3] of a direct 3x3 conv from its h2 output gradient and
+    h2 input (nsm_conv3x3_wgrad_h2); amax = (scale source of dyh, of xh)."""
+    from ._lib import lib
+    cin_p, cout_p = xh.shape[1] // 2, dyh.shape[1] // 2
+    n = int(lib.nsm_conv3x3_wgrad_h2_ws(B, H, W, cin_p, cout_p))
+    ws = empty(max(n, 1), device=dyh.device)
+    ev = _probe(tag)
+    call("nsm_conv3x3_wgrad_h2", ptr(dyh), ptr(xh), B, H, W, cin_p, cout_p, cin, cout, ptr(dw),
+         ptr(ws), n, ptr(amax[0]), ptr(amax[1]), stream())
+    if ev is not None:
+        ev.record()
 
 
 def input_grad(dX, B, C, H, W):

@@ -178,14 +178,25 @@ class StepWeights:
                                                  c0.weight, (tile + 2) ** 2 * cip * cip,
                                                  torch.float32, amax=am)
             else:
+                # the direct 3x3 (conv2) of the fp32 train step on h2 operands:
+                # kind-5 packs, the DGRAD job sharing the FWD job's max|w| slot
+                h2_3x3 = h2 and training and H2_1X1
                 for mode in modes:
                     am = None
-                    if dtype == torch.float32:
+                    if h2_3x3 and mode != ops.PACK_FWD:
+                        am = pb.t[("amaxw1", ops.PACK_FWD)]
+                    elif dtype == torch.float32:
                         am = ops.amax_slot(self.amax, n_am)
                         n_am += 1
+                    if am is not None:
                         pb.t[("amaxw1", mode)] = am
-                    pb.t[("w1", mode)] = add(pk, (ci, ci, 9, cip, cip, mode), c0.weight,
-                                             cip * 9 * cip, dtype, amax=am)
+                    if h2_3x3:
+                        pb.t[("w1", mode)] = add(KIND_PACK_H2, (ci, ci, 9, cip, cip, mode,
+                                                                int(mode != ops.PACK_FWD)),
+                                                 c0.weight, 2 * cip * 9 * cip, ops.H2, amax=am)
+                    else:
+                        pb.t[("w1", mode)] = add(pk, (ci, ci, 9, cip, cip, mode), c0.weight,
+                                                 cip * 9 * cip, dtype, amax=am)
             h2_1x1 = h2 and training and H2_1X1
             for mode in modes:
                 am = None

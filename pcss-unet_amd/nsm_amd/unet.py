@@ -436,7 +436,10 @@ class _BlockSaved:
 # (h2 1x1 operands: AM_A1 holds the bound of A1 from its BN finalize, AM_K1DZ
 # max|k1 dz| of the output BN's backward, AM_DY2B the bound of dY2 derived from it)
 AM_V, AM_VD, AM_DM, AM_A1, AM_DY2, AM_X, AM_DY1, AM_K1DZ, AM_DY2B = range(9)
-AM_PER_BLOCK = 9
+# (the direct 3x3 on h2 operands: AM_K1DZ1 max|k1 dz| of the first BN's
+# backward, AM_DY1B the bound of the h2 dY1 derived from it)
+AM_K1DZ1, AM_DY1B = 9, 10
+AM_PER_BLOCK = 11
 
 
 def _slot(am, i):
@@ -512,7 +515,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     cip, cop = ops.pad32(ci), ops.pad32(co)
     xin = X if src is None else src[0]
     src_hw = None if src is None else (src[1], src[2])
-    assert xin.shape[1] == cip, (xin.shape, cip)
+    assert xin.shape[1] == (2 * cip if xin.dtype == ops.H2 else cip), (xin.shape, cip)
     assert src is None or fuses_resize(blk, xin.dtype)
     dtype = xin.dtype
     if pw is None:
@@ -541,9 +544,15 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
             part1 = ops.bn_partials(Y1)
     else:
         w1 = pw.w1(ops.PACK_FWD)
-        Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd",
-                                    stats=training,
-                                    amax=(_slot(am, AM_X), pw.amax_w1(ops.PACK_FWD)))
+        if w1.dtype == ops.H2:   # h2 operands (X from input_prep_h2; csrc/nsm_conv_h2d.inc)
+            assert X.dtype == ops.H2
+            Y1, part1 = ops.conv3x3_h2(X, B, H, W, w1, b1, cip, stats=training,
+                                       amax=(_slot(am, AM_X), pw.amax_w1(ops.PACK_FWD)),
+                                       tag=name + ".conv.0.fwd")
+        else:
+            Y1, part1 = ops.conv_fwd_bn(X, B, H, W, w1, b1, cip, 3, tag=name + ".conv.0.fwd",
+                                        stats=training,
+                                        amax=(_slot(am, AM_X), pw.amax_w1(ops.PACK_FWD)))
     eps1, eps2 = bn1m.eps, bn2m.eps
     w2 = pw.w2(ops.PACK_FWD)
     b2 = pw.vec("b2")
@@ -610,12 +619,18 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         ops.conv1x1_wgrad_h2(dY2h, s.A1, ci, co, g[c4.weight], amax=(am_dy2, _slot(s.am, AM_A1)),
                              tag=name + ".conv.4.wgrad")
         s.A1 = None
+        recompute = bnb_mode(s.cip, s.cop, dtype, h2=True) == 2
+        # a direct 3x3 on h2 operands (conv2) takes dY1 as h2 too, written by
+        # the BN backward with the bound its finalize derives (AM_DY1B)
+        h2_3x3 = s.X is not None and s.X.dtype == ops.H2 and not recompute
+        if h2_3x3:
+            am_dy1 = _slot(s.am, AM_DY1B)
         dY1 = ops.conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
-                                          g[bn1m.bias], g[c0.bias],
-                                          bnb_mode(s.cip, s.cop, dtype, h2=True) == 2,
+                                          g[bn1m.bias], g[c0.bias], recompute,
                                           tag=name + ".conv.4.dgrad",
                                           amax=(am_dy2, s.pw.amax_w2(ops.PACK_DGRAD)),
-                                          amax_out=am_dy1)
+                                          amax_out=None if h2_3x3 else am_dy1,
+                                          h2_out=(_slot(s.am, AM_K1DZ1), am_dy1) if h2_3x3 else None)
         return _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1)
     dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias],
                      part=gpart, amax=_slot(s.am, AM_DY2))
@@ -683,6 +698,15 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
                                tag=name + ".conv.0.wgrad", dM=dM,
                                amax=(_slot(s.am, AM_DM), _slot(s.am, AM_V)))
         s.V = None
+    elif s.X.dtype == ops.H2:   # direct 3x3 on h2 operands (dY1 from the BN backward)
+        assert dY1.dtype == ops.H2
+        ops.conv3x3_wgrad_h2(dY1, s.X, B, H, W, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad",
+                             amax=(am_dy1, _slot(s.am, AM_X)))
+        if not need_dx:
+            return None
+        return ops.conv3x3_h2(dY1, B, H, W, s.pw.w1(ops.PACK_DGRAD), None, s.cip, stats=False,
+                              amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)),
+                              tag=name + ".conv.0.dgrad")[0]
     else:
         ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad",
                        amax=(am_dy1, _slot(s.am, AM_X)))
@@ -762,7 +786,13 @@ class _UnetFn(torch.autograd.Function):
         # per-step maxima of the f16x2 GEMM operands of every block (their
         # producers fill them; zeroed here, one launch)
         amax = ops.amax_slots(AM_PER_BLOCK * 10, dev) if sw else None
-        X = ops.input_prep(x32, cin_p, cdt, amax=_x_slot(amax, 2))
+        w1_2 = sw.block(2).w1(ops.PACK_FWD) if sw and ops.pad32(
+            mod.conv2.conv[0].in_channels) < WINOGRAD_MIN_CHANNELS else None
+        if w1_2 is not None and w1_2.dtype == ops.H2:
+            # conv2's direct 3x3 on h2 operands: X pre-split, scaled from max|x|
+            X = ops.input_prep_h2(x32, cin_p, _x_slot(amax, 2))
+        else:
+            X = ops.input_prep(x32, cin_p, cdt, amax=_x_slot(amax, 2))
 
         saved, c, shapes = {}, {}, {}
         inp, h, w = X, Rh, Rw

@@ -287,3 +287,68 @@ def test_bn_bwd_h2_bound(ops, device, fused):
     dec = (h[:, :, 0, :] + h[:, :, 1, :]).reshape(M, C) * 2.0 ** (-e)
     err = (dec - d32).abs()
     assert (err <= d32.abs() * 2.0 ** -21 + 2.0 ** (-25 - e)).all()
+
+
+@pytest.mark.parametrize("B,H,W,cin_p,cout_p", [(8, 64, 64, 32, 32), (2, 33, 47, 64, 32),
+                                                (4, 40, 24, 32, 64)])
+def test_conv3x3_h2(ops, device, B, H, W, cin_p, cout_p):
+    """The direct 3x3 (conv2's) on h2 operands: forward with BN partials, the
+    input gradient (DGRAD pack), the weight gradient (cout_p 32) vs float64,
+    within the fp32 MFMA path's error; X through nsm_input_prep_h2 (scale =
+    max|x| its own pass records)."""
+    import torch.nn.functional as F
+    g = torch.Generator().manual_seed(B * H + W + cin_p)
+    C = cin_p // 4
+    xin = torch.randn(B, C, 2 * H, 2 * W, generator=g, dtype=torch.float64) * \
+        _spread(g, C, -6, 0).view(1, C, 1, 1)
+    w = torch.randn(cout_p, cin_p, 3, 3, generator=g, dtype=torch.float64) / (9 * cin_p) ** 0.5
+    b = torch.randn(cout_p, generator=g, dtype=torch.float64) * 0.1
+    dy = torch.randn(B, cout_p, H, W, generator=g, dtype=torch.float64)
+    xin, w, b, dy = (t.to(device) for t in (xin, w, b, dy))
+    x = torch.nn.functional.pixel_unshuffle(xin, 2)               # [B, cin_p, H, W]
+    x.requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    ref = F.conv2d(x, wr, b, padding=1)
+    ref.backward(dy)
+    nh = lambda t: t.permute(0, 2, 3, 1).reshape(-1, t.shape[1]).contiguous()  # noqa: E731
+    am = ops.amax_slots(4, device)
+    ax, aw, awd, ady = (ops.amax_slot(am, i) for i in range(4))
+    xh = ops.input_prep_h2(xin.float().contiguous(), cin_p, ax)
+    ws = w.float().contiguous()
+    wf = ops.pack_conv_weight(ws, cout_p, cin_p, ops.PACK_FWD)
+    wd = ops.pack_conv_weight(ws, cout_p, cin_p, ops.PACK_DGRAD)
+    ops.absmax(wf, aw)
+    ops.absmax(wd, awd)
+    dys = nh(dy).float()
+    ops.absmax(dys, ady)
+    y, part = ops.conv3x3_h2(xh, B, H, W, ops.to_h2(wf.view(cout_p, -1), aw), b.float(), cout_p,
+                             amax=(ax, aw))
+    dyh = ops.to_h2(dys, ady)
+    dx, _ = ops.conv3x3_h2(dyh, B, H, W, ops.to_h2(wd.view(cin_p, -1), awd), None, cin_p,
+                           stats=False, amax=(ady, awd))
+    outs = {"h2": (y, dx)}
+    if cout_p == 32:
+        dw = torch.empty(cout_p, cin_p, 3, 3, device=device)
+        ops.conv3x3_wgrad_h2(dyh, xh, B, H, W, cin_p, cout_p, dw, amax=(ady, ax))
+        outs["h2"] += (dw,)
+    prev = ops.set_f32_split(0)
+    try:
+        xs = nh(x.detach()).float()
+        y0 = ops.conv_fwd(xs, B, H, W, wf, b.float(), cout_p, 3)
+        dx0 = ops.conv_fwd(dys, B, H, W, wd, None, cin_p, 3)
+        outs["fp32"] = (y0, dx0)
+        if cout_p == 32:
+            dw0 = torch.empty_like(dw)
+            ops.conv_wgrad(dys, xs, B, H, W, 3, cin_p, cout_p, dw0)
+            outs["fp32"] += (dw0,)
+    finally:
+        ops.set_f32_split(prev)
+    torch.cuda.synchronize()
+    refs = (nh(ref.detach()), nh(x.grad), wr.grad)
+    for got, base, r in zip(outs["h2"], outs["fp32"], refs):
+        (mx, rms), (mx0, rms0) = _errs(got.reshape(r.shape), r), _errs(base.reshape(r.shape), r)
+        assert rms <= 1.5 * rms0 + 1e-12 and mx <= 2.0 * mx0 + 1e-12, (mx, rms, mx0, rms0)
+    bn = torch.nn.BatchNorm2d(cout_p).to(device)
+    st = ops.bn_train(y, bn, cout_p, 0.1, 1e-5, part=part)
+    yr = nh(ref.detach())
+    torch.testing.assert_close(st.mean.double(), yr.mean(0), rtol=1e-5, atol=1e-6)
