@@ -182,6 +182,16 @@ int nsm_wino_input_h2(const float* x, int ldx, int B, int hi, int wi, int H, int
  * max|dy| (its producer's), betas wino_beta(tile, 0) and (tile, 1) */
 int nsm_wino_dual_input_h2(const float* dy, int lddy, int B, int H, int W, int c_p, int tile,
                            void* Vh, void* dMh, const uint32_t* amax_dy, void* stream);
+/* nsm_wino_dual_input_h2 of a deferred BN backward (nsm_wino_dual_input_bn's
+ * operands: g = dA1, y = Y1, the finalize coefficients): dY1 is formed per patch
+ * element, never stored; bound: the dY1 bound nsm_bn_bwd_finalize derived from
+ * max|k1 dz| — the scale source of Vh / dMh and of the GEMMs reading them.
+ * Replaces the BN-backward apply + transform of the reference's autograd
+ * backward through Unetmodel.py:21-24 (DoubleConv conv.0 -> BN -> LeakyReLU). */
+int nsm_wino_dual_input_bn_h2(const float* g, int ldg, const float* y, int ldy, int B, int H, int W,
+                              int c_p, int tile, const float* scale, const float* shift,
+                              float slope, const float* mask, const float* mean, const float* coef,
+                              void* Vh, void* dMh, const uint32_t* bound, void* stream);
 /* the weight gradient of a Winograd conv from h2 dM (nsm_wino_dual_input_h2) and
  * h2 V (nsm_wino_input_h2): batched split-K GEMMs on the f16 matrix cores, then
  * the filter transform; ws >= nsm_wino_wgrad_h2_ws floats */

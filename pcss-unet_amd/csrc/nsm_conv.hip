@@ -1524,6 +1524,8 @@ struct WinoAct {
   int ldres;
 };
 
+// The column pass streams M's rows (wcol_row: wmat2's bits with one row
+// live): F(6x6) 138 -> 128 VGPRs, 3 -> 4 waves per SIMD
 template <int MT, bool STATS, bool ACT = false>
 __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
                                                           int W, int TH, int TW, long long T,
@@ -1547,12 +1549,16 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
     const long long b = r / TH;
     const size_t plane = (size_t)T * N;
     const float* in = Mb + (size_t)t * N + c;
-    VT m[A][A], o[MT][MT];
+    VT sc[MT][A], o[MT][MT];
 #pragma unroll
-    for (int a = 0; a < A; ++a)
+    for (int a = 0; a < A; ++a) {
+      VT row[A];
 #pragma unroll
-      for (int e = 0; e < A; ++e) m[a][e] = *(const VT*)(in + (a * A + e) * plane);
-    wmat2<CAt<MT>>(m, o);
+      for (int e = 0; e < A; ++e) row[e] = *(const VT*)(in + (a * A + e) * plane);
+      wcol_row<CAt<MT>>(sc, row, a);
+    }
+#pragma unroll
+    for (int a = 0; a < MT; ++a) wmat<CAt<MT>>(sc[a], o[a]);
     const VT bv = bias ? *(const VT*)(bias + c) : VT{};
     VT asc{}, ash{};
     if (ACT) {
@@ -1776,6 +1782,139 @@ __global__ void __launch_bounds__(256) wino_dual_kernel(const float* __restrict_
   }
 }
 
+// wino_dual_kernel<MT, BN=true, H2=true> through LDS: the per-thread form
+// loads every patch element of g and y itself — 2 x 64 4-B loads per thread
+// over patches that overlap 1.78x, each element's BN backward recomputed per
+// patch holding it — and is load-issue-bound (~230 us on conv7's dY1 beside
+// ~150 us for the separate apply). Here a block covers TYB x TXB tiles x 32
+// channels: its (m TYB + 2) x (m TXB + 2) pixel region of g and y is read once
+// with 16-B loads (8 lanes per pixel, coalesced), dY1 = k1 dz + k2 (y - mean)
+// + k3 formed once per element into LDS (zero outside the image: the dgrad's
+// padding), then each thread (tile, channel) reads its (m+2)^2 patch from LDS
+// and writes both transforms as h2, as wino_dual_kernel does.
+template <int MT, int TYB, int TXB>
+__global__ void __launch_bounds__(256) wino_dual_bn_lds_kernel(
+    const float* __restrict__ g, int ldg, int H, int W, int C, int TH, int TW, long long T,
+    WinoBnSrc bn, bf16_t* __restrict__ Vh, bf16_t* __restrict__ dMh, H2Scale hv, H2Scale hd) {
+  constexpr int A = MT + 2, CB = 32, RH = MT * TYB + 2, RW = MT * TXB + 2;
+  static_assert(TYB * TXB * CB == 256, "one (tile, channel) per thread");
+  __shared__ __attribute__((aligned(16))) float reg[RH * RW * CB];
+  const int tid = threadIdx.x;
+  const int txb = blockIdx.x % ((TW + TXB - 1) / TXB), tyb = blockIdx.x / ((TW + TXB - 1) / TXB);
+  const int b = blockIdx.y / (C / CB), c0 = (blockIdx.y % (C / CB)) * CB;
+  const int ty0 = tyb * TYB, tx0 = txb * TXB;
+  // the scales before any lane leaves: amax_read reduces over all 64 lanes
+  const float hsv = exp2i(h2_exp(hv)), hsd = exp2i(h2_exp(hd));
+  {
+    // the region's rows: this lane's 4 channels are fixed (256 % 8 == 0)
+    const int cg = (tid & 7) * 4, c = c0 + cg;
+    const f32x4 sc = *(const f32x4*)(bn.scale + c), sh = *(const f32x4*)(bn.shift + c);
+    const f32x4 mu = *(const f32x4*)(bn.mean + c);
+    const f32x4 k1 = *(const f32x4*)(bn.coef + c), k2 = *(const f32x4*)(bn.coef + C + c);
+    const f32x4 k3 = *(const f32x4*)(bn.coef + 2 * C + c);
+    f32x4 mk = {1.f, 1.f, 1.f, 1.f};
+    if (bn.mask) mk = *(const f32x4*)(bn.mask + (size_t)b * C + c);
+    for (int p = tid >> 3; p < RH * RW; p += 32) {
+      const int py = p / RW, px = p - py * RW;
+      const int yy = MT * ty0 - 1 + py, xx = MT * tx0 - 1 + px;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+        const size_t q = (size_t)(b * H + yy) * W + xx;
+        const f32x4 gv = *(const f32x4*)(g + q * ldg + c);
+        const f32x4 yv = *(const f32x4*)(bn.y + q * bn.ldy + c);
+        f32x4 dz = gv * vlrelu_grad(yv * sc + sh, bn.slope);
+        if (bn.mask) dz = dz * mk;
+        v = k1 * dz + k2 * (yv - mu) + k3;
+      }
+      *(f32x4*)&reg[p * CB + cg] = v;
+    }
+  }
+  __syncthreads();
+  const int cl = tid & (CB - 1), tl = tid / CB;
+  const int ty = ty0 + tl / TXB, tx = tx0 + tl % TXB;
+  if (ty >= TH || tx >= TW) return;  // (no barrier follows)
+  const long long t = ((long long)b * TH + ty) * TW + tx;
+  const int c = c0 + cl;
+  const float* pr = reg + ((tl / TXB) * MT * RW + (tl % TXB) * MT) * CB + cl;
+  float d[A][A];
+#pragma unroll
+  for (int a = 0; a < A; ++a)
+#pragma unroll
+    for (int e = 0; e < A; ++e) d[a][e] = pr[(a * RW + e) * CB];
+  {
+    float v[A][A];
+    wmat2<CBt<MT>>(d, v);
+    h2_write<A>(Vh, T, C, t, c, v, hsv);
+  }
+  float gi[MT][MT], sm[A][A];
+#pragma unroll
+  for (int a = 0; a < MT; ++a)
+#pragma unroll
+    for (int e = 0; e < MT; ++e) gi[a][e] = d[a + 1][e + 1];
+  wmat2<CA<MT>>(gi, sm);
+  h2_write<A>(dMh, T, C, t, c, sm, hsd);
+}
+
+// wino_input_kernel<MT, RELU=false, UP, H2=true> through LDS, in the layout of
+// wino_dual_bn_lds_kernel: a block's (m TYB + 2) x (m TXB + 2) pixel region x
+// 32 channels is formed once — read with 16-B loads, or (UP) sampled from the
+// low-resolution source with the bilinear align_corners weights of
+// nsm_resize_fwd, once per pixel instead of once per patch holding it — then
+// each thread (tile, channel) transforms its patch from LDS and writes V as
+// h2 (scale: max|x| of the source times beta, as nsm_wino_input_h2).
+template <int MT, int TYB, int TXB, bool UP>
+__global__ void __launch_bounds__(256) wino_input_lds_kernel(
+    const float* __restrict__ x, int ld, int H, int W, int C, int TH, int TW, long long T, int hi,
+    int wi, float sh, float sw, bf16_t* __restrict__ Vh, H2Scale hsc) {
+  constexpr int A = MT + 2, CB = 32, RH = MT * TYB + 2, RW = MT * TXB + 2;
+  static_assert(TYB * TXB * CB == 256, "one (tile, channel) per thread");
+  __shared__ __attribute__((aligned(16))) float reg[RH * RW * CB];
+  const int tid = threadIdx.x;
+  const int txb = blockIdx.x % ((TW + TXB - 1) / TXB), tyb = blockIdx.x / ((TW + TXB - 1) / TXB);
+  const int b = blockIdx.y / (C / CB), c0 = (blockIdx.y % (C / CB)) * CB;
+  const int ty0 = tyb * TYB, tx0 = txb * TXB;
+  const float hs = exp2i(h2_exp(hsc));  // before any lane leaves (amax_read: all 64 lanes)
+  {
+    const int c = c0 + (tid & 7) * 4;
+    for (int p = tid >> 3; p < RH * RW; p += 32) {
+      const int py = p / RW, px = p - py * RW;
+      const int yy = MT * ty0 - 1 + py, xx = MT * tx0 - 1 + px;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
+        if constexpr (UP) {
+          int y0, y1, x0, x1;
+          float ly0, ly1, lx0, lx1;
+          lin_idx(sh, yy, hi, y0, y1, ly0, ly1);
+          lin_idx(sw, xx, wi, x0, x1, lx0, lx1);
+          const float* r0 = x + ((size_t)b * hi + y0) * wi * ld + c;
+          const float* r1 = x + ((size_t)b * hi + y1) * wi * ld + c;
+          const f32x4 h0 = lx0 * *(const f32x4*)(r0 + (size_t)x0 * ld) +
+                           lx1 * *(const f32x4*)(r0 + (size_t)x1 * ld);
+          const f32x4 h1 = lx0 * *(const f32x4*)(r1 + (size_t)x0 * ld) +
+                           lx1 * *(const f32x4*)(r1 + (size_t)x1 * ld);
+          v = ly0 * h0 + ly1 * h1;
+        } else {
+          v = *(const f32x4*)(x + ((size_t)(b * H + yy) * W + xx) * ld + c);
+        }
+      }
+      *(f32x4*)&reg[p * CB + (tid & 7) * 4] = v;
+    }
+  }
+  __syncthreads();
+  const int cl = tid & (CB - 1), tl = tid / CB;
+  const int ty = ty0 + tl / TXB, tx = tx0 + tl % TXB;
+  if (ty >= TH || tx >= TW) return;  // (no barrier follows; lane pairs share a tile)
+  const long long t = ((long long)b * TH + ty) * TW + tx;
+  const float* pr = reg + ((tl / TXB) * MT * RW + (tl % TXB) * MT) * CB + cl;
+  float d[A][A], v[A][A];
+#pragma unroll
+  for (int a = 0; a < A; ++a)
+#pragma unroll
+    for (int e = 0; e < A; ++e) d[a][e] = pr[(a * RW + e) * CB];
+  wmat2<CBt<MT>>(d, v);
+  h2_write<A>(Vh, T, C, t, c0 + cl, v, hs);
+}
+
 // dst[b][i] = sum_s src[b][s][i] (float4 lanes, fixed order): the split-K
 // partials of a batched GEMM, one batch entry per grid.y
 __global__ void __launch_bounds__(256) batched_splitsum_kernel(const float* __restrict__ src,
@@ -1891,7 +2030,10 @@ __device__ __forceinline__ void wino_weight_item_h2(const float* __restrict__ w,
   h2_write<A>(U, n_p, k_p, n, k, u, s);
 }
 
-constexpr int PREP_ITEMS = 2048;  // items per block: 8 per thread
+#ifndef NSM_PREP_ITEMS
+#define NSM_PREP_ITEMS 512
+#endif
+constexpr int PREP_ITEMS = NSM_PREP_ITEMS;  // items per block, 2 per thread (8: -0.2 % step, more tail)
 
 // blockIdx -> job by a (uniform) binary search over the jobs' first blocks
 // (job.base / PREP_ITEMS: every job starts on a block boundary, see
@@ -2367,7 +2509,7 @@ static int wino_stat_step(int cout_p, int tile) {
 }
 // blocks of the statistics kernel resident at once on the device (every block
 // does the same grid-stride work, so a grid past one round leaves a tail:
-// F(6x6)'s 138 VGPRs hold 3 blocks per CU, i.e. 768 of a 1024-block grid)
+// F(6x6)'s 128 VGPRs hold 4 blocks per CU, i.e. 1024 blocks)
 static int wino_stat_resident(int tile) {
   static int cache[7] = {0, 0, 0, 0, 0, 0, 0};
   if (tile < 0 || tile > 6) return 1024;
@@ -2703,6 +2845,20 @@ extern "C" float nsm_wino_beta(int tile, int which) {
                                                                           : 0.f;
 }
 
+// NSM_WINO_IN_LDS=1: the F(6x6) h2 input transform on the LDS-region kernel
+// (wino_input_lds_kernel) instead of the per-thread one. Measured (B=8 step,
+// one box): conv7 170.6 -> 208.5 us, conv8 157.4 -> 189.0, conv6 81.8 ->
+// 100.6; step 723 -> 716 frames/s — off: the per-thread kernel's source-row
+// reuse already keeps its loads cheap, and the region phase serialises the
+// block's reads before its writes at 3 blocks per CU
+static bool wino_in_lds() {
+  static bool v = [] {
+    const char* e = getenv("NSM_WINO_IN_LDS");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 extern "C" int nsm_wino_input_h2(const float* x, int ldx, int B, int hi, int wi, int H, int W,
                                  int cin_p, int tile, void* Vh, const uint32_t* amax_x,
                                  void* stream) {
@@ -2717,6 +2873,17 @@ extern "C" int nsm_wino_input_h2(const float* x, int ldx, int B, int hi, int wi,
   const float sh = ac_scale(hi, H), sw = ac_scale(wi, W);
   const H2Scale sc{amax_x, wino_beta(tile, 0)};
   bf16_t* V = (bf16_t*)Vh;
+  if (tile == 6 && wino_in_lds() && B * (cin_p / 32) <= 65535) {
+    const dim3 grid2(ceil_div(g.TW, 4) * ceil_div(g.TH, 2), B * (cin_p / 32));
+    if (up)
+      hipLaunchKernelGGL((wino_input_lds_kernel<6, 2, 4, true>), grid2, dim3(256), 0, s, x, ldx, H, W,
+                         cin_p, g.TH, g.TW, g.T, hi, wi, sh, sw, V, sc);
+    else
+      hipLaunchKernelGGL((wino_input_lds_kernel<6, 2, 4, false>), grid2, dim3(256), 0, s, x, ldx, H,
+                         W, cin_p, g.TH, g.TW, g.T, hi, wi, sh, sw, V, sc);
+    NSM_LAUNCH_CHECK("wino_input_h2");
+    return 0;
+  }
   const bool uni = (cin_p / (tile == 6 ? 1 : 4)) % 64 == 0;
 #define NSM_WI(m, u, un)                                                                          \
   hipLaunchKernelGGL((wino_input_kernel<m, false, u, true, un>), grid, dim3(256), 0, s, x, ldx, H, \
@@ -2754,6 +2921,55 @@ extern "C" int nsm_wino_dual_input_h2(const float* dy, int lddy, int B, int H, i
   else hipLaunchKernelGGL((wino_dual_kernel<6, false, true>), grid, dim3(256), 0, s, A_);
 #undef A_
   NSM_LAUNCH_CHECK("wino_dual_input_h2");
+  return 0;
+}
+
+// NSM_DUAL_LDS=0: the F(6x6) BN-fused h2 dual transform on the per-thread
+// kernel (wino_dual_kernel) instead of the LDS-region one
+static bool dual_lds() {
+  static bool v = [] {
+    const char* e = getenv("NSM_DUAL_LDS");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
+// wino_dual_input_h2 of a BN backward whose apply pass was not run
+// (nsm_wino_dual_input_bn's operands): dY1 = k1 dz + k2 (y - mean) + k3 is
+// formed per patch element and never stored; the h2 scale source is `bound`,
+// the dY1 bound nsm_bn_bwd_finalize derives from max|k1 dz| (its amax_k1dz),
+// which the GEMMs reading Vd / dM take as their operand scale source too
+extern "C" int nsm_wino_dual_input_bn_h2(const float* g, int ldg, const float* y, int ldy, int B,
+                                         int H, int W, int c_p, int tile, const float* scale,
+                                         const float* shift, float slope, const float* mask,
+                                         const float* mean, const float* coef, void* Vh, void* dMh,
+                                         const uint32_t* bound, void* stream) {
+  NSM_CHECK_ARG(g && y && Vh && dMh && scale && shift && mean && coef && bound && c_p % 32 == 0 &&
+                    ldg % 4 == 0 && ldg >= c_p && ldy % 4 == 0 && ldy >= c_p,
+                "wino_dual_input_bn_h2: bad args");
+  NSM_CHECK_ARG(((uintptr_t)Vh % 16) == 0 && ((uintptr_t)dMh % 16) == 0,
+                "wino_dual_input_bn_h2: alignment");
+  WinoGeom geo;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, geo), "wino_dual_input_bn_h2: bad tile or shape");
+  dim3 grid(grid_1d(geo.T * c_p / (tile == 6 ? 1 : 4)));
+  hipStream_t s = as_stream(stream);
+  const WinoBnSrc bn{y, ldy, scale, shift, mean, coef, mask, slope};
+  const H2Scale hv{bound, wino_beta(tile, 0)}, hd{bound, wino_beta(tile, 1)};
+  if (tile == 6 && dual_lds()) {
+    NSM_CHECK_ARG(B * (c_p / 32) <= 65535, "wino_dual_input_bn_h2: grid");
+    const dim3 grid2(ceil_div(geo.TW, 4) * ceil_div(geo.TH, 2), B * (c_p / 32));
+    hipLaunchKernelGGL((wino_dual_bn_lds_kernel<6, 2, 4>), grid2, dim3(256), 0, s, g, ldg, H, W, c_p,
+                       geo.TH, geo.TW, geo.T, bn, (bf16_t*)Vh, (bf16_t*)dMh, hv, hd);
+    NSM_LAUNCH_CHECK("wino_dual_input_bn_h2");
+    return 0;
+  }
+#define A_ g, ldg, H, W, c_p, geo.TH, geo.TW, geo.T, nullptr, nullptr, bn, nullptr, nullptr, \
+           (bf16_t*)Vh, (bf16_t*)dMh, hv, hd
+  if (tile == 2) hipLaunchKernelGGL((wino_dual_kernel<2, true, true>), grid, dim3(256), 0, s, A_);
+  else if (tile == 4) hipLaunchKernelGGL((wino_dual_kernel<4, true, true>), grid, dim3(256), 0, s, A_);
+  else hipLaunchKernelGGL((wino_dual_kernel<6, true, true>), grid, dim3(256), 0, s, A_);
+#undef A_
+  NSM_LAUNCH_CHECK("wino_dual_input_bn_h2");
   return 0;
 }
 

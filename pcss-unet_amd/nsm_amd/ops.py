@@ -383,6 +383,21 @@ def wino_dual_input_bn(d, y, st, mask, B, H, W, tile=4, slope=0.2, amax=(None, N
     return Vd, dM
 
 
+def wino_dual_input_bn_h2(d, y, st, mask, B, H, W, tile, bound, slope=0.2):
+    """wino_dual_input_h2 of d = DeferredBnBwd(g, coef) (BN input y, state st,
+    mask [B][C] or None): dY is formed per element, never stored; bound: the dY
+    bound slot bn_bwd_finalize filled (the scale source of Vd, dM and their
+    GEMMs)."""
+    c_p = y.shape[1]
+    n = (tile + 2) ** 2 * wino_tiles(B, H, W, tile) * 2 * c_p
+    Vd = torch.empty(n, dtype=H2, device=y.device)
+    dM = torch.empty(n, dtype=H2, device=y.device)
+    call("nsm_wino_dual_input_bn_h2", ptr(d.g), d.g.stride(0), ptr(y), y.stride(0), B, H, W, c_p,
+         tile, ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(d.coef), ptr(Vd),
+         ptr(dM), ptr(bound), stream())
+    return Vd, dM
+
+
 def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, dM=None,
                        amax=(None, None)):
     """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino, same tile).
@@ -727,14 +742,16 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
 
 def conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2dh, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
                             recompute, slope=0.2, tag=None, amax=(None, None), amax_out=None,
-                            h2_out=None):
+                            h2_out=None, defer=False):
     """conv1x1_dgrad_bn_bwd on h2 operands (nsm_conv1x1_dgrad_bnbwd_h2): dY2h
     [M, 2 cop] (bn_bwd(h2=...)), w2dh the DGRAD h2 pack; amax = (scale source
     of dY2h, of w2dh). HW: pixels per image (the Dropout2d mask row).
     h2_out=(k1dz slot, bound slot), zeroed (recompute=False only): dY1 is
     returned as an h2 tensor (nsm_bn_bwd_apply_h2) for the direct 3x3's h2
-    gradients."""
+    gradients, or with defer=True as DeferredBnBwd(dA1, coef) whose consumer
+    (wino_dual_input_bn_h2) forms dY1 under the bound slot's scale."""
     assert h2_out is None or not recompute
+    assert not defer or h2_out is not None
     k1dz, bound = h2_out if h2_out is not None else (None, None)
     from ._lib import lib
     M, cop2 = dY2h.shape
@@ -758,6 +775,10 @@ def conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2dh, y, st, mask, c_real, dgamma, dbeta, 
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
          ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), ptr(k1dz), ptr(bound), stream())
+    if defer:
+        if ev is not None:
+            ev.record()
+        return DeferredBnBwd(dA1, coef)
     if h2_out is not None:
         dyh = torch.empty(M, 2 * C, dtype=H2, device=y.device)
         call("nsm_bn_bwd_apply_h2", ptr(dA1), dA1.stride(0), ptr(y), y.stride(0), M, C, HW,

@@ -55,6 +55,11 @@ DUAL_TRANSFORM = os.environ.get("NSM_DUAL_WINO", "1") != "0"
 # issue-bound — conv7 apply 152 + dual 250 us -> fused 484 us, conv6 210 ->
 # 260 us (only conv3 gained, 56 -> 48 us).
 LAZY_DY1 = os.environ.get("NSM_LAZY_DY1", "0") != "0"
+# NSM_LAZY_DY1_H2=0: on h2 Winograd operands, store dY1 (a second GEMM pass,
+# or nsm_bn_bwd_apply) instead of forming it in the dual transform. There the
+# F(6x6) BN-fused transform reads a block's pixel region once into LDS
+# (wino_dual_bn_lds_kernel), which removes the issue bound above.
+LAZY_DY1_H2 = os.environ.get("NSM_LAZY_DY1_H2", "1") != "0"
 # NSM_EVAL_FUSED=0: eval forward with separate BN-apply passes instead of the
 # BN + LeakyReLU (+ skip) in the conv epilogues (nsm_conv_fwd_act)
 EVAL_FUSED = os.environ.get("NSM_EVAL_FUSED", "1") != "0"
@@ -619,18 +624,24 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         ops.conv1x1_wgrad_h2(dY2h, s.A1, ci, co, g[c4.weight], amax=(am_dy2, _slot(s.am, AM_A1)),
                              tag=name + ".conv.4.wgrad")
         s.A1 = None
-        recompute = bnb_mode(s.cip, s.cop, dtype, h2=True) == 2
+        # h2 Winograd 3x3: one GEMM pass storing dA1 + the BN-backward partials;
+        # the dual transform forms dY1 per element (wino_dual_input_bn_h2), so
+        # dY1 is never stored and the GEMM never recomputed, under the bound
+        # the finalize derives from max|k1 dz| (AM_DY1B)
+        lazy = h2 and need_dx and LAZY_DY1_H2
+        recompute = not lazy and bnb_mode(s.cip, s.cop, dtype, h2=True) == 2
         # a direct 3x3 on h2 operands (conv2) takes dY1 as h2 too, written by
         # the BN backward with the bound its finalize derives (AM_DY1B)
         h2_3x3 = s.X is not None and s.X.dtype == ops.H2 and not recompute
-        if h2_3x3:
+        if h2_3x3 or lazy:
             am_dy1 = _slot(s.am, AM_DY1B)
         dY1 = ops.conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
                                           g[bn1m.bias], g[c0.bias], recompute,
                                           tag=name + ".conv.4.dgrad",
                                           amax=(am_dy2, s.pw.amax_w2(ops.PACK_DGRAD)),
-                                          amax_out=None if h2_3x3 else am_dy1,
-                                          h2_out=(_slot(s.am, AM_K1DZ1), am_dy1) if h2_3x3 else None)
+                                          amax_out=None if h2_3x3 or lazy else am_dy1,
+                                          h2_out=(_slot(s.am, AM_K1DZ1), am_dy1)
+                                          if h2_3x3 or lazy else None, defer=lazy)
         return _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1)
     dY2 = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias],
                      part=gpart, amax=_slot(s.am, AM_DY2))
@@ -673,7 +684,10 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
     Vd = None
     if h2:
         tile = wino_tile(s.cip, H, W)
-        Vd, dM = ops.wino_dual_input_h2(dY1, B, H, W, tile, am_dy1)
+        if isinstance(dY1, ops.DeferredBnBwd):
+            Vd, dM = ops.wino_dual_input_bn_h2(dY1, s.Y1, s.bn1, s.mask, B, H, W, tile, am_dy1)
+        else:
+            Vd, dM = ops.wino_dual_input_h2(dY1, B, H, W, tile, am_dy1)
         ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=tile,
                                tag=name + ".conv.0.wgrad", dM=dM,
                                amax=(am_dy1, _slot(s.am, AM_X)))

@@ -352,3 +352,84 @@ def test_conv3x3_h2(ops, device, B, H, W, cin_p, cout_p):
     st = ops.bn_train(y, bn, cout_p, 0.1, 1e-5, part=part)
     yr = nh(ref.detach())
     torch.testing.assert_close(st.mean.double(), yr.mean(0), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("tile", [4, 6])
+@pytest.mark.parametrize("B,H,W,C,drop", [(2, 37, 29, 64, True), (1, 16, 16, 128, False),
+                                         (2, 40, 52, 32, True), (3, 13, 7, 96, False),
+                                         (8, 256, 256, 64, True)])
+def test_wino_dual_input_bn_h2(ops, device, B, H, W, C, drop, tile):
+    """nsm_wino_dual_input_bn_h2 (the first BN's backward formed per element
+    inside the h2 dual transform; F(6x6) through the LDS-region kernel): its Vd
+    and dM decode to the fp32 BN-fused dual transform (nsm_wino_dual_input_bn)
+    within the f16x2 bound, under the scale of the dY bound the finalize
+    derives from max|k1 dz| — which dominates max|dY|. Channel scales of y, g,
+    gamma spread 2^-12..2^0; ragged tile grids, multi-block regions."""
+    import math
+    g = torch.Generator().manual_seed(H * W + C + tile)
+    y = (torch.randn(B * H * W, C, generator=g, dtype=torch.float64) * _spread(g, C) +
+         torch.randn(C, generator=g, dtype=torch.float64)).float().to(device)
+    gr = (torch.randn(B * H * W, C, generator=g, dtype=torch.float64) * _spread(g, C)).float().to(device)
+    mask = ((torch.rand(B, C, generator=g) > 0.2).float() / 0.8).to(device) if drop else None
+    bn = torch.nn.BatchNorm2d(C).to(device)
+    with torch.no_grad():
+        bn.weight.copy_(torch.randn(C, generator=g) * _spread(g, C).float())
+        bn.bias.uniform_(-0.2, 0.2)
+    st = ops.bn_train(y, bn, C, 0.1, 1e-5)
+    grads = [[torch.zeros(C, device=device) for _ in range(3)] for _ in range(2)]
+    d32 = ops.bn_bwd(gr, y, st, H * W, mask, C, *grads[0], defer=True)
+    Vd32, dM32 = ops.wino_dual_input_bn(d32, y, st, mask, B, H, W, tile=tile)
+    dy = ops.bn_bwd(gr, y, st, H * W, mask, C, *[torch.zeros(C, device=device) for _ in range(3)])
+    slots = ops.amax_slots(2, device)
+    k1dz, bnd = ops.amax_slot(slots, 0), ops.amax_slot(slots, 1)
+    dh = ops.bn_bwd(gr, y, st, H * W, mask, C, *grads[1], defer=True, h2=(k1dz, bnd))
+    Vdh, dMh = ops.wino_dual_input_bn_h2(dh, y, st, mask, B, H, W, tile, bnd)
+    torch.cuda.synchronize()
+    for a, b in zip(grads[0], grads[1]):
+        assert torch.equal(a, b)
+    bound = _slot_max(bnd)
+    assert bound >= dy.abs().max().item(), (bound, dy.abs().max().item())
+    for which, ref, h2t in ((0, Vd32, Vdh), (1, dM32, dMh)):
+        sb = float(np.float32(bound) * np.float32(ops.wino_beta(tile, which)))
+        e = max(-126, min(126, 15 - math.ceil(math.log2(sb))))
+        h = h2t.view(-1, C // 8, 2, 8).double()
+        dec = (h[:, :, 0, :] + h[:, :, 1, :]).reshape(-1) * 2.0 ** (-e)
+        r = ref.double().reshape(-1)
+        err = (dec - r).abs()
+        assert (err <= r.abs() * 2.0 ** -20 + 2.0 ** (-22 - e) + 1e-6 * r.abs().max()).all(), \
+            (which, err.max().item(), r.abs().max().item())
+
+
+@pytest.mark.parametrize("up", [False, True])
+@pytest.mark.parametrize("B,hi,wi,H,W,C", [(2, 8, 10, 16, 20, 64), (1, 16, 16, 32, 32, 128),
+                                          (2, 5, 7, 10, 14, 32), (1, 34, 60, 67, 120, 64),
+                                          (3, 20, 20, 40, 40, 96)])
+def test_wino_input_h2(ops, device, B, hi, wi, H, W, C, up):
+    """nsm_wino_input_h2 (F(6x6): the LDS-region kernel, optionally sampling
+    the x2 bilinear upsample) decodes to the fp32 input transform
+    (nsm_wino_input_resize) within the f16x2 bound, under the scale of
+    max|x| x beta."""
+    import math
+    if not up:
+        hi, wi = H, W
+    g = torch.Generator().manual_seed(hi * wi + C + int(up))
+    x = (torch.randn(B * hi * wi, C, generator=g, dtype=torch.float64) * _spread(g, C)).float().to(device)
+    slots = ops.amax_slots(1, device)
+    ax = ops.amax_slot(slots, 0)
+    ops.absmax(x, ax)
+    T = ops.wino_tiles(B, H, W, 6)
+    Vh = torch.empty(64 * T * 2 * C, dtype=ops.H2, device=device)
+    ops.call("nsm_wino_input_h2", ops.ptr(x), x.stride(0), B, hi, wi, H, W, C, 6, ops.ptr(Vh),
+             ops.ptr(ax), ops.stream())
+    V32 = torch.empty(64 * T * C, device=device)
+    ops.call("nsm_wino_input_resize", ops.ptr(x), x.stride(0), B, hi, wi, H, W, C, 6, 0,
+             ops.ptr(V32), None, ops.stream())
+    torch.cuda.synchronize()
+    sb = float(np.float32(_slot_max(ax)) * np.float32(ops.wino_beta(6, 0)))
+    e = max(-126, min(126, 15 - math.ceil(math.log2(sb))))
+    h = Vh.view(-1, C // 8, 2, 8).double()
+    dec = (h[:, :, 0, :] + h[:, :, 1, :]).reshape(-1) * 2.0 ** (-e)
+    r = V32.double()
+    err = (dec - r).abs()
+    assert (err <= r.abs() * 2.0 ** -20 + 2.0 ** (-22 - e) + 1e-6 * r.abs().max()).all(), \
+        (err.max().item(), r.abs().max().item())
