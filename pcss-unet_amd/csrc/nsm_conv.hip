@@ -1814,17 +1814,32 @@ __global__ void __launch_bounds__(256) wino_dual_bn_lds_kernel(
     const f32x4 k3 = *(const f32x4*)(bn.coef + 2 * C + c);
     f32x4 mk = {1.f, 1.f, 1.f, 1.f};
     if (bn.mask) mk = *(const f32x4*)(bn.mask + (size_t)b * C + c);
-    for (int p = tid >> 3; p < RH * RW; p += 32) {
+    // every load of the region goes out before the first is used: the loads
+    // are unconditional (a pixel outside the region or image reads the
+    // batch's first pixel, its value then discarded), so hipcc issues all of
+    // them back to back instead of one loop trip at a time
+    constexpr int NIT = (RH * RW + 31) / 32;
+    f32x4 gv[NIT], yv[NIT];
+    bool ok[NIT];
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int p = (tid >> 3) + 32 * k;
       const int py = p / RW, px = p - py * RW;
       const int yy = MT * ty0 - 1 + py, xx = MT * tx0 - 1 + px;
+      ok[k] = p < RH * RW && (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+      const size_t q = (size_t)b * H * W + (ok[k] ? (size_t)yy * W + xx : 0);
+      gv[k] = *(const f32x4*)(g + q * ldg + c);
+      yv[k] = *(const f32x4*)(bn.y + q * bn.ldy + c);
+    }
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int p = (tid >> 3) + 32 * k;
+      if (p >= RH * RW) break;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) {
-        const size_t q = (size_t)(b * H + yy) * W + xx;
-        const f32x4 gv = *(const f32x4*)(g + q * ldg + c);
-        const f32x4 yv = *(const f32x4*)(bn.y + q * bn.ldy + c);
-        f32x4 dz = gv * vlrelu_grad(yv * sc + sh, bn.slope);
+      if (ok[k]) {
+        f32x4 dz = gv[k] * vlrelu_grad(yv[k] * sc + sh, bn.slope);
         if (bn.mask) dz = dz * mk;
-        v = k1 * dz + k2 * (yv - mu) + k3;
+        v = k1 * dz + k2 * (yv[k] - mu) + k3;
       }
       *(f32x4*)&reg[p * CB + cg] = v;
     }
@@ -1876,7 +1891,10 @@ __global__ void __launch_bounds__(256) wino_input_lds_kernel(
   const float hs = exp2i(h2_exp(hsc));  // before any lane leaves (amax_read: all 64 lanes)
   {
     const int c = c0 + (tid & 7) * 4;
-    for (int p = tid >> 3; p < RH * RW; p += 32) {
+#pragma unroll
+    for (int k = 0; k < (RH * RW + 31) / 32; ++k) {
+      const int p = (tid >> 3) + 32 * k;
+      if (p >= RH * RW) break;
       const int py = p / RW, px = p - py * RW;
       const int yy = MT * ty0 - 1 + py, xx = MT * tx0 - 1 + px;
       f32x4 v = {0.f, 0.f, 0.f, 0.f};
