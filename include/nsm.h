@@ -70,11 +70,13 @@ int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
  * pack as an h2 tensor (a as kind 0; FWD [cout_p][2 taps cin_p], DGRAD
  * [cin_p][2 taps cout_p] float16), amax (required) = the slot the launch first
  * fills with max|w| (beta 1), a[6] = 1: shared with the FWD job of the same
- * weight. `base` = the job's first item in the launch (jobs in
+ * weight; kind 6: Winograd U as a single-plane scaled f16 tensor
+ * [alpha^2][n_p][k_p] (the bf16 path's F(4x4) forward, nsm_wino_gemm_f16), a
+ * and amax as kind 4. `base` = the job's first item in the launch (jobs in
  * ascending base order, consecutive); nsm_prep_items() = the job's extent in
- * the launch (its item count rounded up to whole 2048-item blocks: add it to
+ * the launch (its item count rounded up to whole 512-item blocks: add it to
  * get the next base; total_items = the sum). jobs_dev: a device copy.
- * max_pass: the table holds kind-4 / kind-5 jobs (their max|w| pass runs
+ * max_pass: the table holds kind-4 / 5 / 6 jobs (their max|w| pass runs
  * first; 0 skips that launch). */
 typedef struct {
   int kind;
@@ -84,7 +86,7 @@ typedef struct {
   void* dst;
   uint32_t* amax; /* kinds 0, 2 (may be NULL): atomic max of |written| as fp32
                      bits (zeroed beforehand): the f16x2 GEMM operand scale;
-                     kinds 4, 5: max|w| (see above) */
+                     kinds 4, 5, 6: max|w| (see above) */
 } NsmPrepJob;
 long long nsm_prep_items(const NsmPrepJob* job);
 int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items, int max_pass,
@@ -188,6 +190,21 @@ int nsm_wino_dual_input_h2(const float* dy, int lddy, int B, int H, int W, int c
  * max|k1 dz| — the scale source of Vh / dMh and of the GEMMs reading them.
  * Replaces the BN-backward apply + transform of the reference's autograd
  * backward through Unetmodel.py:21-24 (DoubleConv conv.0 -> BN -> LeakyReLU). */
+/* The bf16 path's Winograd F(4x4) forward (Unetmodel.py:21, the DoubleConv's
+ * 3x3 at >= 512 channels) on single-plane scaled f16 operands: V = s B^T x B
+ * from the bf16 NHWC input x (amax_x: max|x| recorded by x's producer, beta =
+ * nsm_wino_beta(4, 0)) as [36][T][cin_p] f16; the batched GEMM with U of prep
+ * kind 6 (M fp32 [36][T][cout_p]); the output transform writing bf16 y [+ bias]
+ * and, with partial, the BN partials of the rounded values (nslot as
+ * nsm_wino_output_stats, nsm_wino_stat_slots). tile 4 only. */
+int nsm_wino_input_f16(const void* x, int ldx, int B, int H, int W, int cin_p, int tile, void* V,
+                       const uint32_t* amax_x, void* stream);
+int nsm_wino_gemm_f16(const void* V, const void* U, int B, int H, int W, int cin_p, int cout_p,
+                      int tile, float* Mb, const uint32_t* amax_v, float beta_v,
+                      const uint32_t* amax_u, float beta_u, void* stream);
+int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int cout_p, int tile,
+                         const float* bias, void* y, int ldy, float* partial, int nslot,
+                         void* stream);
 int nsm_wino_dual_input_bn_h2(const float* g, int ldg, const float* y, int ldy, int B, int H, int W,
                               int c_p, int tile, const float* scale, const float* shift,
                               float slope, const float* mask, const float* mean, const float* coef,

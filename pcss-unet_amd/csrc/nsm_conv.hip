@@ -1526,7 +1526,9 @@ struct WinoAct {
 
 // The column pass streams M's rows (wcol_row: wmat2's bits with one row
 // live): F(6x6) 138 -> 128 VGPRs, 3 -> 4 waves per SIMD
-template <int MT, bool STATS, bool ACT = false>
+// BFO (the bf16 path, nsm_wino_output_bf16): y holds bf16; the BN partials are
+// of the bf16-rounded outputs, as the direct bf16 convolution's epilogue
+template <int MT, bool STATS, bool ACT = false, bool BFO = false>
 __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
                                                           int W, int TH, int TW, long long T,
                                                           const float* __restrict__ bias,
@@ -1570,11 +1572,20 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
     for (int a = 0; a < MT; ++a) {
       const int yy = MT * ty + a;
       if (yy >= H) continue;
-      float* row = y + ((size_t)(b * H + yy) * W + MT * tx) * ldy + c;
+      const size_t ro = ((size_t)(b * H + yy) * W + MT * tx) * ldy + c;
+      float* row = y + ro;
 #pragma unroll
       for (int e = 0; e < MT; ++e)
         if (MT * tx + e < W) {
           o[a][e] = o[a][e] + bv;
+          if constexpr (BFO) {
+            static_assert(!ACT && std::is_same<VT, f32x4>::value, "bf16 output: F(4x4) / F(2x2)");
+            const VT q = o[a][e];
+            o[a][e] = VT{round_bf(q.x), round_bf(q.y), round_bf(q.z), round_bf(q.w)};
+            st4((bf16_t*)y + ro + (size_t)e * ldy, o[a][e]);
+            if (STATS) ts = ts + o[a][e];
+            continue;
+          }
           VT v = o[a][e];
           if (ACT) {
             v = vlrelu(v * asc + ash, act.slope);
@@ -1992,7 +2003,8 @@ __host__ __device__ inline long long nsm_prep_items_dev(const NsmPrepJob& j) {
     case 1:
     case 5: return (long long)j.a[3] * j.a[4] * j.a[2];
     case 2:
-    case 4: return (long long)j.a[2] * j.a[3];
+    case 4:
+    case 6: return (long long)j.a[2] * j.a[3];
     case 3: return j.a[1];
     default: return -1;
   }
@@ -2051,6 +2063,35 @@ __device__ __forceinline__ void wino_weight_item_h2(const float* __restrict__ w,
 #ifndef NSM_PREP_ITEMS
 #define NSM_PREP_ITEMS 512
 #endif
+// Winograd U as a single-plane scaled f16 tensor [alpha^2][n_p][k_p] (the
+// bf16 path's F(4x4) forward, nsm_wino_gemm_f16), scale s
+template <int MT>
+__device__ __forceinline__ void wino_weight_item_f16(const float* __restrict__ w, int cout, int cin,
+                                                     int n_p, int k_p, int flip,
+                                                     bf16_t* __restrict__ U, int idx, float s) {
+  constexpr int A = MT + 2;
+  const int k = idx % k_p, n = idx / k_p;
+  const int co = flip ? k : n, ci = flip ? n : k;
+  float g[3][3];
+  const bool ok = co < cout && ci < cin;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const int sa = flip ? 2 - a : a, sb = flip ? 2 - b : b;
+      g[a][b] = ok ? w[((size_t)co * cin + ci) * 9 + sa * 3 + sb] : 0.f;
+    }
+  float u[A][A];
+  wmat2<CG<MT>>(g, u);
+  const size_t plane = (size_t)n_p * k_p;
+#pragma unroll
+  for (int a = 0; a < A; ++a)
+#pragma unroll
+    for (int b = 0; b < A; ++b)
+      U[(a * A + b) * plane + (size_t)n * k_p + k] =
+          __builtin_bit_cast(unsigned short, (_Float16)(u[a][b] * s));
+}
+
 constexpr int PREP_ITEMS = NSM_PREP_ITEMS;  // items per block, 2 per thread (8: -0.2 % step, more tail)
 
 // blockIdx -> job by a (uniform) binary search over the jobs' first blocks
@@ -2104,7 +2145,7 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
     if (phase == 0) amax_flush(am, j.amax);
     return;
   }
-  if (j.kind == 4) {  // uniform per block
+  if (j.kind == 4 || j.kind == 6) {  // uniform per block (6: single-plane f16 U)
     const int cout = j.a[0], cin = j.a[1], n_p = j.a[2], k_p = j.a[3], flip = j.a[4];
     if (phase == 0) {
       if (j.a[6]) return;  // its slot is filled by the un-flipped job over the same filters
@@ -2127,6 +2168,11 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
     for (int r = 0; r < PREP_ITEMS / 256; ++r) {
       const long long li = blk0 - j.base + r * 256 + threadIdx.x;
       if (li >= items) break;
+      if (j.kind == 6) {
+        if (j.a[5] == 4) wino_weight_item_f16<4>(j.src, cout, cin, n_p, k_p, flip, U, (int)li, s);
+        else wino_weight_item_f16<2>(j.src, cout, cin, n_p, k_p, flip, U, (int)li, s);
+        continue;
+      }
       if (j.a[5] == 6) wino_weight_item_h2<6>(j.src, cout, cin, n_p, k_p, flip, U, (int)li, s);
       else if (j.a[5] == 4) wino_weight_item_h2<4>(j.src, cout, cin, n_p, k_p, flip, U, (int)li, s);
       else wino_weight_item_h2<2>(j.src, cout, cin, n_p, k_p, flip, U, (int)li, s);
@@ -3116,6 +3162,130 @@ extern "C" int nsm_wino_gemm_h2(const void* V, const void* U, int B, int H, int 
                 "wino_gemm_h2: operand too large");
   return wino_gemm_h2((const bf16_t*)V, (const bf16_t*)U, g.T, cin_p, cout_p, g.alpha2, Mb,
                       H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, as_stream(stream));
+}
+
+// ---- bf16 path: Winograd F(4x4) forward on single-plane scaled f16 operands ----
+// The bf16 configuration's direct 3x3 implicit GEMM (gemm_bf16_dma_kernel) is
+// ~75 % of its step. F(4x4, 3x3) does the same convolution with 4x fewer
+// multiplies; its operands V = B^T d B and U = G g G^T are written ONCE as f16
+// scaled by a power of two (max|source| x the transform's bound, as the h2
+// tensors: no overflow, 11-bit significands), the batched GEMM runs the f16
+// MFMA on them (gemm_h2p/h2q_kernel, single-plane mode), M stays fp32 and the
+// output transform writes Y in bf16 with the BN partials of the rounded
+// values. Rounding: V and U to f16 (2^-11), amplified ~7x by the F(4x4)
+// transforms (tools/wino_coeffs.py: F(4x4) / direct rms 7.3 in fp32) — the
+// size of the direct path's bf16 operand rounding (2^-9 x 2). Unetmodel.py:21.
+typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ f32x4 bf4_to_f32(u32x2 w) {
+  return f32x4{bf_lo(w.x), bf_hi(w.x), bf_lo(w.y), bf_hi(w.y)};
+}
+
+// V [alpha^2][T][C] f16 = s B^T d B of the bf16 NHWC input x (zero padding), 4
+// channels per thread, the column pass streamed over the patch rows
+template <int MT>
+__global__ void __launch_bounds__(256) wino_input_f16_kernel(const bf16_t* __restrict__ x, int ld,
+                                                             int H, int W, int C, int TH, int TW,
+                                                             long long T, bf16_t* __restrict__ V,
+                                                             H2Scale hsc) {
+  constexpr int A = MT + 2;
+  const int C4 = C / 4;
+  const long long total = T * C4;
+  const float hs = exp2i(h2_exp(hsc));  // every lane (amax_read: a wave reduction)
+  const size_t plane = (size_t)T * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const long long t = i / C4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    // the whole patch's loads go out first: unconditional (an element outside
+    // the image reads the image's first pixel, then counts as 0)
+    u32x2 raw[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
+        const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        raw[a][e] = *(const u32x2*)(x + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
+        if (!in) raw[a][e] = u32x2{0u, 0u};
+      }
+    f32x4 sc[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      f32x4 d[A];
+#pragma unroll
+      for (int e = 0; e < A; ++e) d[e] = bf4_to_f32(raw[a][e]);
+      wcol_row<CBt<MT>>(sc, d, a);
+    }
+    bf16_t* out = V + (size_t)t * C + c;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      f32x4 v[A];
+      wmat<CBt<MT>>(sc[a], v);
+#pragma unroll
+      for (int e = 0; e < A; ++e)
+        *(u32x2*)(out + (a * A + e) * plane) =
+            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * hs, f16x4v));
+    }
+  }
+}
+
+extern "C" int nsm_wino_input_f16(const void* x, int ldx, int B, int H, int W, int cin_p, int tile,
+                                  void* V, const uint32_t* amax_x, void* stream) {
+  NSM_CHECK_ARG(x && V && amax_x && tile == 4 && cin_p % 32 == 0 && ldx % 4 == 0 && ldx >= cin_p,
+                "wino_input_f16: bad args (tile 4 only)");
+  NSM_CHECK_ARG(((uintptr_t)x % 8) == 0 && ((uintptr_t)V % 16) == 0, "wino_input_f16: alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input_f16: bad shape");
+  hipLaunchKernelGGL(wino_input_f16_kernel<4>, dim3(grid_1d(g.T * cin_p / 4)), dim3(256), 0,
+                     as_stream(stream), (const bf16_t*)x, ldx, H, W, cin_p, g.TH, g.TW, g.T,
+                     (bf16_t*)V, H2Scale{amax_x, wino_beta(4, 0)});
+  NSM_LAUNCH_CHECK("wino_input_f16");
+  return 0;
+}
+
+extern "C" int nsm_wino_gemm_f16(const void* V, const void* U, int B, int H, int W, int cin_p,
+                                 int cout_p, int tile, float* Mb, const uint32_t* amax_v,
+                                 float beta_v, const uint32_t* amax_u, float beta_u, void* stream) {
+  NSM_CHECK_ARG(V && U && Mb && amax_v && amax_u && cin_p % 128 == 0 && cout_p % 128 == 0,
+                "wino_gemm_f16: bad args (cin_p, cout_p multiples of 128)");
+  NSM_CHECK_ARG(((uintptr_t)V % 16) == 0 && ((uintptr_t)U % 16) == 0 && ((uintptr_t)Mb % 16) == 0,
+                "wino_gemm_f16: 16B alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_gemm_f16: bad tile or shape");
+  NSM_CHECK_ARG(g.T * cin_p < (1ll << 30) && (long long)cout_p * cin_p < (1ll << 30),
+                "wino_gemm_f16: operand too large");
+  return wino_gemm_f16((const bf16_t*)V, (const bf16_t*)U, g.T, cin_p, cout_p, g.alpha2, Mb,
+                       H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, as_stream(stream));
+}
+
+// the output transform writing bf16 Y (+ the BN partials of the rounded values)
+extern "C" int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int cout_p, int tile,
+                                    const float* bias, void* y, int ldy, float* partial, int nslot,
+                                    void* stream) {
+  NSM_CHECK_ARG(Mb && y && tile == 4 && cout_p % 32 == 0 && ldy % 4 == 0,
+                "wino_output_bf16: bad args (tile 4 only)");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_bf16: bad shape");
+  dim3 grid(grid_1d(g.T * (cout_p / 4)));
+  if (partial) {
+    NSM_CHECK_ARG(nslot > 0 && nslot % wino_stat_step(cout_p, tile) == 0 && nslot <= (1 << 20),
+                  "wino_output_bf16: nslot %d not a multiple of %d", nslot,
+                  wino_stat_step(cout_p, tile));
+    grid = dim3((unsigned)((long long)nslot * (cout_p / 4) / 256));
+  }
+  hipStream_t s = as_stream(stream);
+  if (partial)
+    hipLaunchKernelGGL((wino_output_kernel<4, true, false, true>), grid, dim3(256), 0, s, Mb, cout_p,
+                       H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, partial, WinoAct{});
+  else
+    hipLaunchKernelGGL((wino_output_kernel<4, false, false, true>), grid, dim3(256), 0, s, Mb,
+                       cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, nullptr, WinoAct{});
+  NSM_LAUNCH_CHECK("wino_output_bf16");
+  return 0;
 }
 
 // 1: fp32 GEMMs on the bf16 matrix cores by the exact split (default), 0: on

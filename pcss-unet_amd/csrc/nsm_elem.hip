@@ -1995,7 +1995,7 @@ extern "C" int nsm_bn_act(const void* y, int ldy, int M, int C, const float* sca
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(bn_act_kernel<bf16_t>, g, b, 0, as_stream(stream), NSM_CT(bf16_t, y), ldy,
                        M, C / 8, fh, scale, shift, slope, mask, NSM_CT(bf16_t, res), ldres,
-                       NSM_T(bf16_t, out), ldo, nullptr);
+                       NSM_T(bf16_t, out), ldo, amax);
   else
     hipLaunchKernelGGL(bn_act_kernel<float>, g, b, 0, as_stream(stream), NSM_CT(float, y), ldy, M,
                        C / 8, fh, scale, shift, slope, mask, NSM_CT(float, res), ldres,
@@ -2114,7 +2114,7 @@ extern "C" int nsm_bn_act_pool(const void* y, int B, int H, int W, int C, const 
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(bn_act_pool_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(bf16_t, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,
-                       NSM_T(bf16_t, z), NSM_T(bf16_t, pooled), nullptr);
+                       NSM_T(bf16_t, z), NSM_T(bf16_t, pooled), amax);
   else
     hipLaunchKernelGGL(bn_act_pool_kernel<float>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,

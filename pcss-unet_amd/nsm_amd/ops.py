@@ -82,6 +82,8 @@ def amax_slot(buf, i):
 def absmax(x, out=None):
     """Operand-maximum slot holding max|x| (nsm_absmax): the f16x2 GEMM
     operand scale of a tensor whose producer did not record it."""
+    if x.dtype != F32:   # the kernel reads fp32 words
+        raise TypeError(f"absmax: fp32 tensor expected, got {x.dtype}")
     if out is None:
         out = amax_slots(1, x.device)
     call("nsm_absmax", ptr(x), x.numel(), ptr(out), stream())
@@ -317,6 +319,36 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     if stats:
         return y, (V if keep_v else None), part
     return (y, V) if keep_v else y
+
+
+def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None):
+    """The bf16 path's 3x3 (pad 1) forward by Winograd F(4x4,3x3) on single-plane
+    scaled f16 operands (nsm_wino_input_f16 / _gemm_f16 / _output_bf16): x
+    [B*H*W, cin_p] bf16, U the prep-kind-6 filters [36][cout_p][cin_p] f16,
+    amax = (max|x| slot filled by x's producer, max|w| slot of the prep).
+    Returns (y bf16 [B*H*W, cout_p], Partials of the rounded y | None)."""
+    from ._lib import lib
+    assert x.dtype == BF16 and U.dtype == H2
+    cin_p = x.shape[1]
+    T = wino_tiles(B, H, W, 4)
+    st = stream()
+    ev = _probe(tag)
+    V = torch.empty(36 * T * cin_p, dtype=H2, device=x.device)
+    call("nsm_wino_input_f16", ptr(x), x.stride(0), B, H, W, cin_p, 4, ptr(V), ptr(amax[0]), st)
+    Mb = empty(36 * T * cout_p, device=x.device)
+    call("nsm_wino_gemm_f16", ptr(V), ptr(U), B, H, W, cin_p, cout_p, 4, ptr(Mb), ptr(amax[0]),
+         wino_beta(4, 0), ptr(amax[1]), wino_beta(4, 2), st)
+    del V
+    y = torch.empty(B * H * W, cout_p, dtype=BF16, device=x.device)
+    nslot = int(lib.nsm_wino_stat_slots(B, H, W, cout_p, 4)) if stats else 0
+    part = None
+    if nslot > 0:
+        part = Partials(empty(nslot * 3 * cout_p, device=x.device), nslot, 0)
+    call("nsm_wino_output_bf16", ptr(Mb), B, H, W, cout_p, 4, ptr(bias), ptr(y), y.stride(0),
+         ptr(part.buf) if part is not None else None, nslot, st)
+    if ev is not None:
+        ev.record()
+    return y, part
 
 
 H2 = torch.float16   # storage dtype of the pre-split (h2) Winograd operands
@@ -565,14 +597,15 @@ def bn_eval(bn_mod, C, c_real, eps, device, gamma=None, beta=None):
 
 def bn_act(y, st, slope=0.2, res=None, out=None, mask=None, HW=0, amax=None):
     """lrelu(y*scale+shift) (* mask[b, c] with b = row // HW) (+ res).
-    amax: operand-maximum slot receiving max|out| (fp32)."""
+    amax: operand-maximum slot receiving max|out| (of the fp32 values before a
+    bf16 store's rounding)."""
     M, C = y.shape
     o = out if out is not None else like(M, C, y)
     assert res is None or res.dtype == y.dtype
     assert mask is None or HW > 0
     call("nsm_bn_act", ptr(y), y.stride(0), M, C, ptr(st.scale), ptr(st.shift), slope, ptr(mask),
          HW, ptr(res), res.stride(0) if res is not None else 0, ptr(o), o.stride(0), dt(y),
-         ptr(amax) if y.dtype == F32 else None, stream())
+         ptr(amax), stream())
     return o
 
 
@@ -902,7 +935,7 @@ def bn_act_pool(y, st, B, H, W, slope=0.2, amax=None):
     z = like(B * H * W, C, y)
     pooled = like(B * (H // 2) * (W // 2), C, y)
     call("nsm_bn_act_pool", ptr(y), B, H, W, C, ptr(st.scale), ptr(st.shift), slope, ptr(z),
-         ptr(pooled), dt(y), ptr(amax) if y.dtype == F32 else None, stream())
+         ptr(pooled), dt(y), ptr(amax), stream())
     return z, pooled
 
 

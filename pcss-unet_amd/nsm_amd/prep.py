@@ -26,6 +26,7 @@ class NsmPrepJob(ctypes.Structure):
 
 
 KIND_PACK_F32, KIND_PACK_BF16, KIND_WINO, KIND_PAD, KIND_WINO_H2, KIND_PACK_H2 = 0, 1, 2, 3, 4, 5
+KIND_WINO_F16 = 6
 # NSM_H2=0: the fp32 training step keeps fp32 Winograd operands (the GEMMs
 # split them in-kernel, nsm_conv_split16.inc) instead of the pre-split h2
 # tensors their producers write (nsm_conv_h2.inc)
@@ -34,6 +35,21 @@ H2_WINO = os.environ.get("NSM_H2", "1") != "0"
 # fp32 operands (register-path f16x2 split) instead of h2 operands written by
 # their producers (csrc/nsm_conv_h2d.inc); on with the h2 Winograd operands
 H2_1X1 = os.environ.get("NSM_H2_1X1", "1") != "0"
+# NSM_BF16_WINO=0: the bf16 training step's 3x3 forward at >= NSM_BF16_WINO_MIN
+# input channels stays on the direct implicit GEMM instead of Winograd F(4x4)
+# on single-plane scaled f16 operands (ops.conv3x3_wino_f16). Measured (B=64
+# step, A/B on one box): off 1240-1245, conv6 only (>= 1024) 1267-1270,
+# conv5-conv7 (>= 512) 1276-1279 frames/s; conv6's forward 3.87 -> 2.5 ms
+# (input transform 0.38 + GEMM 1.53 + output transform 0.61: the fp32 M,
+# 2.25 x 4 B per output element, bounds the last two)
+BF16_WINO = os.environ.get("NSM_BF16_WINO", "1") != "0"
+BF16_WINO_MIN = int(os.environ.get("NSM_BF16_WINO_MIN", "512"))
+
+
+def bf16_wino(cip, dtype, training):
+    """True when a DoubleConv's 3x3 forward runs ops.conv3x3_wino_f16."""
+    return (BF16_WINO and training and dtype == torch.bfloat16 and cip >= BF16_WINO_MIN
+            and cip % 128 == 0)
 
 
 class LazyBlockWeights:
@@ -104,6 +120,13 @@ class _PreparedBlock:
     def w2(self, mode):
         return self.t[("w2", mode)]
 
+    def Uf16(self):
+        """the bf16 path's F(4x4) forward filters (prep kind 6), or None"""
+        return self.t.get("Uf16")
+
+    def amax_Uf16(self):
+        return self.t.get("amaxUf16")
+
 
 class StepWeights:
     """All layouts of a Unet for one (dtype, input size, train/eval) signature.
@@ -120,7 +143,7 @@ class StepWeights:
         base = 0
         # slots: Winograd U (fwd, dgrad) and the packed 1x1 weights (fwd, dgrad)
         # (fwd + dgrad of each block's 3x3 and 1x1 weight)
-        n_wino = len(shapes) * 4 if dtype == torch.float32 else 0
+        n_wino = len(shapes) * 4
         # per-step maxima of the Winograd weights (the f16x2 GEMMs' operand
         # scales), zeroed by run() before the prep launch refills them
         self.amax = ops.amax_slots(max(n_wino, 1), dev)
@@ -181,7 +204,16 @@ class StepWeights:
                 # the direct 3x3 (conv2) of the fp32 train step on h2 operands:
                 # kind-5 packs, the DGRAD job sharing the FWD job's max|w| slot
                 h2_3x3 = h2 and training and H2_1X1
+                wf16 = bf16_wino(cip, dtype, training)
+                if wf16:   # Winograd F(4x4) forward: single-plane f16 U (kind 6)
+                    am = ops.amax_slot(self.amax, n_am)
+                    n_am += 1
+                    pb.t["amaxUf16"] = am
+                    pb.t["Uf16"] = add(KIND_WINO_F16, (ci, ci, cip, cip, 0, 4, 0), c0.weight,
+                                       36 * cip * cip, ops.H2, amax=am)
                 for mode in modes:
+                    if wf16 and mode == ops.PACK_FWD:
+                        continue   # the forward reads Uf16
                     am = None
                     if h2_3x3 and mode != ops.PACK_FWD:
                         am = pb.t[("amaxw1", ops.PACK_FWD)]
@@ -218,7 +250,7 @@ class StepWeights:
         self.total = base
         self.njobs = len(jobs)
         # the max|w| pass (phase 0) runs only for the h2 jobs' scale sources
-        self.max_pass = int(any(j.kind in (KIND_WINO_H2, KIND_PACK_H2) for j in jobs))
+        self.max_pass = int(any(j.kind in (KIND_WINO_H2, KIND_PACK_H2, KIND_WINO_F16) for j in jobs))
         raw = (NsmPrepJob * len(jobs))(*jobs)
         host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
         self.table = host.to(dev)

@@ -547,6 +547,14 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
                                      amax_v=am_v, amax_u=pw.amax_U1(False))
         if training and part1 is None:
             part1 = ops.bn_partials(Y1)
+    elif training and getattr(pw, "Uf16", None) is not None and pw.Uf16() is not None:
+        # bf16: Winograd F(4x4) forward on single-plane scaled f16 operands
+        # (the backward stays on the direct implicit GEMM, which keeps X)
+        Y1, part1 = ops.conv3x3_wino_f16(X, B, H, W, pw.Uf16(), b1, cip,
+                                         amax=(_slot(am, AM_X), pw.amax_Uf16()),
+                                         tag=name + ".conv.0.fwd")
+        if part1 is None:
+            part1 = ops.bn_partials(Y1)
     else:
         w1 = pw.w1(ops.PACK_FWD)
         if w1.dtype == ops.H2:   # h2 operands (X from input_prep_h2; csrc/nsm_conv_h2d.inc)

@@ -1,0 +1,69 @@
+"""GPU: the bf16 path's Winograd F(4x4,3x3) forward on single-plane scaled
+f16 operands (ops.conv3x3_wino_f16: nsm_wino_input_f16, prep kind 6,
+nsm_wino_gemm_f16 on gemm_h2p/h2q in single-plane mode, nsm_wino_output_bf16)
+against a float64 conv2d of the same bf16 input: its error stays within that of
+the direct bf16 implicit GEMM it replaces (the reference's bf16-autocast
+arithmetic for Unetmodel.py:21), and the BN partials written by the output
+transform are those of the bf16-rounded outputs."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _prep_u(ops, w, cin_p, cout_p, device):
+    """prep kind 6 (single-plane f16 U) through nsm_prep_weights, one job."""
+    from nsm_amd import prep
+    from nsm_amd._lib import lib
+    am = ops.amax_slots(1, device)
+    U = torch.empty(36 * cout_p * cin_p, dtype=ops.H2, device=device)
+    j = prep.NsmPrepJob()
+    j.kind = prep.KIND_WINO_F16
+    for i, v in enumerate((w.shape[0], w.shape[1], cout_p, cin_p, 0, 4, 0)):
+        j.a[i] = v
+    j.base = 0
+    j.src = w.data_ptr()
+    j.dst = U.data_ptr()
+    j.amax = am.data_ptr()
+    n = int(lib.nsm_prep_items(ctypes.byref(j)))
+    raw = (prep.NsmPrepJob * 1)(j)
+    table = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8).to(device)
+    ops.call("nsm_prep_weights", ops.ptr(table), 1, n, 1, ops.stream())
+    torch.cuda.synchronize()
+    return U, am
+
+
+@pytest.mark.parametrize("B,H,W,ci,co", [(2, 32, 32, 512, 512), (1, 37, 29, 512, 1024),
+                                        (4, 16, 16, 1024, 512), (64, 8, 8, 512, 1024)])
+def test_conv3x3_wino_f16_vs_direct_bf16(device, B, H, W, ci, co):
+    from nsm_amd import ops
+    g = torch.Generator().manual_seed(B * H + W + ci)
+    x = torch.randn(B, ci, H, W, generator=g) * torch.pow(2.0, torch.rand(1, ci, 1, 1, generator=g) * 4 - 2)
+    w = torch.randn(co, ci, 3, 3, generator=g) / (9 * ci) ** 0.5
+    b = torch.randn(co, generator=g) * 0.1
+    xb = x.to(torch.bfloat16)
+    ref = F.conv2d(xb.double(), w.double(), b.double(), padding=1)
+    nhwc = lambda t: t.permute(0, 2, 3, 1).reshape(-1, t.shape[1]).contiguous()  # noqa: E731
+    xd = nhwc(xb).to(device)
+    ax = ops.amax_slots(1, device)
+    ops.absmax(xd.float(), ax)   # (x's producer records it in the model path)
+    U, au = _prep_u(ops, w.to(device).contiguous(), ci, co, device)
+    y, part = ops.conv3x3_wino_f16(xd, B, H, W, U, b.to(device), co, amax=(ax, au))
+    wp = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_FWD, torch.bfloat16)
+    y0 = ops.conv_fwd(xd, B, H, W, wp, b.to(device), co, 3)
+    torch.cuda.synchronize()
+    r = nhwc(ref)
+    e1 = (y.double().cpu() - r)
+    e0 = (y0.double().cpu() - r)
+    rms1, rms0 = e1.pow(2).mean().sqrt().item(), e0.pow(2).mean().sqrt().item()
+    mx1, mx0 = e1.abs().max().item(), e0.abs().max().item()
+    print(f"wino f16 rms {rms1:.3e} max {mx1:.3e} | direct bf16 rms {rms0:.3e} max {mx0:.3e}")
+    assert rms1 <= 1.5 * rms0 and mx1 <= 2.0 * mx0, (rms1, rms0, mx1, mx0)
+    if part is not None:
+        bn = torch.nn.BatchNorm2d(co).to(device)
+        st = ops.bn_train(y, bn, co, 0.1, 1e-5, part=part)
+        yr = y.double()
+        torch.testing.assert_close(st.mean.double(), yr.mean(0), rtol=1e-5, atol=1e-6)
