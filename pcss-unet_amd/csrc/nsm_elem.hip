@@ -2073,7 +2073,7 @@ extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, 
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, gr, b, 0, as_stream(stream),
                        NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, C / 8, fh, scale,
-                       shift, slope, mask, mean, coef, NSM_T(bf16_t, dy), lddy, nullptr);
+                       shift, slope, mask, mean, coef, NSM_T(bf16_t, dy), lddy, amax);
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, gr, b, 0, as_stream(stream),
                        NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, C / 8, fh, scale,

@@ -712,7 +712,7 @@ def bn_bwd(g, y, st, HW, mask, c_real, dgamma, dbeta, dbias_prev, slope=0.2, par
     dy = like(M, C, y)
     call("nsm_bn_bwd_apply", ptr(g), g.stride(0), ptr(y), y.stride(0), M, C, HW, ptr(st.scale),
          ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy), dy.stride(0), dt(y),
-         ptr(amax) if y.dtype == F32 else None, stream())
+         ptr(amax), stream())
     return dy
 
 
@@ -767,7 +767,7 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     else:
         call("nsm_bn_bwd_apply", ptr(dA1), dA1.stride(0), ptr(y), y.stride(0), M, C, H * W,
              ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(coef), ptr(dy),
-             dy.stride(0), dtc, ptr(amax_out) if dtc == NSM_F32 else None, stream())
+             dy.stride(0), dtc, ptr(amax_out), stream())
     if ev is not None:
         ev.record()
     return dy

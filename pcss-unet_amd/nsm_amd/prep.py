@@ -120,9 +120,10 @@ class _PreparedBlock:
     def w2(self, mode):
         return self.t[("w2", mode)]
 
-    def Uf16(self):
-        """the bf16 path's F(4x4) forward filters (prep kind 6), or None"""
-        return self.t.get("Uf16")
+    def Uf16(self, flip=False):
+        """the bf16 path's F(4x4) filters (prep kind 6; flip: the input
+        gradient's), or None"""
+        return self.t.get("Uf16d" if flip else "Uf16")
 
     def amax_Uf16(self):
         return self.t.get("amaxUf16")
@@ -211,9 +212,12 @@ class StepWeights:
                     pb.t["amaxUf16"] = am
                     pb.t["Uf16"] = add(KIND_WINO_F16, (ci, ci, cip, cip, 0, 4, 0), c0.weight,
                                        36 * cip * cip, ops.H2, amax=am)
+                    # the input gradient's filters (flipped; the forward job's max|w| slot)
+                    pb.t["Uf16d"] = add(KIND_WINO_F16, (ci, ci, cip, cip, 1, 4, 1), c0.weight,
+                                        36 * cip * cip, ops.H2, amax=am)
                 for mode in modes:
-                    if wf16 and mode == ops.PACK_FWD:
-                        continue   # the forward reads Uf16
+                    if wf16:
+                        continue   # forward and input gradient read Uf16 / Uf16d
                     am = None
                     if h2_3x3 and mode != ops.PACK_FWD:
                         am = pb.t[("amaxw1", ops.PACK_FWD)]

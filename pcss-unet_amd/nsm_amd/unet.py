@@ -662,6 +662,8 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
                        pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
     mode = bnb_mode(s.cip, s.cop, dtype)
+    if mode == 2 and _wino_f16(s):
+        mode = 1   # dY1 through nsm_bn_bwd_apply, which records max|dY1| (the dgrad's V scale)
     # pre-split (h2) Winograd operands: dY1's producer records max|dY1|, the
     # scale source of both its transforms (Vd, dM)
     # dY1 is consumed only by its two Winograd transforms: leave the BN apply
@@ -740,9 +742,21 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
         return ops.conv3x3_wino(dY1, B, H, W, U1d, None, s.cip, tile=tile,
                                 tag=name + ".conv.0.dgrad", v_in=Vd, amax_v=_slot(s.am, AM_VD),
                                 amax_u=s.pw.amax_U1(True))
+    if _wino_f16(s):   # bf16: Winograd F(4x4) on f16 operands, as the forward
+        return ops.conv3x3_wino_f16(dY1, B, H, W, s.pw.Uf16(True), None, s.cip,
+                                    amax=(am_dy1, s.pw.amax_Uf16()), stats=False,
+                                    tag=name + ".conv.0.dgrad")[0]
     w1d = s.pw.w1(ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad",
                         amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)))
+
+
+def _wino_f16(s):
+    """True when block s's 3x3 runs the bf16 path's F(4x4) f16 Winograd
+    (forward and input gradient; its filters were prepared)."""
+    pw = s.pw
+    return (s.Y1 is not None and s.Y1.dtype == torch.bfloat16
+            and getattr(pw, "Uf16", None) is not None and pw.Uf16(True) is not None)
 
 
 def _bnred_of(s):
