@@ -205,6 +205,18 @@ int nsm_wino_gemm_f16(const void* V, const void* U, int B, int H, int W, int cin
 int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int cout_p, int tile,
                          const float* bias, void* y, int ldy, float* partial, int nslot,
                          void* stream);
+/* Its weight gradient: dM = s (A dY A^T) of the bf16 output gradient dY as
+ * [36][T][c_p] f16 (amax_dy: max|dY| from dY's producer, beta =
+ * nsm_wino_beta(4, 1)); then dw [cout][cin][3][3] from dM and the forward's V
+ * (batched split-K GEMMs on the f16 matrix cores, one product per k-step, and
+ * the filter transform); ws >= nsm_wino_wgrad_f16_ws floats. tile 4. */
+int nsm_wino_dout_f16(const void* dy, int lddy, int B, int H, int W, int c_p, int tile, void* dM,
+                      const uint32_t* amax_dy, void* stream);
+size_t nsm_wino_wgrad_f16_ws(int B, int H, int W, int cin_p, int cout_p, int tile);
+int nsm_conv3x3_wgrad_wino_f16(const void* dM, const void* V, int B, int H, int W, int cin_p,
+                               int cout_p, int cin, int cout, int tile, float* dw, float* ws,
+                               size_t ws_floats, const uint32_t* amax_dy, const uint32_t* amax_x,
+                               void* stream);
 int nsm_wino_dual_input_bn_h2(const float* g, int ldg, const float* y, int ldy, int B, int H, int W,
                               int c_p, int tile, const float* scale, const float* shift,
                               float slope, const float* mask, const float* mean, const float* coef,

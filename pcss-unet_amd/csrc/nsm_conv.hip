@@ -3288,6 +3288,131 @@ extern "C" int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int co
   return 0;
 }
 
+// dM [alpha^2][T][C] f16 = s (A dY A^T) of the bf16 output gradient (the
+// weight gradient's transform of dY, as wino_dout_kernel), 4 channels per
+// thread, the interior's loads first, the column pass streamed
+template <int MT>
+__global__ void __launch_bounds__(256) wino_dout_f16_kernel(const bf16_t* __restrict__ dy, int ld,
+                                                            int H, int W, int C, int TH, int TW,
+                                                            long long T, bf16_t* __restrict__ dM,
+                                                            H2Scale hsc) {
+  constexpr int A = MT + 2;
+  const int C4 = C / 4;
+  const long long total = T * C4;
+  const float hs = exp2i(h2_exp(hsc));  // every lane (amax_read: a wave reduction)
+  const size_t plane = (size_t)T * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const long long t = i / C4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    u32x2 raw[MT][MT];
+#pragma unroll
+    for (int a = 0; a < MT; ++a)
+#pragma unroll
+      for (int e = 0; e < MT; ++e) {
+        const int yy = MT * ty + a, xx = MT * tx + e;
+        const bool in = yy < H && xx < W;
+        raw[a][e] = *(const u32x2*)(dy + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
+        if (!in) raw[a][e] = u32x2{0u, 0u};
+      }
+    f32x4 sc[A][MT];
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      f32x4 d[MT];
+#pragma unroll
+      for (int e = 0; e < MT; ++e) d[e] = bf4_to_f32(raw[a][e]);
+      wcol_row<CA<MT>>(sc, d, a);
+    }
+    bf16_t* out = dM + (size_t)t * C + c;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      f32x4 v[A];
+      wmat<CA<MT>>(sc[a], v);
+#pragma unroll
+      for (int e = 0; e < A; ++e)
+        *(u32x2*)(out + (a * A + e) * plane) =
+            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * hs, f16x4v));
+    }
+  }
+}
+
+extern "C" int nsm_wino_dout_f16(const void* dy, int lddy, int B, int H, int W, int c_p, int tile,
+                                 void* dM, const uint32_t* amax_dy, void* stream) {
+  NSM_CHECK_ARG(dy && dM && amax_dy && tile == 4 && c_p % 32 == 0 && lddy % 4 == 0 && lddy >= c_p,
+                "wino_dout_f16: bad args (tile 4 only)");
+  NSM_CHECK_ARG(((uintptr_t)dy % 8) == 0 && ((uintptr_t)dM % 16) == 0, "wino_dout_f16: alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_dout_f16: bad shape");
+  hipLaunchKernelGGL(wino_dout_f16_kernel<4>, dim3(grid_1d(g.T * c_p / 4)), dim3(256), 0,
+                     as_stream(stream), (const bf16_t*)dy, lddy, H, W, c_p, g.TH, g.TW, g.T,
+                     (bf16_t*)dM, H2Scale{amax_dy, wino_beta(4, 1)});
+  NSM_LAUNCH_CHECK("wino_dout_f16");
+  return 0;
+}
+
+// the weight-gradient plan of the f16 path: the h2 plan's, on its 256 / 128 tiles
+static WinoWgradPlan plan_wino_wgrad_f16(long long T, int cin_p, int cout_p, int nb) {
+  WinoWgradPlan p = plan_wino_wgrad_h2(T, cin_p, cout_p, nb);
+  if ((p.BM == 256 && p.BN == 256) || (p.BM == 128 && p.BN == 128)) return p;
+  // (the h2 planner's smaller tiles: 128 x 128 with its ~512-block split)
+  p.BM = p.BN = 128;
+  const long long tiles = (long long)ceil_div(cout_p, 128) * ceil_div(cin_p, 128) * nb;
+  long long sp = (512 + tiles - 1) / tiles, maxs = (T + 255) / 256;
+  if (sp > maxs) sp = maxs;
+  if (sp > 64) sp = 64;
+  if (sp < 1) sp = 1;
+  long long kc = (T + sp - 1) / sp;
+  kc = (kc + BK - 1) / BK * BK;
+  sp = (T + kc - 1) / kc;
+  p.splits = (int)sp;
+  p.kchunk = (int)kc;
+  p.slab_floats = (size_t)nb * sp * cout_p * cin_p;
+  if (sp > 1) p.slab_floats += (size_t)nb * cout_p * cin_p;
+  return p;
+}
+
+extern "C" size_t nsm_wino_wgrad_f16_ws(int B, int H, int W, int cin_p, int cout_p, int tile) {
+  WinoGeom g;
+  if (!wino_geom(tile, B, H, W, g)) return 0;
+  return plan_wino_wgrad_f16(g.T, cin_p, cout_p, g.alpha2).slab_floats;
+}
+
+// dw[co][ci][3][3] (reference layout) of the bf16 path's Winograd F(4x4) 3x3
+// from dM (nsm_wino_dout_f16, scale source amax_dy) and the forward's V
+// (nsm_wino_input_f16, scale source amax_x): batched split-K GEMMs on the f16
+// matrix cores, then the filter transform (wgrad_wino_finish)
+extern "C" int nsm_conv3x3_wgrad_wino_f16(const void* dM, const void* V, int B, int H, int W,
+                                          int cin_p, int cout_p, int cin, int cout, int tile,
+                                          float* dw, float* ws, size_t ws_floats,
+                                          const uint32_t* amax_dy, const uint32_t* amax_x,
+                                          void* stream) {
+  NSM_CHECK_ARG(dM && V && dw && ws && amax_dy && amax_x && tile == 4,
+                "conv3x3_wgrad_wino_f16: bad args");
+  NSM_CHECK_ARG(cin_p % 128 == 0 && cout_p % 128 == 0 && cin <= cin_p && cout <= cout_p,
+                "conv3x3_wgrad_wino_f16: channels (multiples of 128)");
+  NSM_CHECK_ARG(((uintptr_t)dM % 16) == 0 && ((uintptr_t)V % 16) == 0 && ((uintptr_t)ws % 16) == 0,
+                "conv3x3_wgrad_wino_f16: alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "conv3x3_wgrad_wino_f16: bad shape");
+  NSM_CHECK_ARG(g.T * (long long)std::max(cin_p, cout_p) < (1ll << 30),
+                "conv3x3_wgrad_wino_f16: operand too large");
+  const int nb = g.alpha2;
+  const WinoWgradPlan pl = plan_wino_wgrad_f16(g.T, cin_p, cout_p, nb);
+  if (ws_floats < pl.slab_floats)
+    return fail(NSM_E_WS, "conv3x3_wgrad_wino_f16: workspace too small");
+  hipStream_t s = as_stream(stream);
+  const int rc = wino_wgrad_gemm_f16((const bf16_t*)dM, (const bf16_t*)V, g.T, cin_p, cout_p, nb,
+                                     pl.BM, pl.BN, pl.kchunk, pl.splits, ws,
+                                     H2Scale{amax_dy, wino_beta(tile, 1)},
+                                     H2Scale{amax_x, wino_beta(tile, 0)}, s);
+  if (rc) return rc;
+  return wgrad_wino_finish(ws, pl, nb, cout_p, cin_p, cin, cout, tile, dw, s);
+}
+
 // 1: fp32 GEMMs on the bf16 matrix cores by the exact split (default), 0: on
 // v_mfma_f32_32x32x2_f32; returns the previous mode
 extern "C" int nsm_set_f32_split(int mode) {

@@ -321,12 +321,36 @@ def conv3x3_wino(x, B, H, W, U, bias, cout_p, tile=4, tag=None, keep_v=False, re
     return (y, V) if keep_v else y
 
 
-def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None):
+def wino_dout_f16(dy, B, H, W, amax_dy):
+    """dM [36][T][C] f16 = s A dY A^T of the bf16 output gradient
+    (nsm_wino_dout_f16): the F(4x4) weight gradient's transform of dY."""
+    c_p = dy.shape[1]
+    dM = torch.empty(36 * wino_tiles(B, H, W, 4) * c_p, dtype=H2, device=dy.device)
+    call("nsm_wino_dout_f16", ptr(dy), dy.stride(0), B, H, W, c_p, 4, ptr(dM), ptr(amax_dy), stream())
+    return dM
+
+
+def conv3x3_wgrad_wino_f16(dM, V, B, H, W, cin_p, cout_p, cin, cout, dw, amax, tag=None):
+    """dw [cout, cin, 3, 3] of the bf16 path's F(4x4) 3x3 from dM (wino_dout_f16)
+    and the forward's V (conv3x3_wino_f16(keep_v=True)); amax = (max|dY| slot,
+    max|x| slot), their scale sources."""
+    from ._lib import lib
+    n = int(lib.nsm_wino_wgrad_f16_ws(B, H, W, cin_p, cout_p, 4))
+    ws = empty(n, device=dM.device)
+    ev = _probe(tag)
+    call("nsm_conv3x3_wgrad_wino_f16", ptr(dM), ptr(V), B, H, W, cin_p, cout_p, cin, cout, 4,
+         ptr(dw), ptr(ws), n, ptr(amax[0]), ptr(amax[1]), stream())
+    if ev is not None:
+        ev.record()
+
+
+def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, keep_v=False):
     """The bf16 path's 3x3 (pad 1) forward by Winograd F(4x4,3x3) on single-plane
     scaled f16 operands (nsm_wino_input_f16 / _gemm_f16 / _output_bf16): x
     [B*H*W, cin_p] bf16, U the prep-kind-6 filters [36][cout_p][cin_p] f16,
     amax = (max|x| slot filled by x's producer, max|w| slot of the prep).
-    Returns (y bf16 [B*H*W, cout_p], Partials of the rounded y | None)."""
+    Returns (y bf16 [B*H*W, cout_p], Partials of the rounded y | None) and,
+    with keep_v, V (the weight gradient's operand)."""
     from ._lib import lib
     assert x.dtype == BF16 and U.dtype == H2
     cin_p = x.shape[1]
@@ -338,7 +362,8 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None):
     Mb = empty(36 * T * cout_p, device=x.device)
     call("nsm_wino_gemm_f16", ptr(V), ptr(U), B, H, W, cin_p, cout_p, 4, ptr(Mb), ptr(amax[0]),
          wino_beta(4, 0), ptr(amax[1]), wino_beta(4, 2), st)
-    del V
+    if not keep_v:
+        V = None
     y = torch.empty(B * H * W, cout_p, dtype=BF16, device=x.device)
     nslot = int(lib.nsm_wino_stat_slots(B, H, W, cout_p, 4)) if stats else 0
     part = None
@@ -348,7 +373,7 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None):
          ptr(part.buf) if part is not None else None, nslot, st)
     if ev is not None:
         ev.record()
-    return y, part
+    return (y, part, V) if keep_v else (y, part)
 
 
 H2 = torch.float16   # storage dtype of the pre-split (h2) Winograd operands

@@ -60,6 +60,9 @@ LAZY_DY1 = os.environ.get("NSM_LAZY_DY1", "0") != "0"
 # F(6x6) BN-fused transform reads a block's pixel region once into LDS
 # (wino_dual_bn_lds_kernel), which removes the issue bound above.
 LAZY_DY1_H2 = os.environ.get("NSM_LAZY_DY1_H2", "1") != "0"
+# NSM_WGRAD_F16=0: the bf16 path's F(4x4) layers take their weight gradient
+# from the direct implicit GEMM instead of the Winograd domain (dM x V)
+WGRAD_F16 = os.environ.get("NSM_WGRAD_F16", "1") != "0"
 # NSM_EVAL_FUSED=0: eval forward with separate BN-apply passes instead of the
 # BN + LeakyReLU (+ skip) in the conv epilogues (nsm_conv_fwd_act)
 EVAL_FUSED = os.environ.get("NSM_EVAL_FUSED", "1") != "0"
@@ -431,7 +434,7 @@ def _masks_for(mod, B, device, training):
 
 class _BlockSaved:
     __slots__ = ("X", "Y1", "Y2", "bn1", "bn2", "mask", "B", "H", "W", "cip", "cop", "V", "A1",
-                 "pw", "Z", "am")
+                 "pw", "Z", "am", "Vf16")
 
 
 # a block's operand-maximum slots (the f16x2 GEMMs' operand scales, filled by
@@ -497,7 +500,7 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
     Z = ops.conv_fwd_act(A1, B, H, W, pw.w2(ops.PACK_FWD), pw.vec("b2"), cop, 1, bn2, res=res,
                          slope=SLOPE, tag=name + ".conv.4.fwd")
     s = _BlockSaved()
-    s.X = s.Y1 = s.Y2 = s.mask = s.V = s.A1 = None
+    s.X = s.Y1 = s.Y2 = s.mask = s.V = s.A1 = s.Vf16 = None
     s.bn1, s.bn2, s.pw, s.Z = bn1, bn2, pw, Z
     s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
     s.am = am
@@ -528,7 +531,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     if fuse_out and not training and EVAL_FUSED:
         return _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am)
     b1 = pw.vec("b1")
-    V = None
+    V = Vf16 = None
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         tile = wino_tile(cip, H, W)
         U1 = pw.U1(tile, False)
@@ -550,9 +553,11 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     elif training and getattr(pw, "Uf16", None) is not None and pw.Uf16() is not None:
         # bf16: Winograd F(4x4) forward on single-plane scaled f16 operands
         # (the backward stays on the direct implicit GEMM, which keeps X)
-        Y1, part1 = ops.conv3x3_wino_f16(X, B, H, W, pw.Uf16(), b1, cip,
-                                         amax=(_slot(am, AM_X), pw.amax_Uf16()),
-                                         tag=name + ".conv.0.fwd")
+        r = ops.conv3x3_wino_f16(X, B, H, W, pw.Uf16(), b1, cip,
+                                 amax=(_slot(am, AM_X), pw.amax_Uf16()),
+                                 tag=name + ".conv.0.fwd", keep_v=WGRAD_F16)
+        Y1, part1 = r[0], r[1]
+        Vf16 = r[2] if WGRAD_F16 else None
         if part1 is None:
             part1 = ops.bn_partials(Y1)
     else:
@@ -604,6 +609,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     s.pw = pw
     s.B, s.H, s.W, s.cip, s.cop = B, H, W, cip, cop
     s.V = V if training else None  # Winograd-domain input, reused by the weight gradient
+    s.Vf16 = Vf16 if training else None  # (the bf16 path's F(4x4) V, likewise)
     s.A1 = A1 if training else None  # activated 1x1 operand, reused by its weight gradient
     s.Z = None
     s.am = am
@@ -731,6 +737,11 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
         return ops.conv3x3_h2(dY1, B, H, W, s.pw.w1(ops.PACK_DGRAD), None, s.cip, stats=False,
                               amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)),
                               tag=name + ".conv.0.dgrad")[0]
+    elif s.Vf16 is not None:   # bf16 F(4x4): dY's transform, then the Winograd-domain GEMMs
+        dM = ops.wino_dout_f16(dY1, B, H, W, am_dy1)
+        ops.conv3x3_wgrad_wino_f16(dM, s.Vf16, B, H, W, s.cip, s.cip, ci, ci, g[c0.weight],
+                                   amax=(am_dy1, _slot(s.am, AM_X)), tag=name + ".conv.0.wgrad")
+        s.Vf16 = None
     else:
         ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad",
                        amax=(am_dy1, _slot(s.am, AM_X)))

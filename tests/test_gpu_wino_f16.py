@@ -67,3 +67,39 @@ def test_conv3x3_wino_f16_vs_direct_bf16(device, B, H, W, ci, co):
         st = ops.bn_train(y, bn, co, 0.1, 1e-5, part=part)
         yr = y.double()
         torch.testing.assert_close(st.mean.double(), yr.mean(0), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("B,H,W,c", [(2, 32, 32, 512), (1, 37, 29, 512), (4, 16, 16, 1024)])
+def test_wgrad_wino_f16_vs_direct_bf16(device, B, H, W, c):
+    """The weight gradient in the F(4x4) domain (nsm_wino_dout_f16 + the
+    single-plane KM GEMMs + the filter transform) against a float64 weight
+    gradient of the unrounded fp32 operands: within 2x the error of the direct
+    bf16 weight gradient (whose error is the bf16 rounding of x and dY, as in
+    the reference's bf16 autocast; the F(4x4) f16 operands add theirs)."""
+    from nsm_amd import ops
+    g = torch.Generator().manual_seed(B * H + W + c)
+    x32 = torch.randn(B, c, H, W, generator=g)
+    dy32 = torch.randn(B, c, H, W, generator=g) * 0.01
+    x, dy = x32.to(torch.bfloat16), dy32.to(torch.bfloat16)
+    w = torch.randn(c, c, 3, 3, generator=g) / (9 * c) ** 0.5
+    xr = x32.double().requires_grad_(True)
+    wr = w.double().requires_grad_(True)
+    F.conv2d(xr, wr, None, padding=1).backward(dy32.double())
+    nhwc = lambda t: t.permute(0, 2, 3, 1).reshape(-1, t.shape[1]).contiguous()  # noqa: E731
+    xd, dyd = nhwc(x).to(device), nhwc(dy).to(device)
+    ax, ady = ops.amax_slots(1, device), ops.amax_slots(1, device)
+    ops.absmax(xd.float(), ax)
+    ops.absmax(dyd.float(), ady)
+    U, au = _prep_u(ops, w.to(device).contiguous(), c, c, device)
+    _, _, V = ops.conv3x3_wino_f16(xd, B, H, W, U, None, c, amax=(ax, au), stats=False, keep_v=True)
+    dM = ops.wino_dout_f16(dyd, B, H, W, ady)
+    dw = torch.empty(c, c, 3, 3, device=device)
+    ops.conv3x3_wgrad_wino_f16(dM, V, B, H, W, c, c, c, c, dw, amax=(ady, ax))
+    dw0 = torch.empty_like(dw)
+    ops.conv_wgrad(dyd, xd, B, H, W, 3, c, c, dw0)
+    torch.cuda.synchronize()
+    r = wr.grad
+    e1, e0 = dw.double().cpu() - r, dw0.double().cpu() - r
+    rms1, rms0 = e1.pow(2).mean().sqrt().item(), e0.pow(2).mean().sqrt().item()
+    print(f"wgrad wino f16 rms {rms1:.3e} | direct bf16 rms {rms0:.3e} | ref rms {r.pow(2).mean().sqrt().item():.3e}")
+    assert rms1 <= 2.0 * rms0, (rms1, rms0)
