@@ -328,6 +328,35 @@ def dominant_roofline(B, H, W, conv_ms, gemm_ms, launches, wino_tile):
                            "direct_conv_flops": alg_flops, "direct_conv_bytes": alg_bytes}}
 
 
+def wino_f16_roofline(B, H, W, conv_ms, gemm_ms, launches):
+    """Roofline object of conv6.conv.0's forward on the bf16 path (at >= 512
+    channels, nsm_amd.prep.BF16_WINO): Winograd F(4x4,3x3) on single-plane
+    scaled f16 operands, 36 batched GEMMs of T x 1024 x 1024 on
+    gemm_h2p_kernel's single-plane mode (ONE f16 product per fp32-accumulated
+    term: the pipe work equals the Winograd products), HIP events per launch.
+    whole_conv adds the input / output transforms and the direct-conv rate."""
+    h6, w6 = H // 8, W // 8
+    T6 = B * ((h6 + 3) // 4) * ((w6 + 3) // 4)
+    work = 36 * 2.0 * T6 * 1024 * 1024
+    alg_flops = conv_flops(B, h6, w6, 1024, 1024, 3)
+    alg_bytes = (2 * B * h6 * w6 * 1024 + 9 * 1024 * 1024) * 2
+    achieved = work / (gemm_ms * 1e-3) / 1e12
+    return {"kernel": f"conv6.conv.0.fwd bf16 path: Winograd F(4x4,3x3) batched GEMM (36 x M={T6} "
+                      f"N=1024 K=1024) on single-plane scaled f16 operands, B={B} at {h6}x{w6}: "
+                      "gemm_h2p_kernel<256,256,...,SP> (persistent, LDS-DMA, "
+                      "v_mfma_f32_16x16x32_f16, one product per term)",
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+            "basis": f"f16 MFMA work per launch ({work / 1e9:.1f} GFLOP) / launch time / dense peak",
+            "avg_launch_ms": round(gemm_ms, 4), "launches": launches, "flops_per_launch": work,
+            "algorithmic_bytes_per_launch": 36 * (T6 * 1024 * 2 * 2 + T6 * 1024 * 4),
+            "whole_conv": {"what": "nsm_wino_input_f16 + nsm_wino_gemm_f16 + nsm_wino_output_bf16",
+                           "avg_ms": round(conv_ms, 4),
+                           "pipe_frac": round(work / (conv_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4),
+                           "direct_equiv_tflops": round(alg_flops / (conv_ms * 1e-3) / 1e12, 1),
+                           "direct_conv_flops": alg_flops, "direct_conv_bytes": alg_bytes}}
+
+
 def direct_roofline(B, H, W, kern_ms, launches):
     """Roofline object of conv6.conv.0 forward as one bf16 implicit GEMM
     (M = B*(H/8)*(W/8) pixels, N = 1024, K = 9*1024)."""
@@ -579,9 +608,12 @@ def train_measure(args, world, rank, dev):
     full = (H, W, C) == (512, 512, 7)
     pipe_mult, peak = pipe_products(bf16)
     if bf16:
-        work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30)
-        roof = direct_roofline(B, H, W, kern_ms, len(evs))
-        traffic, traffic_src = (load_traffic("traffic_conv6_fwd_bf16.json") if B == 64 and full
+        from nsm_amd.prep import BF16_WINO, BF16_WINO_MIN
+        work = stage_work(C, H, W, B, bytes_per=2, wino_min=BF16_WINO_MIN if BF16_WINO else 1 << 30)
+        roof = (wino_f16_roofline(B, H, W, kern_ms, gemm_ms, len(evs)) if BF16_WINO and gemm_ms
+                else direct_roofline(B, H, W, kern_ms, len(evs)))
+        traffic, traffic_src = (load_traffic("traffic_conv6_fwd_gemm_bf16.json" if BF16_WINO
+                                             else "traffic_conv6_fwd_bf16.json") if B == 64 and full
                                 else (None, None))
         tag = f"b{B}_bf16"
     else:

@@ -360,8 +360,11 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     V = torch.empty(36 * T * cin_p, dtype=H2, device=x.device)
     call("nsm_wino_input_f16", ptr(x), x.stride(0), B, H, W, cin_p, 4, ptr(V), ptr(amax[0]), st)
     Mb = empty(36 * T * cout_p, device=x.device)
+    evg = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
     call("nsm_wino_gemm_f16", ptr(V), ptr(U), B, H, W, cin_p, cout_p, 4, ptr(Mb), ptr(amax[0]),
          wino_beta(4, 0), ptr(amax[1]), wino_beta(4, 2), st)
+    if evg is not None:
+        evg.record()
     if not keep_v:
         V = None
     y = torch.empty(B * H * W, cout_p, dtype=BF16, device=x.device)

@@ -37,6 +37,11 @@ KINDS = {
     "bf16": (lambda r: "gemm_bf16_dma_kernel<256, 256" in r["Kernel_Name"]
              and "ConvActDma" in r["Kernel_Name"] and grid_blocks(r)[:2] in ((4, 1024), (1024, 4)),
              False),
+    # the bf16 path's F(4x4) forward (round 4): input transform + the
+    # single-plane persistent GEMM + output transform
+    "bf16_wino": (lambda r: ("gemm_h2p_kernel<256, 256" in r["Kernel_Name"]
+                             or "gemm_h2q_kernel<256, 256" in r["Kernel_Name"])
+                  and r["Kernel_Name"].rstrip().endswith("true>"), True),
 }
 
 kind, path, outp = sys.argv[1], sys.argv[2], sys.argv[3]

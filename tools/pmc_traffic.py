@@ -50,6 +50,23 @@ KINDS = {
                  desc="conv6.conv.0 fwd bf16 LDS-DMA implicit GEMM, B=64: gemm_bf16_dma_kernel"
                       "<256,256,...,ConvActDma,RowsKDma,EpiStoreB> grid 4x1024 (M=262144 N=1024 "
                       "K=9216)"),
+    # round 4: the bf16 path's conv6 forward is Winograd F(4x4) on f16 operands
+    # (input transform + the single-plane persistent GEMM + output transform)
+    "bf16_wino": dict(match=lambda n: ("gemm_h2p_kernel<256, 256" in n or "gemm_h2q_kernel<256, 256" in n)
+                      and n.rstrip().endswith("true>"),
+                      grid=(256 * 512, 64 * 4 * 36 * 512), triple=True,
+                      alg=(2 * 262144 * 1024 + 9 * 1024 * 1024) * 2,
+                      desc="conv6.conv.0 fwd as a whole on the bf16 path, B=64: wino_input_f16 + "
+                           "gemm_h2p_kernel<256,256,...,SP> + wino_output_kernel<4,...,bf16>; "
+                           "algorithmic bytes = x + y + weights of the direct conv (bf16)"),
+    "bf16_wino_gemm": dict(match=lambda n: ("gemm_h2p_kernel<256, 256" in n
+                                            or "gemm_h2q_kernel<256, 256" in n)
+                           and n.rstrip().endswith("true>"),
+                           grid=(256 * 512, 64 * 4 * 36 * 512), triple=False,
+                           alg=36 * (16384 * 1024 * 2 + 1024 * 1024 * 2 + 16384 * 1024 * 4),
+                           desc="conv6.conv.0 fwd's F(4x4) batched GEMM alone on the bf16 path, B=64 "
+                                "(36 x M=16384 N=1024 K=1024, single-plane f16 V, U; fp32 M): "
+                                "algorithmic bytes = V + U read + M written"),
 }
 FWD = [c for c, n in CODES.items() if n == "conv6.fwd"][0]
 

@@ -55,8 +55,10 @@ fi
 if [ "$WHICH" != f32 ]; then
   ARGS="--dtype bf16 --batch 64"
   run b64_bf16
-  python3 tools/conv6_trace.py bf16 "$OUT/mtrace_b64_bf16.csv" "profiles/$R/trace_conv6_fwd_bf16.json"
-  python3 tools/pmc_traffic.py bf16 "profiles/$R/traffic_conv6_fwd_bf16.json" \
+  python3 tools/conv6_trace.py bf16_wino "$OUT/mtrace_b64_bf16.csv" "profiles/$R/trace_conv6_fwd_bf16.json"
+  python3 tools/pmc_traffic.py bf16_wino "profiles/$R/traffic_conv6_fwd_bf16.json" \
+      "$OUT/rdreq_b64_bf16.csv" "$OUT/fetch_b64_bf16.csv" "$OUT/write_b64_bf16.csv"
+  python3 tools/pmc_traffic.py bf16_wino_gemm "profiles/$R/traffic_conv6_fwd_gemm_bf16.json" \
       "$OUT/rdreq_b64_bf16.csv" "$OUT/fetch_b64_bf16.csv" "$OUT/write_b64_bf16.csv"
 fi
 mkdir -p "$OUT/profiles_copy"
