@@ -41,7 +41,7 @@ KINDS = {
     # single-plane persistent GEMM + output transform
     "bf16_wino": (lambda r: ("gemm_h2p_kernel<256, 256" in r["Kernel_Name"]
                              or "gemm_h2q_kernel<256, 256" in r["Kernel_Name"])
-                  and r["Kernel_Name"].rstrip().endswith("true>"), True),
+                  and ", true>" in r["Kernel_Name"], True),
 }
 
 kind, path, outp = sys.argv[1], sys.argv[2], sys.argv[3]

@@ -53,7 +53,7 @@ KINDS = {
     # round 4: the bf16 path's conv6 forward is Winograd F(4x4) on f16 operands
     # (input transform + the single-plane persistent GEMM + output transform)
     "bf16_wino": dict(match=lambda n: ("gemm_h2p_kernel<256, 256" in n or "gemm_h2q_kernel<256, 256" in n)
-                      and n.rstrip().endswith("true>"),
+                      and ", true>" in n,
                       grid=(256 * 512, 64 * 4 * 36 * 512), triple=True,
                       alg=(2 * 262144 * 1024 + 9 * 1024 * 1024) * 2,
                       desc="conv6.conv.0 fwd as a whole on the bf16 path, B=64: wino_input_f16 + "
@@ -61,7 +61,7 @@ KINDS = {
                            "algorithmic bytes = x + y + weights of the direct conv (bf16)"),
     "bf16_wino_gemm": dict(match=lambda n: ("gemm_h2p_kernel<256, 256" in n
                                             or "gemm_h2q_kernel<256, 256" in n)
-                           and n.rstrip().endswith("true>"),
+                           and ", true>" in n,
                            grid=(256 * 512, 64 * 4 * 36 * 512), triple=False,
                            alg=36 * (16384 * 1024 * 2 + 1024 * 1024 * 2 + 16384 * 1024 * 4),
                            desc="conv6.conv.0 fwd's F(4x4) batched GEMM alone on the bf16 path, B=64 "
