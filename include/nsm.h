@@ -205,6 +205,19 @@ int nsm_wino_gemm_f16(const void* V, const void* U, int B, int H, int W, int cin
 int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int cout_p, int tile,
                          const float* bias, void* y, int ldy, float* partial, int nslot,
                          void* stream);
+/* The same GEMM / output transform with M held as f16 (half the bytes of the
+ * GEMM's writes and the output transform's reads): nsm_wino_gemm_f16m writes
+ * M16 [36][T][cout_p] f16 scaled by 2^-(15 + ceil log2 cin_p) in the operands'
+ * scaled units (a static bound: |M16| <= 2^15, no maximum pass);
+ * nsm_wino_output_bf16m takes the same scale slots / bounds and cin_p to undo
+ * it. NSM_BF16_M16 selects this pair in the Python path. */
+int nsm_wino_gemm_f16m(const void* V, const void* U, int B, int H, int W, int cin_p, int cout_p,
+                       int tile, void* M16, const uint32_t* amax_v, float beta_v,
+                       const uint32_t* amax_u, float beta_u, void* stream);
+int nsm_wino_output_bf16m(const void* M16, int B, int H, int W, int cin_p, int cout_p, int tile,
+                          const uint32_t* amax_v, float beta_v, const uint32_t* amax_u,
+                          float beta_u, const float* bias, void* y, int ldy, float* partial,
+                          int nslot, void* stream);
 /* Its weight gradient: dM = s (A dY A^T) of the bf16 output gradient dY as
  * [36][T][c_p] f16 (amax_dy: max|dY| from dY's producer, beta =
  * nsm_wino_beta(4, 1)); then dw [cout][cin][3][3] from dM and the forward's V

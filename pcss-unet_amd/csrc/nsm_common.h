@@ -208,6 +208,14 @@ __device__ __forceinline__ f32x2 unpack_h2(uint32_t w) {
   return __builtin_convertvector(__builtin_bit_cast(f16x2, w), f32x2);
 }
 
+// f16 Winograd M of the bf16 path (nsm_conv_h2.inc, O16): 15 + ceil log2 K
+__device__ __forceinline__ int o16_exp(int K) {
+  return 15 + (K > 1 ? 32 - __builtin_clz((unsigned)(K - 1)) : 0);
+}
+__device__ __forceinline__ u32x2 pack_f16x4(f32x4 v) {
+  return u32x2{pack_h2(f32x2{v.x, v.y}), pack_h2(f32x2{v.z, v.w})};
+}
+
 __device__ __forceinline__ void split4h(f32x4 v, float s, u32x2& h, u32x2& l) {
   const f32x2 a = f32x2{v.x, v.y} * s, b = f32x2{v.z, v.w} * s;
   h = u32x2{pack_h2(a), pack_h2(b)};

@@ -1524,19 +1524,34 @@ struct WinoAct {
   int ldres;
 };
 
+// M16: M is the f16 output of the O16 GEMM (nsm_wino_gemm_f16m), scaled by
+// 2^(e_v + e_u - o16_exp(K)) against the true M
+struct WinoM16 {
+  H2Scale sv, su;
+  int K;
+};
+
 // The column pass streams M's rows (wcol_row: wmat2's bits with one row
 // live): F(6x6) 138 -> 128 VGPRs, 3 -> 4 waves per SIMD
 // BFO (the bf16 path, nsm_wino_output_bf16): y holds bf16; the BN partials are
 // of the bf16-rounded outputs, as the direct bf16 convolution's epilogue
-template <int MT, bool STATS, bool ACT = false, bool BFO = false>
+template <int MT, bool STATS, bool ACT = false, bool BFO = false, bool M16 = false>
 __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
                                                           int W, int TH, int TW, long long T,
                                                           const float* __restrict__ bias,
                                                           float* __restrict__ y, int ldy,
                                                           float* __restrict__ partial,
-                                                          WinoAct act = WinoAct{}) {
+                                                          WinoAct act = WinoAct{},
+                                                          WinoM16 m16 = WinoM16{}) {
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
+  static_assert(!M16 || (BFO && CW == 4), "f16 M: the bf16 path's F(4x4)");
+  float msc = 1.f;  // every lane reads the scale slots (wave reduction) before the loop
+  if constexpr (M16) {
+    int e = o16_exp(m16.K) - h2_exp(m16.sv);
+    e = e < -126 ? -126 : (e > 126 ? 126 : e);
+    msc = exp2i(e) * exp2i(-h2_exp(m16.su));
+  }
   const int N4 = N / CW;
   const long long total = T * N4;
   const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1551,12 +1566,21 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
     const long long b = r / TH;
     const size_t plane = (size_t)T * N;
     const float* in = Mb + (size_t)t * N + c;
+    const bf16_t* in16 = (const bf16_t*)Mb + (size_t)t * N + c;
     VT sc[MT][A], o[MT][MT];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       VT row[A];
 #pragma unroll
-      for (int e = 0; e < A; ++e) row[e] = *(const VT*)(in + (a * A + e) * plane);
+      for (int e = 0; e < A; ++e) {
+        if constexpr (M16) {
+          const u32x2 h = *(const u32x2*)(in16 + (a * A + e) * plane);
+          const f32x2 lo = unpack_h2(h.x), hi = unpack_h2(h.y);
+          row[e] = VT{lo.x, lo.y, hi.x, hi.y} * msc;
+        } else {
+          row[e] = *(const VT*)(in + (a * A + e) * plane);
+        }
+      }
       wcol_row<CAt<MT>>(sc, row, a);
     }
 #pragma unroll
@@ -3260,6 +3284,56 @@ extern "C" int nsm_wino_gemm_f16(const void* V, const void* U, int B, int H, int
                 "wino_gemm_f16: operand too large");
   return wino_gemm_f16((const bf16_t*)V, (const bf16_t*)U, g.T, cin_p, cout_p, g.alpha2, Mb,
                        H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, as_stream(stream));
+}
+
+// the same GEMM writing M as f16 (O16: scale 2^-(15 + ceil log2 cin_p) in the
+// operands' scaled units; M16 [alpha^2][T][cout_p] f16, half of Mb's bytes)
+extern "C" int nsm_wino_gemm_f16m(const void* V, const void* U, int B, int H, int W, int cin_p,
+                                  int cout_p, int tile, void* M16, const uint32_t* amax_v,
+                                  float beta_v, const uint32_t* amax_u, float beta_u, void* stream) {
+  NSM_CHECK_ARG(V && U && M16 && amax_v && amax_u && cin_p % 128 == 0 && cout_p % 128 == 0,
+                "wino_gemm_f16m: bad args (cin_p, cout_p multiples of 128)");
+  NSM_CHECK_ARG(((uintptr_t)V % 16) == 0 && ((uintptr_t)U % 16) == 0 && ((uintptr_t)M16 % 16) == 0,
+                "wino_gemm_f16m: 16B alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_gemm_f16m: bad tile or shape");
+  NSM_CHECK_ARG(g.T * cin_p < (1ll << 30) && g.T * cout_p < (1ll << 30) &&
+                    (long long)cout_p * cin_p < (1ll << 30),
+                "wino_gemm_f16m: operand too large");
+  return wino_gemm_f16((const bf16_t*)V, (const bf16_t*)U, g.T, cin_p, cout_p, g.alpha2, (float*)M16,
+                       H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, as_stream(stream), true);
+}
+
+// the output transform of nsm_wino_gemm_f16m's f16 M (same scale slots / bounds
+// as the GEMM call, cin_p its K) writing bf16 Y (+ the BN partials)
+extern "C" int nsm_wino_output_bf16m(const void* M16, int B, int H, int W, int cin_p, int cout_p,
+                                     int tile, const uint32_t* amax_v, float beta_v,
+                                     const uint32_t* amax_u, float beta_u, const float* bias,
+                                     void* y, int ldy, float* partial, int nslot, void* stream) {
+  NSM_CHECK_ARG(M16 && y && amax_v && amax_u && tile == 4 && cin_p > 0 && cout_p % 32 == 0 &&
+                    ldy % 4 == 0,
+                "wino_output_bf16m: bad args (tile 4 only)");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_bf16m: bad shape");
+  dim3 grid(grid_1d(g.T * (cout_p / 4)));
+  if (partial) {
+    NSM_CHECK_ARG(nslot > 0 && nslot % wino_stat_step(cout_p, tile) == 0 && nslot <= (1 << 20),
+                  "wino_output_bf16m: nslot %d not a multiple of %d", nslot,
+                  wino_stat_step(cout_p, tile));
+    grid = dim3((unsigned)((long long)nslot * (cout_p / 4) / 256));
+  }
+  const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, cin_p};
+  hipStream_t s = as_stream(stream);
+  if (partial)
+    hipLaunchKernelGGL((wino_output_kernel<4, true, false, true, true>), grid, dim3(256), 0, s,
+                       (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, partial,
+                       WinoAct{}, m16);
+  else
+    hipLaunchKernelGGL((wino_output_kernel<4, false, false, true, true>), grid, dim3(256), 0, s,
+                       (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, nullptr,
+                       WinoAct{}, m16);
+  NSM_LAUNCH_CHECK("wino_output_bf16m");
+  return 0;
 }
 
 // the output transform writing bf16 Y (+ the BN partials of the rounded values)

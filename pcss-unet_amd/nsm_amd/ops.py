@@ -344,11 +344,18 @@ def conv3x3_wgrad_wino_f16(dM, V, B, H, W, cin_p, cout_p, cin, cout, dw, amax, t
         ev.record()
 
 
-def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, keep_v=False):
+# NSM_BF16_M16=0: the bf16 path's Winograd M in fp32 instead of f16
+BF16_M16 = os.environ.get("NSM_BF16_M16", "1") != "0"
+
+
+def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, keep_v=False,
+                     m16=None):
     """The bf16 path's 3x3 (pad 1) forward by Winograd F(4x4,3x3) on single-plane
     scaled f16 operands (nsm_wino_input_f16 / _gemm_f16 / _output_bf16): x
     [B*H*W, cin_p] bf16, U the prep-kind-6 filters [36][cout_p][cin_p] f16,
-    amax = (max|x| slot filled by x's producer, max|w| slot of the prep).
+    amax = (max|x| slot filled by x's producer, max|w| slot of the prep);
+    m16 (default NSM_BF16_M16): M between the GEMM and the output transform
+    as f16 (nsm_wino_gemm_f16m / _output_bf16m) instead of fp32.
     Returns (y bf16 [B*H*W, cout_p], Partials of the rounded y | None) and,
     with keep_v, V (the weight gradient's operand)."""
     from ._lib import lib
@@ -359,10 +366,12 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     ev = _probe(tag)
     V = torch.empty(36 * T * cin_p, dtype=H2, device=x.device)
     call("nsm_wino_input_f16", ptr(x), x.stride(0), B, H, W, cin_p, 4, ptr(V), ptr(amax[0]), st)
-    Mb = empty(36 * T * cout_p, device=x.device)
+    m16 = BF16_M16 if m16 is None else m16
+    bv, bu = wino_beta(4, 0), wino_beta(4, 2)
+    Mb = torch.empty(36 * T * cout_p, dtype=H2 if m16 else torch.float32, device=x.device)
     evg = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
-    call("nsm_wino_gemm_f16", ptr(V), ptr(U), B, H, W, cin_p, cout_p, 4, ptr(Mb), ptr(amax[0]),
-         wino_beta(4, 0), ptr(amax[1]), wino_beta(4, 2), st)
+    call("nsm_wino_gemm_f16m" if m16 else "nsm_wino_gemm_f16", ptr(V), ptr(U), B, H, W, cin_p,
+         cout_p, 4, ptr(Mb), ptr(amax[0]), bv, ptr(amax[1]), bu, st)
     if evg is not None:
         evg.record()
     if not keep_v:
@@ -372,8 +381,13 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     part = None
     if nslot > 0:
         part = Partials(empty(nslot * 3 * cout_p, device=x.device), nslot, 0)
-    call("nsm_wino_output_bf16", ptr(Mb), B, H, W, cout_p, 4, ptr(bias), ptr(y), y.stride(0),
-         ptr(part.buf) if part is not None else None, nslot, st)
+    pb = ptr(part.buf) if part is not None else None
+    if m16:
+        call("nsm_wino_output_bf16m", ptr(Mb), B, H, W, cin_p, cout_p, 4, ptr(amax[0]), bv,
+             ptr(amax[1]), bu, ptr(bias), ptr(y), y.stride(0), pb, nslot, st)
+    else:
+        call("nsm_wino_output_bf16", ptr(Mb), B, H, W, cout_p, 4, ptr(bias), ptr(y), y.stride(0),
+             pb, nslot, st)
     if ev is not None:
         ev.record()
     return (y, part, V) if keep_v else (y, part)

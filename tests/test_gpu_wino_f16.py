@@ -36,9 +36,10 @@ def _prep_u(ops, w, cin_p, cout_p, device):
     return U, am
 
 
+@pytest.mark.parametrize("m16", [False, True])
 @pytest.mark.parametrize("B,H,W,ci,co", [(2, 32, 32, 512, 512), (1, 37, 29, 512, 1024),
                                         (4, 16, 16, 1024, 512), (64, 8, 8, 512, 1024)])
-def test_conv3x3_wino_f16_vs_direct_bf16(device, B, H, W, ci, co):
+def test_conv3x3_wino_f16_vs_direct_bf16(device, B, H, W, ci, co, m16):
     from nsm_amd import ops
     g = torch.Generator().manual_seed(B * H + W + ci)
     x = torch.randn(B, ci, H, W, generator=g) * torch.pow(2.0, torch.rand(1, ci, 1, 1, generator=g) * 4 - 2)
@@ -51,7 +52,7 @@ def test_conv3x3_wino_f16_vs_direct_bf16(device, B, H, W, ci, co):
     ax = ops.amax_slots(1, device)
     ops.absmax(xd.float(), ax)   # (x's producer records it in the model path)
     U, au = _prep_u(ops, w.to(device).contiguous(), ci, co, device)
-    y, part = ops.conv3x3_wino_f16(xd, B, H, W, U, b.to(device), co, amax=(ax, au))
+    y, part = ops.conv3x3_wino_f16(xd, B, H, W, U, b.to(device), co, amax=(ax, au), m16=m16)
     wp = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_FWD, torch.bfloat16)
     y0 = ops.conv_fwd(xd, B, H, W, wp, b.to(device), co, 3)
     torch.cuda.synchronize()
@@ -60,7 +61,8 @@ def test_conv3x3_wino_f16_vs_direct_bf16(device, B, H, W, ci, co):
     e0 = (y0.double().cpu() - r)
     rms1, rms0 = e1.pow(2).mean().sqrt().item(), e0.pow(2).mean().sqrt().item()
     mx1, mx0 = e1.abs().max().item(), e0.abs().max().item()
-    print(f"wino f16 rms {rms1:.3e} max {mx1:.3e} | direct bf16 rms {rms0:.3e} max {mx0:.3e}")
+    print(f"wino f16 (M16 {m16}) rms {rms1:.3e} max {mx1:.3e} | direct bf16 rms {rms0:.3e} "
+          f"max {mx0:.3e} | ratio {rms1 / rms0:.3f} {mx1 / mx0:.3f}")
     assert rms1 <= 1.5 * rms0 and mx1 <= 2.0 * mx0, (rms1, rms0, mx1, mx0)
     if part is not None:
         bn = torch.nn.BatchNorm2d(co).to(device)
