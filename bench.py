@@ -335,22 +335,27 @@ def wino_f16_roofline(B, H, W, conv_ms, gemm_ms, launches):
     gemm_h2p_kernel's single-plane mode (ONE f16 product per fp32-accumulated
     term: the pipe work equals the Winograd products), HIP events per launch.
     whole_conv adds the input / output transforms and the direct-conv rate."""
+    from nsm_amd.ops import BF16_M16
     h6, w6 = H // 8, W // 8
     T6 = B * ((h6 + 3) // 4) * ((w6 + 3) // 4)
     work = 36 * 2.0 * T6 * 1024 * 1024
     alg_flops = conv_flops(B, h6, w6, 1024, 1024, 3)
     alg_bytes = (2 * B * h6 * w6 * 1024 + 9 * 1024 * 1024) * 2
     achieved = work / (gemm_ms * 1e-3) / 1e12
+    m_bytes = 2 if BF16_M16 else 4   # M written as f16 (nsm_wino_gemm_f16m) or fp32
     return {"kernel": f"conv6.conv.0.fwd bf16 path: Winograd F(4x4,3x3) batched GEMM (36 x M={T6} "
                       f"N=1024 K=1024) on single-plane scaled f16 operands, B={B} at {h6}x{w6}: "
                       "gemm_h2p_kernel<256,256,...,SP> (persistent, LDS-DMA, "
-                      "v_mfma_f32_16x16x32_f16, one product per term)",
+                      "v_mfma_f32_16x16x32_f16, one product per term; M written as "
+                      + ("f16)" if BF16_M16 else "fp32)"),
             "bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
             "basis": f"f16 MFMA work per launch ({work / 1e9:.1f} GFLOP) / launch time / dense peak",
             "avg_launch_ms": round(gemm_ms, 4), "launches": launches, "flops_per_launch": work,
-            "algorithmic_bytes_per_launch": 36 * (T6 * 1024 * 2 * 2 + T6 * 1024 * 4),
-            "whole_conv": {"what": "nsm_wino_input_f16 + nsm_wino_gemm_f16 + nsm_wino_output_bf16",
+            # V + U read, M written
+            "algorithmic_bytes_per_launch": 36 * (T6 * 1024 * 2 + 1024 * 1024 * 2 + T6 * 1024 * m_bytes),
+            "whole_conv": {"what": "nsm_wino_input_f16 + nsm_wino_gemm_f16" + ("m" if BF16_M16 else "")
+                                   + " + nsm_wino_output_bf16" + ("m" if BF16_M16 else ""),
                            "avg_ms": round(conv_ms, 4),
                            "pipe_frac": round(work / (conv_ms * 1e-3) / 1e12 / BF16_PEAK_TFLOPS, 4),
                            "direct_equiv_tflops": round(alg_flops / (conv_ms * 1e-3) / 1e12, 1),

@@ -63,9 +63,10 @@ KINDS = {
                                             or "gemm_h2q_kernel<256, 256" in n)
                            and ", true>" in n,
                            grid=(256 * 512, 64 * 4 * 36 * 512), triple=False,
-                           alg=36 * (16384 * 1024 * 2 + 1024 * 1024 * 2 + 16384 * 1024 * 4),
+                           alg=36 * (16384 * 1024 * 2 + 1024 * 1024 * 2 + 16384 * 1024 * 2),
                            desc="conv6.conv.0 fwd's F(4x4) batched GEMM alone on the bf16 path, B=64 "
-                                "(36 x M=16384 N=1024 K=1024, single-plane f16 V, U; fp32 M): "
+                                "(36 x M=16384 N=1024 K=1024, single-plane f16 V, U; f16 M, "
+                                "nsm_wino_gemm_f16m): "
                                 "algorithmic bytes = V + U read + M written"),
 }
 FWD = [c for c, n in CODES.items() if n == "conv6.fwd"][0]
