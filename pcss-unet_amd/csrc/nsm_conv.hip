@@ -3431,6 +3431,22 @@ extern "C" int nsm_wino_dout_f16(const void* dy, int lddy, int B, int H, int W, 
 // the weight-gradient plan of the f16 path: the h2 plan's, on its 256 / 128 tiles
 static WinoWgradPlan plan_wino_wgrad_f16(long long T, int cin_p, int cout_p, int nb) {
   WinoWgradPlan p = plan_wino_wgrad_h2(T, cin_p, cout_p, nb);
+  // NSM_F16_WG_SPLITS: K splits of the 256x256 tiles (A/B)
+  static const long long force = [] {
+    const char* e = getenv("NSM_F16_WG_SPLITS");
+    return e ? atoll(e) : 0ll;
+  }();
+  if (force > 0 && p.BM == 256 && p.BN == 256) {
+    long long sp = force, maxs = (T + 255) / 256;
+    if (sp > maxs) sp = maxs;
+    long long kc = (T + sp - 1) / sp;
+    kc = (kc + BK - 1) / BK * BK;
+    sp = (T + kc - 1) / kc;
+    p.splits = (int)sp;
+    p.kchunk = (int)kc;
+    p.slab_floats = (size_t)nb * sp * cout_p * cin_p;
+    if (sp > 1) p.slab_floats += (size_t)nb * cout_p * cin_p;
+  }
   if ((p.BM == 256 && p.BN == 256) || (p.BM == 128 && p.BN == 128)) return p;
   // (the h2 planner's smaller tiles: 128 x 128 with its ~512-block split)
   p.BM = p.BN = 128;
