@@ -211,6 +211,12 @@ int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int cout_p, int t
  * scaled units (a static bound: |M16| <= 2^15, no maximum pass);
  * nsm_wino_output_bf16m takes the same scale slots / bounds and cin_p to undo
  * it. NSM_BF16_M16 selects this pair in the Python path. */
+/* Both F(4x4) transforms of the bf16 output gradient dY from one read: V
+ * (the input gradient's operand, as nsm_wino_input_f16 of dY) and dM (as
+ * nsm_wino_dout_f16), scale source amax_dy for both. NSM_BF16_DUAL selects it
+ * in the Python path. */
+int nsm_wino_dual_f16(const void* dy, int lddy, int B, int H, int W, int c_p, int tile, void* V,
+                      void* dM, const uint32_t* amax_dy, void* stream);
 int nsm_wino_gemm_f16m(const void* V, const void* U, int B, int H, int W, int cin_p, int cout_p,
                        int tile, void* M16, const uint32_t* amax_v, float beta_v,
                        const uint32_t* amax_u, float beta_u, void* stream);

@@ -2118,6 +2118,75 @@ __device__ __forceinline__ void wino_weight_item_f16(const float* __restrict__ w
 
 constexpr int PREP_ITEMS = NSM_PREP_ITEMS;  // items per block, 2 per thread (8: -0.2 % step, more tail)
 
+// U of one (n, k) item, unscaled (flip: the input gradient's filters)
+template <int MT>
+__device__ __forceinline__ void wino_weight_u(const float* __restrict__ w, int cout, int cin, int k_p,
+                                              int flip, int idx, float (&u)[MT + 2][MT + 2]) {
+  const int k = idx % k_p, n = idx / k_p;
+  const int co = flip ? k : n, ci = flip ? n : k;
+  float g[3][3];
+  const bool ok = co < cout && ci < cin;
+#pragma unroll
+  for (int a = 0; a < 3; ++a)
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+      const int sa = flip ? 2 - a : a, sb = flip ? 2 - b : b;
+      g[a][b] = ok ? w[((size_t)co * cin + ci) * 9 + sa * 3 + sb] : 0.f;
+    }
+  wmat2<CG<MT>>(g, u);
+}
+
+// A block's U items (kinds 4 and 6, phase 1) with 16-B stores: each thread
+// transforms its item, 16 planes at a time go through LDS ([plane][item]),
+// then each store task takes 8 consecutive items (k) of one plane and writes
+// their h and l chunks (h2, kind 4: the 8h / 8l of one channel chunk) or their
+// 8 f16 (kind 6). One item per thread wrote 2-B (kind 6) or lane-paired 4-B
+// (h2_write) words: 64 (36) store instructions per item. items % 8 == 0
+// (k_p % 32), so a group of 8 is wholly inside or outside the job.
+template <int MT, bool SPL>
+__device__ void wino_weight_block(const NsmPrepJob& j, long long lbase, long long items, float s,
+                                  float* __restrict__ stg) {
+  constexpr int A = MT + 2, NPL = A * A, CH = 16;
+  const int cout = j.a[0], cin = j.a[1], n_p = j.a[2], k_p = j.a[3], flip = j.a[4];
+  bf16_t* U = (bf16_t*)j.dst;
+  const int cols = SPL ? k_p : 2 * k_p;  // f16 row length of U
+  const size_t plane = (size_t)n_p * cols;
+  for (int r = 0; r < PREP_ITEMS / 256; ++r) {
+    const long long lr = lbase + r * 256;
+    if (lr >= items) break;  // uniform
+    const long long li = lr + threadIdx.x;
+    float u[A][A];
+    wino_weight_u<MT>(j.src, cout, cin, k_p, flip, li < items ? (int)li : 0, u);
+#pragma unroll
+    for (int c0 = 0; c0 < NPL; c0 += CH) {
+      __syncthreads();  // the previous chunk's LDS reads are done
+#pragma unroll
+      for (int q = 0; q < CH; ++q)
+        if (c0 + q < NPL) stg[q * 256 + threadIdx.x] = u[(c0 + q) / A][(c0 + q) % A] * s;
+      __syncthreads();
+      for (int t = threadIdx.x; t < CH * 32; t += 256) {
+        const int pl = t >> 5, grp = t & 31;
+        const long long l0 = lr + 8 * grp;
+        if (c0 + pl >= NPL || l0 >= items) continue;
+        const int n = (int)(l0 / k_p), k0 = (int)(l0 - (long long)n * k_p);
+        const f32x4 a = *(const f32x4*)&stg[pl * 256 + 8 * grp];
+        const f32x4 b = *(const f32x4*)&stg[pl * 256 + 8 * grp + 4];
+        bf16_t* o = U + (size_t)(c0 + pl) * plane + (size_t)n * cols + (SPL ? k0 : 2 * k0);
+        if constexpr (SPL) {
+          *(u32x4*)o = u32x4{pack_h2(f32x2{a.x, a.y}), pack_h2(f32x2{a.z, a.w}),
+                             pack_h2(f32x2{b.x, b.y}), pack_h2(f32x2{b.z, b.w})};
+        } else {
+          u32x2 ha, la, hb, lb;
+          split4h(a, 1.f, ha, la);
+          split4h(b, 1.f, hb, lb);
+          *(u32x4*)o = u32x4{ha.x, ha.y, hb.x, hb.y};
+          *(u32x4*)(o + 8) = u32x4{la.x, la.y, lb.x, lb.y};
+        }
+      }
+    }
+  }
+}
+
 // blockIdx -> job by a (uniform) binary search over the jobs' first blocks
 // (job.base / PREP_ITEMS: every job starts on a block boundary, see
 // nsm_prep_items), then the block's items of that job, coalesced
@@ -2125,8 +2194,11 @@ constexpr int PREP_ITEMS = NSM_PREP_ITEMS;  // items per block, 2 per thread (8:
 // j.amax (the scale source of the U they write in phase 1, beta = wino_beta G),
 // the h2 packs (kind 5) max|w| of theirs (beta 1); every other job waits for
 // phase 1
+// (phase bit 1: the U jobs by wino_weight_block, NSM_PREP_WIDE)
 __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __restrict__ jobs,
                                                            int njobs, int phase) {
+  const bool wide = (phase & 2) != 0;
+  phase &= 1;
   const long long blk0 = (long long)blockIdx.x * PREP_ITEMS;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
@@ -2189,6 +2261,21 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
     }
     const float s = exp2i(h2_exp(H2Scale{j.amax, wino_beta(j.a[5], 2)}));
     bf16_t* U = (bf16_t*)j.dst;
+    if (wide) {
+      __shared__ __attribute__((aligned(16))) float stg[16 * 256];
+      const long long lb = blk0 - j.base;
+      if (j.kind == 6) {
+        if (j.a[5] == 4) wino_weight_block<4, true>(j, lb, items, s, stg);
+        else wino_weight_block<2, true>(j, lb, items, s, stg);
+      } else if (j.a[5] == 6) {
+        wino_weight_block<6, false>(j, lb, items, s, stg);
+      } else if (j.a[5] == 4) {
+        wino_weight_block<4, false>(j, lb, items, s, stg);
+      } else {
+        wino_weight_block<2, false>(j, lb, items, s, stg);
+      }
+      return;
+    }
     for (int r = 0; r < PREP_ITEMS / 256; ++r) {
       const long long li = blk0 - j.base + r * 256 + threadIdx.x;
       if (li >= items) break;
@@ -2306,9 +2393,13 @@ extern "C" int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long
   NSM_CHECK_ARG(total_items / PREP_ITEMS < (1ll << 31), "prep_weights: too many items");
   // phase 0 (the max|w| pass of the h2 jobs, kinds 4 and 5) only where the
   // table holds such jobs (max_pass): otherwise every block of it would return
+  static const bool wide = [] {  // NSM_PREP_WIDE=1: the U jobs by wino_weight_block
+    const char* e = getenv("NSM_PREP_WIDE");
+    return e && atoi(e) != 0;
+  }();
   for (int phase = max_pass ? 0 : 1; phase < 2; ++phase)
     hipLaunchKernelGGL(prep_weights_kernel, dim3((unsigned)(total_items / PREP_ITEMS)), dim3(256), 0,
-                       as_stream(stream), jobs_dev, njobs, phase);
+                       as_stream(stream), jobs_dev, njobs, phase | (wide && phase ? 2 : 0));
   NSM_LAUNCH_CHECK("prep_weights");
   return 0;
 }
@@ -3425,6 +3516,99 @@ extern "C" int nsm_wino_dout_f16(const void* dy, int lddy, int B, int H, int W, 
                      as_stream(stream), (const bf16_t*)dy, lddy, H, W, c_p, g.TH, g.TW, g.T,
                      (bf16_t*)dM, H2Scale{amax_dy, wino_beta(4, 1)});
   NSM_LAUNCH_CHECK("wino_dout_f16");
+  return 0;
+}
+
+// both F(4x4) transforms of the bf16 output gradient dY from one read of its
+// patches (the fp32 path's wino_dual_kernel): V [alpha^2][T][C] f16 = s_v B^T
+// d B of the 6x6 patch (the input gradient's operand, zero padding) and dM =
+// s_d A dY A^T of its 4x4 interior (the weight gradient's), both scales from
+// max|dY| (betas 0 and 1). wino_input_f16 + wino_dout_f16 read dY twice.
+template <int MT>
+__global__ void __launch_bounds__(256) wino_dual_f16_kernel(const bf16_t* __restrict__ dy, int ld,
+                                                            int H, int W, int C, int TH, int TW,
+                                                            long long T, bf16_t* __restrict__ V,
+                                                            bf16_t* __restrict__ dM, H2Scale hv,
+                                                            H2Scale hd) {
+  constexpr int A = MT + 2;
+  const int C4 = C / 4;
+  const long long total = T * C4;
+  // every lane (amax_read: a wave reduction)
+  const float sv = exp2i(h2_exp(hv)), sd = exp2i(h2_exp(hd));
+  const size_t plane = (size_t)T * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const long long t = i / C4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    u32x2 raw[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
+        const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        raw[a][e] = *(const u32x2*)(dy + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
+        if (!in) raw[a][e] = u32x2{0u, 0u};
+      }
+    {
+      f32x4 sc[A][A];
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        f32x4 d[A];
+#pragma unroll
+        for (int e = 0; e < A; ++e) d[e] = bf4_to_f32(raw[a][e]);
+        wcol_row<CBt<MT>>(sc, d, a);
+      }
+      bf16_t* out = V + (size_t)t * C + c;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        f32x4 v[A];
+        wmat<CBt<MT>>(sc[a], v);
+#pragma unroll
+        for (int e = 0; e < A; ++e)
+          *(u32x2*)(out + (a * A + e) * plane) =
+              __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * sv, f16x4v));
+      }
+    }
+    f32x4 sc[A][MT];
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      f32x4 d[MT];
+#pragma unroll
+      for (int e = 0; e < MT; ++e) d[e] = bf4_to_f32(raw[a + 1][e + 1]);
+      wcol_row<CA<MT>>(sc, d, a);
+    }
+    bf16_t* out = dM + (size_t)t * C + c;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      f32x4 v[A];
+      wmat<CA<MT>>(sc[a], v);
+#pragma unroll
+      for (int e = 0; e < A; ++e)
+        *(u32x2*)(out + (a * A + e) * plane) =
+            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * sd, f16x4v));
+    }
+  }
+}
+
+extern "C" int nsm_wino_dual_f16(const void* dy, int lddy, int B, int H, int W, int c_p, int tile,
+                                 void* V, void* dM, const uint32_t* amax_dy, void* stream) {
+  NSM_CHECK_ARG(dy && V && dM && amax_dy && tile == 4 && c_p % 32 == 0 && lddy % 4 == 0 &&
+                    lddy >= c_p,
+                "wino_dual_f16: bad args (tile 4 only)");
+  NSM_CHECK_ARG(((uintptr_t)dy % 8) == 0 && ((uintptr_t)V % 16) == 0 && ((uintptr_t)dM % 16) == 0,
+                "wino_dual_f16: alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_dual_f16: bad shape");
+  hipLaunchKernelGGL(wino_dual_f16_kernel<4>, dim3(grid_1d(g.T * c_p / 4)), dim3(256), 0,
+                     as_stream(stream), (const bf16_t*)dy, lddy, H, W, c_p, g.TH, g.TW, g.T,
+                     (bf16_t*)V, (bf16_t*)dM, H2Scale{amax_dy, wino_beta(4, 0)},
+                     H2Scale{amax_dy, wino_beta(4, 1)});
+  NSM_LAUNCH_CHECK("wino_dual_f16");
   return 0;
 }
 

@@ -330,6 +330,19 @@ def wino_dout_f16(dy, B, H, W, amax_dy):
     return dM
 
 
+def wino_dual_f16(dy, B, H, W, amax_dy):
+    """(V, dM) of the bf16 output gradient from one read (nsm_wino_dual_f16):
+    V as conv3x3_wino_f16's input transform of dy (the input gradient's
+    operand, its v_in), dM as wino_dout_f16(dy)."""
+    c_p = dy.shape[1]
+    n = 36 * wino_tiles(B, H, W, 4) * c_p
+    V = torch.empty(n, dtype=H2, device=dy.device)
+    dM = torch.empty(n, dtype=H2, device=dy.device)
+    call("nsm_wino_dual_f16", ptr(dy), dy.stride(0), B, H, W, c_p, 4, ptr(V), ptr(dM), ptr(amax_dy),
+         stream())
+    return V, dM
+
+
 def conv3x3_wgrad_wino_f16(dM, V, B, H, W, cin_p, cout_p, cin, cout, dw, amax, tag=None):
     """dw [cout, cin, 3, 3] of the bf16 path's F(4x4) 3x3 from dM (wino_dout_f16)
     and the forward's V (conv3x3_wino_f16(keep_v=True)); amax = (max|dY| slot,
@@ -349,13 +362,14 @@ BF16_M16 = os.environ.get("NSM_BF16_M16", "1") != "0"
 
 
 def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, keep_v=False,
-                     m16=None):
+                     m16=None, v_in=None):
     """The bf16 path's 3x3 (pad 1) forward by Winograd F(4x4,3x3) on single-plane
     scaled f16 operands (nsm_wino_input_f16 / _gemm_f16 / _output_bf16): x
     [B*H*W, cin_p] bf16, U the prep-kind-6 filters [36][cout_p][cin_p] f16,
     amax = (max|x| slot filled by x's producer, max|w| slot of the prep);
     m16 (default NSM_BF16_M16): M between the GEMM and the output transform
-    as f16 (nsm_wino_gemm_f16m / _output_bf16m) instead of fp32.
+    as f16 (nsm_wino_gemm_f16m / _output_bf16m) instead of fp32; v_in: V
+    already formed from x (wino_dual_f16), the input transform skipped.
     Returns (y bf16 [B*H*W, cout_p], Partials of the rounded y | None) and,
     with keep_v, V (the weight gradient's operand)."""
     from ._lib import lib
@@ -364,8 +378,11 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     T = wino_tiles(B, H, W, 4)
     st = stream()
     ev = _probe(tag)
-    V = torch.empty(36 * T * cin_p, dtype=H2, device=x.device)
-    call("nsm_wino_input_f16", ptr(x), x.stride(0), B, H, W, cin_p, 4, ptr(V), ptr(amax[0]), st)
+    if v_in is not None:
+        V = v_in
+    else:
+        V = torch.empty(36 * T * cin_p, dtype=H2, device=x.device)
+        call("nsm_wino_input_f16", ptr(x), x.stride(0), B, H, W, cin_p, 4, ptr(V), ptr(amax[0]), st)
     m16 = BF16_M16 if m16 is None else m16
     bv, bu = wino_beta(4, 0), wino_beta(4, 2)
     Mb = torch.empty(36 * T * cout_p, dtype=H2 if m16 else torch.float32, device=x.device)

@@ -63,6 +63,10 @@ LAZY_DY1_H2 = os.environ.get("NSM_LAZY_DY1_H2", "1") != "0"
 # NSM_WGRAD_F16=0: the bf16 path's F(4x4) layers take their weight gradient
 # from the direct implicit GEMM instead of the Winograd domain (dM x V)
 WGRAD_F16 = os.environ.get("NSM_WGRAD_F16", "1") != "0"
+# NSM_BF16_DUAL=1: with WGRAD_F16, the bf16 output gradient's two F(4x4)
+# transforms (the input gradient's V, the weight gradient's dM) from one read
+# of dY1 (ops.wino_dual_f16) instead of wino_input_f16 + wino_dout_f16
+BF16_DUAL = os.environ.get("NSM_BF16_DUAL", "0") != "0"
 # NSM_EVAL_FUSED=0: eval forward with separate BN-apply passes instead of the
 # BN + LeakyReLU (+ skip) in the conv epilogues (nsm_conv_fwd_act)
 EVAL_FUSED = os.environ.get("NSM_EVAL_FUSED", "1") != "0"
@@ -738,7 +742,10 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
                               amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)),
                               tag=name + ".conv.0.dgrad")[0]
     elif s.Vf16 is not None:   # bf16 F(4x4): dY's transform, then the Winograd-domain GEMMs
-        dM = ops.wino_dout_f16(dY1, B, H, W, am_dy1)
+        if need_dx and BF16_DUAL:   # with the input gradient's V, from one read of dY1
+            Vd, dM = ops.wino_dual_f16(dY1, B, H, W, am_dy1)
+        else:
+            dM = ops.wino_dout_f16(dY1, B, H, W, am_dy1)
         ops.conv3x3_wgrad_wino_f16(dM, s.Vf16, B, H, W, s.cip, s.cip, ci, ci, g[c0.weight],
                                    amax=(am_dy1, _slot(s.am, AM_X)), tag=name + ".conv.0.wgrad")
         s.Vf16 = None
@@ -756,7 +763,7 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
     if _wino_f16(s):   # bf16: Winograd F(4x4) on f16 operands, as the forward
         return ops.conv3x3_wino_f16(dY1, B, H, W, s.pw.Uf16(True), None, s.cip,
                                     amax=(am_dy1, s.pw.amax_Uf16()), stats=False,
-                                    tag=name + ".conv.0.dgrad")[0]
+                                    tag=name + ".conv.0.dgrad", v_in=Vd)[0]
     w1d = s.pw.w1(ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad",
                         amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)))

@@ -105,3 +105,24 @@ def test_wgrad_wino_f16_vs_direct_bf16(device, B, H, W, c):
     rms1, rms0 = e1.pow(2).mean().sqrt().item(), e0.pow(2).mean().sqrt().item()
     print(f"wgrad wino f16 rms {rms1:.3e} | direct bf16 rms {rms0:.3e} | ref rms {r.pow(2).mean().sqrt().item():.3e}")
     assert rms1 <= 2.0 * rms0, (rms1, rms0)
+
+
+@pytest.mark.parametrize("B,H,W,c", [(2, 32, 32, 512), (1, 37, 29, 128), (3, 13, 22, 256)])
+def test_wino_dual_f16_matches_separate_transforms(device, B, H, W, c):
+    """nsm_wino_dual_f16 (one read of dY) writes exactly the V of
+    nsm_wino_input_f16 and the dM of nsm_wino_dout_f16 (same arithmetic,
+    same scale slot), ragged edges included."""
+    from nsm_amd import ops
+    g = torch.Generator().manual_seed(B * H * W + c)
+    dy = (torch.randn(B * H * W, c, generator=g) * 1e-3).to(torch.bfloat16).to(device)
+    am = ops.amax_slots(1, device)
+    ops.absmax(dy.float(), am)
+    V, dM = ops.wino_dual_f16(dy, B, H, W, am)
+    V0 = torch.empty_like(V)
+    ops.call("nsm_wino_input_f16", ops.ptr(dy), dy.stride(0), B, H, W, c, 4, ops.ptr(V0), ops.ptr(am),
+             ops.stream())
+    dM0 = ops.wino_dout_f16(dy, B, H, W, am)
+    torch.cuda.synchronize()
+    assert torch.equal(V.view(torch.int16), V0.view(torch.int16))
+    assert torch.equal(dM.view(torch.int16), dM0.view(torch.int16))
+    assert V.abs().max().item() > 0 and dM.abs().max().item() > 0
