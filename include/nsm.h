@@ -161,6 +161,10 @@ int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int W, int cin
  * zeroed first; NaN counts above +Inf): the maximum a GEMM operand needs when
  * its producer does not record it. */
 int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
+/* the same over n bf16 values (x 16-B aligned): the input maximum of a bf16
+ * F(4x4) Winograd conv whose input producer records none (the decoder's lazy
+ * resampling, NSM_LAZY_DECODER=1) */
+int nsm_absmax_bf16(const void* x, int64_t n, uint32_t* out, void* stream);
 /* ---- pre-split ("h2") Winograd operands (csrc/nsm_conv_h2.inc) -------------
  * An h2 tensor is an fp32 [rows][C] matrix X stored as fp16 [rows][2C]: with
  * s = 2^(15 - ceil(log2(beta * m))), m = the max of the operand-maximum slot

@@ -47,6 +47,22 @@ def lr_lambda(warmup_epochs, num_epochs):
     return f
 
 
+FLT_MAX = 3.4028234663852886e38
+
+
+def fp32_norm(t):
+    """torch.norm of an fp32 gradient as the reference's device computes it
+    (main.py:95, CUDA): the squares accumulate in fp32, so a sum of squares
+    above FLT_MAX (a norm above ~1.8e19) reads +inf. Below that the value is
+    torch.norm's. (Some hosts' CPU kernels sum in double and return a finite
+    norm up to FLT_MAX; this restatement fixes the fp32 behaviour so the
+    decision does not depend on the host.)"""
+    n = torch.norm(t)
+    if torch.isfinite(n) and t.double().pow(2).sum().item() > FLT_MAX:
+        return torch.tensor(float("inf"))
+    return n
+
+
 def sanitize_and_clip(params, epoch, num_epochs, scale=1.0, noise=None):
     """Apply main.py:287-418 to `params` (each with .grad) in place.
     Returns True when the reference would skip the optimizer step. `noise`
@@ -93,7 +109,7 @@ def sanitize_and_clip(params, epoch, num_epochs, scale=1.0, noise=None):
     if math.isfinite(scale):
         for p in params:
             if p.grad is not None:
-                n = torch.norm(p.grad.data)
+                n = fp32_norm(p.grad.data)
                 p.grad.data.mul_(torch.clamp(torch.tensor(1.0 / max(1.0, n / (1000.0 * scale))),
                                              max=1.0))
     # unscale_ (a no-op multiply by 1/scale when the scaler is disabled)
@@ -107,7 +123,7 @@ def sanitize_and_clip(params, epoch, num_epochs, scale=1.0, noise=None):
             continue
         if torch.isnan(p.grad).any() or torch.isinf(p.grad).any():
             return True
-        n = torch.norm(p.grad)
+        n = fp32_norm(p.grad)
         if n > 1e3:
             if n > 1e5:
                 return True

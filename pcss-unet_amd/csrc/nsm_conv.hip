@@ -2644,6 +2644,15 @@ extern "C" int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream
   return 0;
 }
 
+extern "C" int nsm_absmax_bf16(const void* x, int64_t n, uint32_t* out, void* stream) {
+  NSM_CHECK_ARG(x && out && n > 0 && ((uintptr_t)x % 16) == 0, "absmax_bf16: bad args");
+  const long long g = std::min<long long>(ceil_div(n, 2048), 2048);
+  hipLaunchKernelGGL(absmax_bf16_kernel, dim3((int)g), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)x, (long long)n, out);
+  NSM_LAUNCH_CHECK("absmax_bf16");
+  return 0;
+}
+
 extern "C" int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int W, int cin_p,
                                int cout_p, int tile, float* Mb, const uint32_t* amax_v,
                                const uint32_t* amax_u, void* stream) {

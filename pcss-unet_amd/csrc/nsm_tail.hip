@@ -17,6 +17,7 @@
 // separate fp32 products, exactly like the three mul_ calls), and AdamW is
 // torch's single-tensor AdamW. FP contraction is off in this file so no FMA
 // merges two of those roundings.
+#include <cfloat>
 #include <math.h>
 
 #include "nsm_common.h"
@@ -316,8 +317,11 @@ __global__ void __launch_bounds__(1024) tail_finalize_kernel(
       }
     }
     if (lane == 0) {
-      // torch.norm of an fp32 tensor accumulates in double on the CPU, rounds to fp32
-      const float n1 = (float)sqrt(s2);
+      // the fp32 norm: the squares are summed in double and rounded to fp32,
+      // except that a sum of squares above FLT_MAX reads +inf, as an fp32
+      // accumulation of them does (the reference's device, main.py:95,
+      // torch.norm on CUDA; and the CPU kernels of most hosts)
+      const float n1 = s2 > (double)FLT_MAX ? __builtin_inff() : (float)sqrt(s2);
       // main.py:365: g *= clamp(1 / max(1, |g| / (1000*scale)), max=1)
       const float t = n1 / (float)(1000.0 * (double)scale);
       float f1 = t > 1.f ? 1.f / t : 1.f;
@@ -325,15 +329,11 @@ __global__ void __launch_bounds__(1024) tail_finalize_kernel(
       // main.py:368 unscale_ (x 1/scale), then :371-397 on the unscaled grad
       const float inv_s = (float)(1.0 / (double)scale);
       float n2 = (n1 * f1) * inv_s;
-      // The tail follows the arithmetic of the reference's CPU path, the
-      // oracle of this port (scale 1, main.py:175): torch.norm of an fp32
-      // tensor sums the squares in double there, so the fp32 norm is +inf only
-      // when the norm itself exceeds FLT_MAX (finite values, |g| > 3.4e38).
+      // A norm above ~1.8e19 (sum of squares > FLT_MAX) reads +inf (above).
       // Then the reference's factor 1/max(1, inf) = 0 zeroes the gradient,
       // whose norm is 0 and the step goes on (main.py:361-365); inf * 0 is NaN
-      // here. (On CUDA torch sums the squares in fp32 and a norm above ~1.8e19
-      // already reads inf; a norm between the two is rescaled to 1000 here, as
-      // on the CPU: tests/test_gpu_tail.py::test_large_finite_norm_rescales_like_cpu.)
+      // here, so n2 is set to 0 (tests/test_gpu_tail.py::
+      // test_large_finite_norm_zeroes_like_fp32_norm).
       if (n1 == __builtin_inff()) n2 = 0.f;
       // a non-finite survivor of the repair (:374-381) is impossible once
       // zeroed; only an infinite norm (overflowed sum of squares) is left

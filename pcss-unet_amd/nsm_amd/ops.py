@@ -75,18 +75,25 @@ def amax_slots(n, device):
 
 
 def amax_slot(buf, i):
-    """Slot i of an amax_slots buffer (None -> None)."""
-    return None if buf is None else buf[i * AMAX_WORDS:(i + 1) * AMAX_WORDS]
+    """Slot i of an amax_slots buffer (None -> None). A slot past the buffer's
+    end raises: its pointer would aim the kernels' atomics outside it."""
+    if buf is None:
+        return None
+    s = buf[i * AMAX_WORDS:(i + 1) * AMAX_WORDS]
+    if s.numel() != AMAX_WORDS:
+        raise IndexError(f"amax slot {i} outside a buffer of {buf.numel() // AMAX_WORDS} slots")
+    return s
 
 
 def absmax(x, out=None):
     """Operand-maximum slot holding max|x| (nsm_absmax): the f16x2 GEMM
     operand scale of a tensor whose producer did not record it."""
-    if x.dtype != F32:   # the kernel reads fp32 words
-        raise TypeError(f"absmax: fp32 tensor expected, got {x.dtype}")
+    if x.dtype not in (F32, BF16):
+        raise TypeError(f"absmax: fp32 or bf16 tensor expected, got {x.dtype}")
     if out is None:
         out = amax_slots(1, x.device)
-    call("nsm_absmax", ptr(x), x.numel(), ptr(out), stream())
+    call("nsm_absmax_bf16" if x.dtype == BF16 else "nsm_absmax", ptr(x), x.numel(), ptr(out),
+         stream())
     return out
 
 

@@ -149,6 +149,7 @@ class StepWeights:
         # scales), zeroed by run() before the prep launch refills them
         self.amax = ops.amax_slots(max(n_wino, 1), dev)
         n_am = 0
+        first = min(shapes)   # the block whose input the forward writes (conv2)
 
         def add(kind, a, src, shape_numel, out_dtype, amax=None):
             nonlocal base
@@ -203,8 +204,12 @@ class StepWeights:
                                                  torch.float32, amax=am)
             else:
                 # the direct 3x3 (conv2) of the fp32 train step on h2 operands:
-                # kind-5 packs, the DGRAD job sharing the FWD job's max|w| slot
-                h2_3x3 = h2 and training and H2_1X1
+                # kind-5 packs, the DGRAD job sharing the FWD job's max|w| slot.
+                # Only the first block: its input is the one written as h2
+                # (ops.input_prep_h2); a later direct 3x3 (NSM_WINOGRAD=0 or a
+                # raised NSM_WINO_MIN) reads the fp32 output of the block before
+                h2_3x3 = h2 and training and H2_1X1 and k == first
+
                 wf16 = bf16_wino(cip, dtype, training)
                 if wf16:   # Winograd F(4x4) forward: single-plane f16 U (kind 6)
                     am = ops.amax_slot(self.amax, n_am)
@@ -251,6 +256,9 @@ class StepWeights:
                     pb.t[("w2", mode)] = add(pk, (co, ci, 1, cop, cip, mode), c4.weight, cop * cip,
                                              dtype, amax=am)
             self.blocks[k] = pb
+        # every slot handed out lies inside self.amax (a slice past its end
+        # would aim the producers' atomics outside the buffer)
+        assert n_am <= max(n_wino, 1), (n_am, n_wino)
         self.total = base
         self.njobs = len(jobs)
         # the max|w| pass (phase 0) runs only for the h2 jobs' scale sources

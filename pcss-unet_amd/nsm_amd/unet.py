@@ -648,10 +648,11 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         # dY1 is never stored and the GEMM never recomputed, under the bound
         # the finalize derives from max|k1 dz| (AM_DY1B)
         lazy = h2 and need_dx and LAZY_DY1_H2
-        recompute = not lazy and bnb_mode(s.cip, s.cop, dtype, h2=True) == 2
         # a direct 3x3 on h2 operands (conv2) takes dY1 as h2 too, written by
-        # the BN backward with the bound its finalize derives (AM_DY1B)
-        h2_3x3 = s.X is not None and s.X.dtype == ops.H2 and not recompute
+        # the BN backward with the bound its finalize derives (AM_DY1B); the
+        # recompute form (mode 2) writes fp32 dY1, so it is not used there
+        h2_3x3 = s.X is not None and s.X.dtype == ops.H2
+        recompute = not lazy and not h2_3x3 and bnb_mode(s.cip, s.cop, dtype, h2=True) == 2
         if h2_3x3 or lazy:
             am_dy1 = _slot(s.am, AM_DY1B)
         dY1 = ops.conv1x1_dgrad_bn_bwd_h2(dY2h, HW, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
@@ -895,6 +896,10 @@ class _UnetFn(torch.autograd.Function):
                     up = ops.resize_act(cur, B, h, w, h2, w2, SLOPE)
                 else:                      # match is the identity (bitwise, as in ATen)
                     up = ops.resize(cur, B, h, w, h2, w2)
+                if lazy and up is not None and amax is not None:
+                    # the lazy resampling kernels record no maximum: block k's
+                    # input-maximum slot (the bf16 F(4x4) V scale) from up itself
+                    ops.absmax(up, _x_slot(amax, k))
                 ups[k] = (h, w, h2, w2, th, tw)
                 res = c[SKIP_OF[k]] if k in SKIP_OF else None
                 s = _block_fwd(mod.block(k), up, B, th, tw, training, masks.get(k), f"conv{k}",

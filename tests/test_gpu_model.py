@@ -195,10 +195,17 @@ def _rel(a, b):
     return np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
 
 
+@pytest.mark.parametrize("lazy_decoder", [False, True])
 @pytest.mark.parametrize("name", ["train_c7_p0_b2_64", "train_c4_drop_b2_64"])
-def test_train_fixture_bf16(device, name):
+def test_train_fixture_bf16(device, name, lazy_decoder, monkeypatch):
+    """bf16 train step vs the reference's own bf16-autocast deviation; with
+    lazy_decoder (NSM_LAZY_DECODER=1) the decoder inputs come from the lazy
+    resampling kernels, and the F(4x4) conv6/conv7 must still get their input
+    maximum (the V scale)."""
     import nsm_amd
+    from nsm_amd import unet as U
     from util import is_pre_bn_bias
+    monkeypatch.setattr(U, "LAZY_DECODER", lazy_decoder)
     fx = load(name)
     in_ch, p = int(fx["meta/in_ch"]), float(fx["meta/dropout"])
     masks = {int(k.split("/")[1]): torch.from_numpy(fx[k]) for k in fx if k.startswith("mask/")}

@@ -153,6 +153,36 @@ def test_split_train_step_vs_oracle(ops, device):
         assert errs[mode][1] <= 2.0 * errs[0][1] + 1e-6
 
 
+@pytest.mark.parametrize("wino_min", [1 << 30, 256])
+def test_train_step_direct_3x3_blocks_vs_oracle(ops, device, monkeypatch, wino_min):
+    """fp32 training with some or all 3x3 convs on the direct implicit GEMM
+    (NSM_WINOGRAD=0 / a raised NSM_WINO_MIN): only conv2, whose input the
+    forward writes as h2, takes the h2 direct path; conv3.. read the fp32
+    output of the block before and keep fp32 packs. Output, loss
+    and weight grads of a 1x7x128x128 step vs the CPU oracle."""
+    from oracle import unet_ref as O
+    from oracle.weights import make_state, synthetic_batch
+    from nsm_amd import CustomLoss, Unet
+    from nsm_amd import unet as U
+    monkeypatch.setattr(U, "WINOGRAD_MIN_CHANNELS", wino_min)
+    np_sd = make_state(7, 43)
+    x_np, y_np = synthetic_batch(1, 7, 128, 128)
+    sd = O.torch_state(np_sd, requires_grad=True)
+    oo, _ = O.forward(sd, torch.from_numpy(x_np), True, None, 0.0)
+    O.custom_loss(oo, torch.from_numpy(y_np), 0.9).backward()
+    m = Unet(in_ch=7, dropout_rate=0.0)
+    m.load_state_dict({k: torch.from_numpy(v.copy()) for k, v in np_sd.items()})
+    m = m.to(device).train()
+    out = m(torch.from_numpy(x_np).to(device).requires_grad_(True))
+    CustomLoss(device, 0.9)(out, torch.from_numpy(y_np).to(device)).backward()
+    torch.cuda.synchronize()
+    oe = (out.detach().cpu() - oo.detach()).abs().max().item()
+    ge = max(((p.grad.cpu().double() - sd[k].grad.double()).norm() / sd[k].grad.double().norm()).item()
+             for k, p in m.named_parameters() if not k.endswith("bias"))
+    print(f"wino_min {wino_min}: out {oe:.2e} grad rel {ge:.2e}")
+    assert oe <= 1e-4 and ge <= 2e-2, (oe, ge)
+
+
 def _h2(ops, t, rows, C, amax, beta):
     """fp32 [rows][C] -> h2 tensor (nsm_to_h2) with scale source (amax, beta)."""
     from nsm_amd._lib import call, ptr, stream

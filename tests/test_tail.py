@@ -102,3 +102,12 @@ def test_flat_adamw_checkpoint_format_is_torch_adamw():
     back.load_state_dict(out)
     assert back.param_groups[0]["lr"] == 1e-3
     assert torch.equal(back.state_dict()["state"][1]["exp_avg"], sd["state"][1]["exp_avg"])
+
+
+def test_fp32_norm_overflow_edge():
+    """The oracle's fp32 norm (step_tail_ref.fp32_norm): torch.norm's value below
+    the fp32 sum-of-squares overflow, +inf above it (~1.8e19) on every host."""
+    g = torch.tensor([3.0, -4.0])
+    assert T.fp32_norm(g).item() == torch.norm(g).item() == 5.0
+    assert torch.isinf(T.fp32_norm(torch.tensor([1e20, -1e20, 1.0])))
+    assert torch.isfinite(T.fp32_norm(torch.tensor([1e19, 1.0])))
