@@ -362,6 +362,33 @@ def wino_f16_roofline(B, H, W, conv_ms, gemm_ms, launches):
                            "direct_conv_flops": alg_flops, "direct_conv_bytes": alg_bytes}}
 
 
+def vgg_roofline(B, H, W, conv_ms, gemm_ms, launches, amax):
+    """Roofline object of the deepest VGG19 conv the perceptual loss runs
+    (features.30, 512->512 3x3 at H/16 x W/16 on the 2B output+target images,
+    customLoss.py:42-90): Winograd F(4x4,3x3), 36 batched GEMMs of T x 512 x
+    512, timed per launch with HIP events. Its operands carry recorded maxima
+    (amax) -> the f16x2 split (3 f16 products per fp32 product), else the
+    bf16 three-way split (6)."""
+    h, w = H // 16, W // 16
+    T = 2 * B * ((h + 3) // 4) * ((w + 3) // 4)
+    ex = 36 * 2.0 * T * 512 * 512
+    mult = 3 if amax else 6
+    work = mult * ex
+    achieved = work / (gemm_ms * 1e-3) / 1e12
+    alg = conv_flops(2 * B, h, w, 512, 512, 3)
+    return {"kernel": f"vgg features.30 fwd: Winograd F(4x4,3x3) batched GEMM (36 x M={T} N=512 "
+                      f"K=512), 2B={2 * B} images at {h}x{w}, fp32 via "
+                      + ("the f16x2 split (3 f16 products)" if amax else
+                         "the exact 3-way bf16 split (6 bf16 products)"),
+            "bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
+            "basis": f"16-bit MFMA work per launch ({mult} x {ex / 1e9:.1f} GFLOP of fp32 products) "
+                     "/ launch time / dense peak",
+            "avg_launch_ms": round(gemm_ms, 4), "launches": launches, "flops_per_launch": work,
+            "whole_conv": {"avg_ms": round(conv_ms, 4),
+                           "direct_equiv_tflops": round(alg / (conv_ms * 1e-3) / 1e12, 1)}}
+
+
 def direct_roofline(B, H, W, kern_ms, launches):
     """Roofline object of conv6.conv.0 forward as one bf16 implicit GEMM
     (M = B*(H/8)*(W/8) pixels, N = 1024, K = 9*1024)."""
@@ -505,6 +532,9 @@ def _summary(r):
         out["dp"] = r["dp"]
     if r["config"]["workload"].startswith(("configs[2]", "configs[3]")):
         out["stages"] = r["stages"]
+    if "vgg_perceptual" in r:
+        out["config"] += "+vgg"
+        out["vgg_perceptual"] = r["vgg_perceptual"]
     if "cpu_baseline" in r:
         out["cpu_baseline"] = r["cpu_baseline"]
     return out
@@ -523,11 +553,15 @@ def secondary_configs(args, world, rank, dev):
     kws = [dict(workload="train", dtype="bf16", batch=64, steps=max(10, args.steps // 5),
                 warmup=3)]
     if world == 1:
+        # the reference-faithful step: CustomLoss with its VGG19 perceptual
+        # term (customLoss.py:137; random-init VGG weights, value unpinned)
+        kws += [dict(workload="train", dtype="f32", batch=8, steps=max(5, args.steps // 10),
+                     warmup=2, vgg=True)]
         kws += [dict(workload="infer1080", dtype="bf16", batch=1, steps=100, warmup=5),
                 dict(workload="infer1080", dtype="f32", batch=1, steps=50, warmup=5),
                 dict(workload="infer256", dtype="f32", batch=1, steps=100, warmup=5)]
     for kw in kws:
-        a = _ap.Namespace(**{**base, **kw, "vgg": False})
+        a = _ap.Namespace(**{**base, "vgg": False, **kw})
         torch.cuda.empty_cache()
         if a.workload == "train":
             r = train_measure(a, world, rank, dev)
@@ -596,6 +630,8 @@ def train_measure(args, world, rank, dev):
         nops.PROBES[st + ".fwd"] = []
         nops.PROBES[st + ".bwd"] = []
     nops.PROBES["vgg.fwd"] = []
+    nops.PROBES["vgg.30"] = []
+    nops.PROBES["vgg.30.gemm"] = []
     dp_tags = ("dp.bn_broadcast", "dp.allreduce_wait")
     for t in dp_tags:
         nops.PROBES[t] = []
@@ -605,6 +641,8 @@ def train_measure(args, world, rank, dev):
     kern_ms = mean_ms(evs)
     gemm_ms = mean_ms(nops.PROBES.pop(probe_tag + ".gemm"))
     vgg_evs = nops.PROBES.pop("vgg.fwd")
+    vgg30 = nops.PROBES.pop("vgg.30")
+    vgg30_gemm = mean_ms(nops.PROBES.pop("vgg.30.gemm"))
     times = {}
     for st in STAGES:
         fw, bw = nops.PROBES.pop(st + ".fwd"), nops.PROBES.pop(st + ".bwd")
@@ -672,7 +710,12 @@ def train_measure(args, world, rank, dev):
         vfl = 2 * B * vgg_fwd_flops(H, W)
         vms = mean_ms(vgg_evs)
         res["vgg_perceptual"] = {"ms": round(vms, 3), "direct_equiv_gflop": round(vfl / 1e9, 1),
-                                 "tflops": round(vfl / (vms * 1e-3) / 1e12, 2)}
+                                 "tflops": round(vfl / (vms * 1e-3) / 1e12, 2),
+                                 "share_of_step": round(vms / (elapsed / args.steps * 1e3), 3)}
+        if vgg30:
+            res["vgg_perceptual"]["roofline"] = vgg_roofline(
+                B, H, W, mean_ms(vgg30), vgg30_gemm, len(vgg30),
+                getattr(getattr(crit, "vgg_loss", None), "f16x2", False))
     return res
 
 

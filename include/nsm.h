@@ -165,6 +165,15 @@ int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
  * F(4x4) Winograd conv whose input producer records none (the decoder's lazy
  * resampling, NSM_LAZY_DECODER=1) */
 int nsm_absmax_bf16(const void* x, int64_t n, uint32_t* out, void* stream);
+/* PMC calibration (tools/pmc_calib.py): one launch moving exactly `bytes`
+ * (a multiple of 4096, < 2 GB) in one access pattern of this library's
+ * kernels, so rocprofv3's byte counters can be checked against a known count:
+ * kind 0 read by global_load_dwordx4, 1 read by LDS-DMA buffer_load ... lds,
+ * 2 write by global_store_dwordx4, 3 write by LDS-staged raw_buffer_store_b128
+ * (the persistent h2 GEMM's fp32 epilogue), 4 write by raw_buffer_store_b64
+ * (its f16-M epilogue), 5 write by 4-B stores, 6 write by 8-B stores. A
+ * read-only kind writes at most one dword per block of 2048 to dst. */
+int nsm_pmc_calib(int kind, const void* src, void* dst, int64_t bytes, void* stream);
 /* ---- pre-split ("h2") Winograd operands (csrc/nsm_conv_h2.inc) -------------
  * An h2 tensor is an fp32 [rows][C] matrix X stored as fp16 [rows][2C]: with
  * s = 2^(15 - ceil(log2(beta * m))), m = the max of the operand-maximum slot

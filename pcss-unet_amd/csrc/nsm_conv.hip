@@ -3703,3 +3703,89 @@ extern "C" int nsm_set_f32_split(int mode) {
   g_f32_split = mode < 0 ? 0 : (mode > 2 ? 2 : mode);
   return prev;
 }
+
+// ---- PMC calibration (tools/pmc_calib.py) -----------------------------------
+// Launches of KNOWN byte counts in the access patterns of this library's
+// kernels, so a rocprofv3 counter (WRITE_SIZE, FETCH_SIZE, TCC_EA0_RDREQ*) can
+// be read against the bytes it should report before it is used on them
+// (MI355X_MICROARCH.md §HBM calibrates only 16-B/lane global loads/stores).
+// kind 0: read-only, global_load_dwordx4 (16 B/lane)
+//      1: read-only, buffer_load ... lds (LDS-DMA, 16 B/lane; the GEMM loaders)
+//      2: write-only, global_store_dwordx4
+//      3: write-only, rows staged in LDS then raw_buffer_store_b128 (the
+//         persistent h2 GEMM's fp32 epilogue)
+//      4: write-only, raw_buffer_store_b64 (its f16-M epilogue)
+//      5: write-only, global_store_dword (4 B/lane)
+//      6: write-only, global_store_dwordx2 (8 B/lane)
+// A read-only kernel writes one dword per block (its checksum) to dst.
+__global__ void __launch_bounds__(256) pmc_calib_kernel(int kind, const u32x4* __restrict__ src,
+                                                        u32x4* __restrict__ dst, long long n16) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[256 * 8];
+  const long long stride = (long long)gridDim.x * 256;
+  const long long i0 = (long long)blockIdx.x * 256 + threadIdx.x;
+  unsigned acc = 0;
+  if (kind == 0) {
+    for (long long i = i0; i < n16; i += stride) {
+      const u32x4 v = src[i];
+      acc ^= v.x ^ v.y ^ v.z ^ v.w;
+    }
+  } else if (kind == 1) {
+    // every wave DMAs 64 x 16 B per trip into its own LDS slice
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)src, (short)0, 0x7FFFFFFF, 0x00020000);
+    bf16_t* my = lds + (threadIdx.x >> 6) * 512;
+    for (long long b = (long long)blockIdx.x * 256; b < n16; b += stride) {
+      // wave-uniform chunk base; the byte offset of this lane's 16 B (< 2 GB)
+      const long long wb = b + (threadIdx.x & ~63);
+      if (wb < n16) {
+        const uint32_t off = (uint32_t)((wb + (threadIdx.x & 63)) * 16);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)my, 16, off, 0, 0, 0);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const u32x4 v = *(const u32x4*)&lds[threadIdx.x * 8];
+    acc = v.x ^ v.y ^ v.z ^ v.w;
+  } else if (kind == 2) {
+    for (long long i = i0; i < n16; i += stride) dst[i] = u32x4{(unsigned)i, 1u, 2u, 3u};
+  } else if (kind == 3 || kind == 4) {
+    // 16 rows x 64 fp32 per wave staged in LDS (as the epilogue), then the
+    // buffer stores of 16 B (kind 3) or of 8 B f16x4 (kind 4) per lane
+    float* stg = (float*)lds + (threadIdx.x >> 6) * 256;
+    const __amdgpu_buffer_rsrc_t r =
+        __builtin_amdgcn_make_buffer_rsrc((void*)dst, (short)0, 0x7FFFFFFF, 0x00020000);
+    const long long per = kind == 3 ? 1 : 2;  // lanes per 16 B of output
+    const long long nl = n16 * per;           // lane-stores in total
+    for (long long i = i0; i < nl; i += stride) {
+      stg[(threadIdx.x & 63) * 4 + 0] = (float)i;
+      __builtin_amdgcn_wave_barrier();
+      const f32x4 v = *(const f32x4*)&stg[(threadIdx.x & 63) * 4];
+      if (kind == 3)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, (uint32_t)(i * 16), 0,
+                                               0);
+      else
+        __builtin_amdgcn_raw_buffer_store_b64(pack_f16x4(v), r, (uint32_t)(i * 8), 0, 0);
+    }
+  } else if (kind == 5) {
+    unsigned* d = (unsigned*)dst;
+    for (long long i = i0; i < n16 * 4; i += stride) d[i] = (unsigned)i;
+  } else if (kind == 6) {
+    u32x2* d = (u32x2*)dst;
+    for (long long i = i0; i < n16 * 2; i += stride) d[i] = u32x2{(unsigned)i, 7u};
+  }
+  if (kind <= 1) {
+    for (int o = 32; o > 0; o >>= 1) acc ^= (unsigned)__shfl_xor((int)acc, o);
+    if ((threadIdx.x & 63) == 0 && acc == 0x9E3779B9u) ((unsigned*)dst)[blockIdx.x] = acc;
+  }
+}
+
+extern "C" int nsm_pmc_calib(int kind, const void* src, void* dst, int64_t bytes, void* stream) {
+  NSM_CHECK_ARG(kind >= 0 && kind <= 6 && bytes > 0 && bytes % 4096 == 0 && bytes < (1ll << 31),
+                "pmc_calib: kind 0..6, bytes a multiple of 4096 below 2 GB");
+  NSM_CHECK_ARG(dst && (kind >= 2 || src), "pmc_calib: null pointer");
+  const long long n16 = bytes / 16;
+  hipLaunchKernelGGL(pmc_calib_kernel, dim3(2048), dim3(256), 0, as_stream(stream), kind,
+                     (const u32x4*)src, (u32x4*)dst, n16);
+  NSM_LAUNCH_CHECK("pmc_calib");
+  return 0;
+}

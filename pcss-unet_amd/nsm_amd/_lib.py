@@ -37,6 +37,7 @@ _SIGS = {
     "nsm_wino_gemm_s": (I, [P, P, I, I, I, I, I, I, P, P, P, P]),
     "nsm_absmax": (I, [P, L, P, P]),
     "nsm_absmax_bf16": (I, [P, L, P, P]),
+    "nsm_pmc_calib": (I, [I, P, P, L, P]),
     "nsm_to_h2": (I, [P, L, I, P, F, P, P]),
     "nsm_wino_gemm_h2": (I, [P, P, I, I, I, I, I, I, P, P, F, P, F, P]),
     "nsm_wino_beta": (F, [I, I]),

@@ -26,6 +26,8 @@ reference does at construction — offline, pass a local checkpoint
 randomly initialised (He normal, zero bias): the VALUE is then not the
 reference's (parity-unpinned offline), the work is identical.
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
@@ -36,6 +38,11 @@ from .unet import WINO_TILE
 
 # VGG19's 3x3 convs with >= 128 input channels run Winograd F(4x4,3x3)
 WINOGRAD_MIN_CHANNELS = 128
+# NSM_VGG_F16X2=0: the Winograd GEMMs on the exact three-way bf16 split (6
+# products) instead of the f16x2 split (3 products; fp32 accuracy,
+# nsm_conv_split16.inc) whose operand maxima the input transform (max|V|) and
+# the plan (max|U|, once per weight set) record
+VGG_F16X2 = os.environ.get("NSM_VGG_F16X2", "1") != "0"
 
 VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M",
              512, 512, 512, 512, "M", 512, 512, 512, 512, "M"]
@@ -118,7 +125,8 @@ class MultiLayerVGGLoss(nn.Module):
                 cop = ops.pad32(co)
                 w, b = m.weight.detach().float(), ops.pad_vec(m.bias.detach().float(), cop)
                 if cin_p >= WINOGRAD_MIN_CHANNELS:
-                    op = ("wino", ops.wino_weight(w, cop, cin_p, flip=False, tile=WINO_TILE), b, cop)
+                    U = ops.wino_weight(w, cop, cin_p, flip=False, tile=WINO_TILE)
+                    op = ("wino", U, b, cop, ops.absmax(U) if VGG_F16X2 else None)
                 else:
                     op = ("conv", ops.pack_conv_weight(w, cop, cin_p, ops.PACK_FWD), b, cop)
                 plan.append((idx,) + op)
@@ -149,7 +157,12 @@ class MultiLayerVGGLoss(nn.Module):
         ones = zeros = None
         terms = []
         wts = self._wts
-        for step in self._plan():
+        plan = self._plan()
+        n_w = sum(1 for st in plan if st[1] == "wino")
+        # max|V| of every Winograd conv's input transform (zeroed once per call)
+        am_v = ops.amax_slots(n_w, o.device) if VGG_F16X2 and n_w else None
+        i_w = 0
+        for step in plan:
             idx, kind = step[0], step[1]
             if kind == "conv":
                 _, _, wpk, bias, cop = step
@@ -164,9 +177,11 @@ class MultiLayerVGGLoss(nn.Module):
                                    tag=f"vgg.{idx}")
                 relu = False
             elif kind == "wino":
-                _, _, U, bias, cop = step
+                _, _, U, bias, cop, am_u = step
                 cur = ops.conv3x3_wino(cur, n2, h, w, U, bias, cop, tile=WINO_TILE, relu=relu,
-                                       tag=f"vgg.{idx}")
+                                       tag=f"vgg.{idx}", amax_v=ops.amax_slot(am_v, i_w)
+                                       if am_v is not None else None, amax_u=am_u)
+                i_w += 1
                 relu = False
             elif kind == "relu":
                 relu = True
@@ -178,6 +193,7 @@ class MultiLayerVGGLoss(nn.Module):
                 i = self.feature_layers.index(idx)
                 terms.append(ops.l1_mean(cur[:half], cur[half:], wts[i]))
         self.last_terms = terms        # weighted per-tap terms (device scalars)
+        self.f16x2 = am_v is not None
         total = terms[0]
         for v in terms[1:]:
             total = total + v
