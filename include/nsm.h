@@ -237,6 +237,15 @@ int nsm_wino_output_bf16m(const void* M16, int B, int H, int W, int cin_p, int c
                           const uint32_t* amax_v, float beta_v, const uint32_t* amax_u,
                           float beta_u, const float* bias, void* y, int ldy, float* partial,
                           int nslot, void* stream);
+/* eval: the same output transform writing lrelu(y*act_scale + act_shift,
+ * slope) in bf16 (the DoubleConv's first BatchNorm from its running
+ * statistics + LeakyReLU, Unetmodel.py:22-23, fused; the bf16 eval forward's
+ * F(4x4) layers) */
+int nsm_wino_output_bf16m_act(const void* M16, int B, int H, int W, int cin_p, int cout_p, int tile,
+                              const uint32_t* amax_v, float beta_v, const uint32_t* amax_u,
+                              float beta_u, const float* bias, void* y, int ldy,
+                              const float* act_scale, const float* act_shift, float slope,
+                              void* stream);
 /* Its weight gradient: dM = s (A dY A^T) of the bf16 output gradient dY as
  * [36][T][c_p] f16 (amax_dy: max|dY| from dY's producer, beta =
  * nsm_wino_beta(4, 1)); then dw [cout][cin][3][3] from dM and the forward's V

@@ -1603,8 +1603,11 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
         if (MT * tx + e < W) {
           o[a][e] = o[a][e] + bv;
           if constexpr (BFO) {
-            static_assert(!ACT && std::is_same<VT, f32x4>::value, "bf16 output: F(4x4) / F(2x2)");
-            const VT q = o[a][e];
+            static_assert(std::is_same<VT, f32x4>::value, "bf16 output: F(4x4) / F(2x2)");
+            // ACT (the bf16 eval path): lrelu(BN(y)) from the running statistics,
+            // rounded once to bf16 (the skip add is on the block output, not here)
+            VT q = o[a][e];
+            if constexpr (ACT) q = vlrelu(q * asc + ash, act.slope);
             o[a][e] = VT{round_bf(q.x), round_bf(q.y), round_bf(q.z), round_bf(q.w)};
             st4((bf16_t*)y + ro + (size_t)e * ldy, o[a][e]);
             if (STATS) ts = ts + o[a][e];
@@ -3433,6 +3436,29 @@ extern "C" int nsm_wino_output_bf16m(const void* M16, int B, int H, int W, int c
                        (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, nullptr,
                        WinoAct{}, m16);
   NSM_LAUNCH_CHECK("wino_output_bf16m");
+  return 0;
+}
+
+// eval: the output transform of nsm_wino_gemm_f16m's f16 M writing
+// lrelu(BN(y)) in bf16, BN from the running statistics (act_scale, act_shift:
+// nsm_bn_eval's folded vectors) — the bf16 eval forward's first BatchNorm +
+// LeakyReLU of a DoubleConv (Unetmodel.py:21-23) in the 3x3 conv's epilogue
+extern "C" int nsm_wino_output_bf16m_act(const void* M16, int B, int H, int W, int cin_p, int cout_p,
+                                         int tile, const uint32_t* amax_v, float beta_v,
+                                         const uint32_t* amax_u, float beta_u, const float* bias,
+                                         void* y, int ldy, const float* act_scale,
+                                         const float* act_shift, float slope, void* stream) {
+  NSM_CHECK_ARG(M16 && y && amax_v && amax_u && act_scale && act_shift && tile == 4 && cin_p > 0 &&
+                    cout_p % 32 == 0 && ldy % 4 == 0 && ldy >= cout_p,
+                "wino_output_bf16m_act: bad args (tile 4 only)");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_bf16m_act: bad shape");
+  const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, cin_p};
+  const WinoAct act{act_scale, act_shift, slope, nullptr, 0};
+  hipLaunchKernelGGL((wino_output_kernel<4, false, true, true, true>), dim3(grid_1d(g.T * (cout_p / 4))),
+                     dim3(256), 0, as_stream(stream), (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T,
+                     bias, (float*)y, ldy, nullptr, act, m16);
+  NSM_LAUNCH_CHECK("wino_output_bf16m_act");
   return 0;
 }
 

@@ -369,7 +369,7 @@ BF16_M16 = os.environ.get("NSM_BF16_M16", "1") != "0"
 
 
 def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, keep_v=False,
-                     m16=None, v_in=None):
+                     m16=None, v_in=None, act=None):
     """The bf16 path's 3x3 (pad 1) forward by Winograd F(4x4,3x3) on single-plane
     scaled f16 operands (nsm_wino_input_f16 / _gemm_f16 / _output_bf16): x
     [B*H*W, cin_p] bf16, U the prep-kind-6 filters [36][cout_p][cin_p] f16,
@@ -377,6 +377,8 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     m16 (default NSM_BF16_M16): M between the GEMM and the output transform
     as f16 (nsm_wino_gemm_f16m / _output_bf16m) instead of fp32; v_in: V
     already formed from x (wino_dual_f16), the input transform skipped.
+    act: eval BNState — the output transform writes lrelu(BN(y)) instead of y
+    (nsm_wino_output_bf16m_act; f16 M, no statistics).
     Returns (y bf16 [B*H*W, cout_p], Partials of the rounded y | None) and,
     with keep_v, V (the weight gradient's operand)."""
     from ._lib import lib
@@ -390,7 +392,7 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     else:
         V = torch.empty(36 * T * cin_p, dtype=H2, device=x.device)
         call("nsm_wino_input_f16", ptr(x), x.stride(0), B, H, W, cin_p, 4, ptr(V), ptr(amax[0]), st)
-    m16 = BF16_M16 if m16 is None else m16
+    m16 = (BF16_M16 if m16 is None else m16) or act is not None
     bv, bu = wino_beta(4, 0), wino_beta(4, 2)
     Mb = torch.empty(36 * T * cout_p, dtype=H2 if m16 else torch.float32, device=x.device)
     evg = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
@@ -401,6 +403,14 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     if not keep_v:
         V = None
     y = torch.empty(B * H * W, cout_p, dtype=BF16, device=x.device)
+    if act is not None:
+        assert not stats
+        call("nsm_wino_output_bf16m_act", ptr(Mb), B, H, W, cin_p, cout_p, 4, ptr(amax[0]), bv,
+             ptr(amax[1]), bu, ptr(bias), ptr(y), y.stride(0), ptr(act.scale), ptr(act.shift), 0.2,
+             st)
+        if ev is not None:
+            ev.record()
+        return (y, None, V) if keep_v else (y, None)
     nslot = int(lib.nsm_wino_stat_slots(B, H, W, cout_p, 4)) if stats else 0
     part = None
     if nslot > 0:

@@ -44,12 +44,16 @@ H2_1X1 = os.environ.get("NSM_H2_1X1", "1") != "0"
 # 2.25 x 4 B per output element, bounds the last two)
 BF16_WINO = os.environ.get("NSM_BF16_WINO", "1") != "0"
 BF16_WINO_MIN = int(os.environ.get("NSM_BF16_WINO_MIN", "512"))
+# NSM_BF16_WINO_EVAL=0: the bf16 eval forward (configs[4]'s 1080p bf16 line)
+# keeps its 3x3 convs on the direct implicit GEMM instead of the same F(4x4)
+# f16 Winograd (BN + LeakyReLU in the output transform)
+BF16_WINO_EVAL = os.environ.get("NSM_BF16_WINO_EVAL", "1") != "0"
 
 
 def bf16_wino(cip, dtype, training):
     """True when a DoubleConv's 3x3 forward runs ops.conv3x3_wino_f16."""
-    return (BF16_WINO and training and dtype == torch.bfloat16 and cip >= BF16_WINO_MIN
-            and cip % 128 == 0)
+    return (BF16_WINO and (training or BF16_WINO_EVAL) and dtype == torch.bfloat16
+            and cip >= BF16_WINO_MIN and cip % 128 == 0)
 
 
 class LazyBlockWeights:
@@ -217,9 +221,9 @@ class StepWeights:
                     pb.t["amaxUf16"] = am
                     pb.t["Uf16"] = add(KIND_WINO_F16, (ci, ci, cip, cip, 0, 4, 0), c0.weight,
                                        36 * cip * cip, ops.H2, amax=am)
-                    # the input gradient's filters (flipped; the forward job's max|w| slot)
-                    pb.t["Uf16d"] = add(KIND_WINO_F16, (ci, ci, cip, cip, 1, 4, 1), c0.weight,
-                                        36 * cip * cip, ops.H2, amax=am)
+                    if training:   # the input gradient's filters (flipped; the forward job's slot)
+                        pb.t["Uf16d"] = add(KIND_WINO_F16, (ci, ci, cip, cip, 1, 4, 1), c0.weight,
+                                            36 * cip * cip, ops.H2, amax=am)
                 for mode in modes:
                     if wf16:
                         continue   # forward and input gradient read Uf16 / Uf16d

@@ -497,6 +497,15 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
         A1 = ops.conv3x3_wino(xin, B, H, W, pw.U1(tile, False), b1, cip, tile=tile,
                               tag=name + ".conv.0.fwd", src_hw=src_hw, act=(bn1, None),
                               amax_v=_slot(am, AM_V), amax_u=pw.amax_U1(False))
+    elif _has_f16_u(pw) and am is not None:
+        # bf16 eval: Winograd F(4x4) on f16 operands, BN + LeakyReLU in the
+        # output transform; the V scale from max|x| (the fused epilogues that
+        # wrote x record none)
+        assert src_hw is None
+        ops.absmax(xin, _slot(am, AM_X))
+        A1 = ops.conv3x3_wino_f16(xin, B, H, W, pw.Uf16(), b1, cip,
+                                  amax=(_slot(am, AM_X), pw.amax_Uf16()), stats=False,
+                                  tag=name + ".conv.0.fwd", act=bn1)[0]
     else:
         assert src_hw is None
         A1 = ops.conv_fwd_act(xin, B, H, W, pw.w1(ops.PACK_FWD), b1, cip, 3, bn1, slope=SLOPE,
@@ -555,15 +564,15 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
                                      amax_v=am_v, amax_u=pw.amax_U1(False))
         if training and part1 is None:
             part1 = ops.bn_partials(Y1)
-    elif training and getattr(pw, "Uf16", None) is not None and pw.Uf16() is not None:
+    elif _has_f16_u(pw):
         # bf16: Winograd F(4x4) forward on single-plane scaled f16 operands
-        # (the backward stays on the direct implicit GEMM, which keeps X)
+        keep = WGRAD_F16 and training
         r = ops.conv3x3_wino_f16(X, B, H, W, pw.Uf16(), b1, cip,
-                                 amax=(_slot(am, AM_X), pw.amax_Uf16()),
-                                 tag=name + ".conv.0.fwd", keep_v=WGRAD_F16)
+                                 amax=(_slot(am, AM_X), pw.amax_Uf16()), stats=training,
+                                 tag=name + ".conv.0.fwd", keep_v=keep)
         Y1, part1 = r[0], r[1]
-        Vf16 = r[2] if WGRAD_F16 else None
-        if part1 is None:
+        Vf16 = r[2] if keep else None
+        if training and part1 is None:
             part1 = ops.bn_partials(Y1)
     else:
         w1 = pw.w1(ops.PACK_FWD)
@@ -769,6 +778,11 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
     w1d = s.pw.w1(ops.PACK_DGRAD)
     return ops.conv_fwd(dY1, B, H, W, w1d, None, s.cip, 3, tag=name + ".conv.0.dgrad",
                         amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)))
+
+
+def _has_f16_u(pw):
+    """The block's weight layouts hold the bf16 path's F(4x4) filters."""
+    return getattr(pw, "Uf16", None) is not None and pw.Uf16() is not None
 
 
 def _wino_f16(s):
