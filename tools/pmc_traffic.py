@@ -26,7 +26,12 @@ F32_GEMM = lambda n: ((n.count("RowsKLoader<128, 256>") == 2 and "EpiStore" in n
                        and any(k in n for k in ("gemm_f32_kernel", "gemm_f32s_kernel", "gemm_f32h_kernel")))
                       or (any(k in n for k in ("gemm_h2_kernel<256, 256", "gemm_h2q_kernel<256, 256",
                                                "gemm_h2p_kernel<256, 256"))
-                          and n.count("H2RowsDma<256, 8") >= 2))
+                          and n.count("H2RowsDma<256, 8") >= 2
+                          # not conv6's 1x1 forward GEMM (EpiStoreH): its 128x2 blocks of
+                          # 512 threads equal the persistent grid's 256 x 512 in the PMC
+                          # CSV's thread count, which round 4's summary averaged in
+                          # (profiles/r05/pmc_calibration.json)
+                          and "EpiStoreH" not in n and "EpiBnBwd" not in n))
 # blocks x threads of conv6.conv.0's forward GEMM: the register-path kernels'
 # 8x8x64 blocks of 256 threads, the h2 kernels' 4x4x64 blocks of 512, or the
 # persistent h2 kernel's one block of 512 per CU (256 CUs)
