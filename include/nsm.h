@@ -63,21 +63,25 @@ int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
  * calls). kind 0: pack fp32, 1: pack bf16, a = {cout, cin, taps, cout_p, cin_p,
  * mode}; kind 2: Winograd U, a = {cout, cin, n_p, k_p, flip, tile}; kind 3: pad
  * vector, a = {n, n_p}; kind 4: Winograd U as an h2 tensor [alpha^2][n_p][2 k_p]
- * (nsm_to_h2's layout), a as kind 2, amax (required) = the slot the launch first
- * fills with max|w| of the filters, the scale source of U (beta =
- * nsm_wino_beta(tile, 2)); a[6] = 1: the slot is shared with an earlier kind-4
- * job over the same filters, which fills it (this job only reads it); kind 5:
- * pack as an h2 tensor (a as kind 0; FWD [cout_p][2 taps cin_p], DGRAD
- * [cin_p][2 taps cout_p] float16), amax (required) = the slot the launch first
- * fills with max|w| (beta 1), a[6] = 1: shared with the FWD job of the same
- * weight; kind 6: Winograd U as a single-plane scaled f16 tensor
- * [alpha^2][n_p][k_p] (the bf16 path's F(4x4) forward, nsm_wino_gemm_f16), a
- * and amax as kind 4. `base` = the job's first item in the launch (jobs in
- * ascending base order, consecutive); nsm_prep_items() = the job's extent in
- * the launch (its item count rounded up to whole 512-item blocks: add it to
- * get the next base; total_items = the sum). jobs_dev: a device copy.
- * max_pass: the table holds kind-4 / 5 / 6 jobs (their max|w| pass runs
- * first; 0 skips that launch). */
+ * (nsm_to_h2's layout), a as kind 2, amax (required) = the slot that receives
+ * max|w| of the filters, the scale source of U (beta = nsm_wino_beta(tile, 2));
+ * a[6] = 0, or the first block (base / 512) + 1 of an earlier kind-4 job over
+ * the same filters whose maximum this job shares (same slot); kind 5: pack as
+ * an h2 tensor (a as kind 0; FWD [cout_p][2 taps cin_p], DGRAD [cin_p][2 taps
+ * cout_p] float16), amax (required) = the slot that receives max|w| (beta 1),
+ * a[6] as kind 4 (the FWD job of the same weight); kind 6: Winograd U as a
+ * single-plane scaled f16 tensor [alpha^2][n_p][k_p] (the bf16 path's F(4x4)
+ * forward, nsm_wino_gemm_f16), a and amax as kind 4. `base` = the job's first
+ * item in the launch (jobs in ascending base order, consecutive);
+ * nsm_prep_items() = the job's extent in the launch (its item count rounded up
+ * to whole 512-item blocks: add it to get the next base; total_items = the
+ * sum). jobs_dev: a device copy. max_pass: the table holds kind-4 / 5 / 6 jobs
+ * (their max|w| pass runs first, one word per block into pmax [total_items /
+ * 512], so those slots need no zeroing; their line 0 is stored, lines 1..63
+ * must hold 0). zero0 / zero1 (nzero words each, may be 0): zeroed by the first
+ * launch before anything is written — the step's weight slots (kinds 0 and 2
+ * record max|written| by atomics; kinds 4-6 rely on lines 1..63 = 0) and the
+ * forward's activation slots — so the step needs no fill launches. */
 typedef struct {
   int kind;
   int a[7];
@@ -90,7 +94,8 @@ typedef struct {
 } NsmPrepJob;
 long long nsm_prep_items(const NsmPrepJob* job);
 int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items, int max_pass,
-                     void* stream);
+                     uint32_t* pmax, uint32_t* zero0, int64_t nzero0, uint32_t* zero1,
+                     int64_t nzero1, void* stream);
 
 /* ---- convolution as MFMA implicit GEMM (fp32 in, fp32 accumulate) ----------
  * nsm_conv_fwd: y[p][co] = bias[co] + sum_{tap,ci} pro(x[p+off(tap)][ci]) * W
@@ -230,6 +235,16 @@ int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int cout_p, int t
  * in the Python path. */
 int nsm_wino_dual_f16(const void* dy, int lddy, int B, int H, int W, int c_p, int tile, void* V,
                       void* dM, const uint32_t* amax_dy, void* stream);
+/* nsm_wino_dual_f16 of a dY that is never stored: dY = k1 dz + k2 (y - mean) +
+ * k3, dz = g lrelu'(y scale + shift) mask[b][c], formed per element and rounded
+ * to bf16 as nsm_bn_bwd_apply writes it (g = dA1 of nsm_conv1x1_dgrad_bnbwd
+ * mode 1, y = Y1, coef = the finalize's {k1, k2, k3}), the transforms scaled
+ * from `bound` (nsm_bn_bwd_finalize's dY bound slot). The bf16 path's F(4x4)
+ * layers (Unetmodel.py:21-24 backward); removes the nsm_bn_bwd_apply pass. */
+int nsm_wino_dual_bn_f16(const void* g, int ldg, const void* y, int ldy, int B, int H, int W, int c_p,
+                         int tile, const float* scale, const float* shift, float slope,
+                         const float* mask, const float* mean, const float* coef, void* V, void* dM,
+                         const uint32_t* bound, void* stream);
 int nsm_wino_gemm_f16m(const void* V, const void* U, int B, int H, int W, int cin_p, int cout_p,
                        int tile, void* M16, const uint32_t* amax_v, float beta_v,
                        const uint32_t* amax_u, float beta_u, void* stream);
@@ -651,6 +666,9 @@ int nsm_conv_fwd_bf16(const void* x, int ldx, int B, int H, int W, int cin_p, co
  *   mode 2: out = dY1 = coef0*dz + coef1*(y1-mean) + coef2 (coef from
  *           nsm_bn_bwd_finalize); modes 0 + 2 run the GEMM twice so dA1 never
  *           reaches HBM.
+ * amax_out (may be NULL): mode 2 (fp32) max|dY1| written; modes 0/1 (bf16)
+ * max|scale * dz|, the k1 term of the dY1 bound nsm_bn_bwd_finalize derives
+ * (the scale source of nsm_wino_dual_bn_f16).
  * Replaces ConvolutionBackward(conv.4) + BatchNorm/LeakyReLU/Dropout2d
  * backward of conv.1-3 (autograd of Unetmodel.py:21-26). dtype NSM_F32 | NSM_BF16. */
 int nsm_conv1x1_dgrad_bnbwd(const void* dy2, int lddy2, int B, int H, int W, int cop,

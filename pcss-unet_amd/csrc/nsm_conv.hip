@@ -2192,16 +2192,48 @@ __device__ void wino_weight_block(const NsmPrepJob& j, long long lbase, long lon
 
 // blockIdx -> job by a (uniform) binary search over the jobs' first blocks
 // (job.base / PREP_ITEMS: every job starts on a block boundary, see
-// nsm_prep_items), then the block's items of that job, coalesced
-// phase 0: the h2 Winograd jobs (kind 4) record max|w| of their filters into
-// j.amax (the scale source of the U they write in phase 1, beta = wino_beta G),
-// the h2 packs (kind 5) max|w| of theirs (beta 1); every other job waits for
-// phase 1
+// nsm_prep_items), then the block's items of that job, coalesced.
+// phase 0: zeroes the step's operand-maximum slot buffers (z0, z1: the weight
+// slots this launch fills, the forward's activation slots), and every block of
+// an h2 / f16 job (kinds 4, 5, 6) stores max|w| of its filters as ONE word,
+// pmax[blockIdx.x] (no atomics, so the slots need no zeroing before it);
+// phase 1: such a job reduces the pmax words of its source job's blocks (its
+// own, or those of the job whose filters it shares: a[6] = that job's first
+// block + 1), the job's first block stores the maximum into line 0 of its slot
+// (lines 1..63 stay 0: zeroed in phase 0) for the GEMMs, and all its blocks
+// write with the scale derived from it; kinds 0 and 2 record max|written| by
+// atomics (the slots zeroed in phase 0). Every other job waits for phase 1.
 // (phase bit 1: the U jobs by wino_weight_block, NSM_PREP_WIDE)
+__device__ __forceinline__ uint32_t block_max_u32(uint32_t m, uint32_t* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  m = max(max(red[0], red[1]), max(red[2], red[3]));
+  __syncthreads();
+  return m;
+}
+
+// the h2 exponent of a maximum held as a value (h2_exp's arithmetic)
+__device__ __forceinline__ int h2_exp_of(uint32_t m, float beta) {
+  uint32_t b = __float_as_uint(__uint_as_float(m) * beta);
+  if (m < 0x7f800000u && b >= 0x7f800000u) b = 0x7f7fffffu;
+  return pow2_scale_exp(b);
+}
+
 __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __restrict__ jobs,
-                                                           int njobs, int phase) {
+                                                           int njobs, int phase,
+                                                           uint32_t* __restrict__ pmax,
+                                                           uint32_t* __restrict__ z0, long long nz0,
+                                                           uint32_t* __restrict__ z1, long long nz1) {
+  __shared__ uint32_t red[4];
   const bool wide = (phase & 2) != 0;
   phase &= 1;
+  if (phase == 0) {  // the slot buffers of this step (uniform branch)
+    const long long gs = (long long)gridDim.x * 256, i0 = (long long)blockIdx.x * 256 + threadIdx.x;
+    for (long long i = i0; i < nz0; i += gs) z0[i] = 0u;
+    for (long long i = i0; i < nz1; i += gs) z1[i] = 0u;
+  }
   const long long blk0 = (long long)blockIdx.x * PREP_ITEMS;
   int lo = 0, hi = njobs - 1;
   while (lo < hi) {
@@ -2211,11 +2243,21 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
   const NsmPrepJob& j = jobs[lo];
   const long long items = nsm_prep_items_dev(j);
   uint32_t am = 0;  // max|written| (the f16x2 GEMMs' operand scale, j.amax)
+  const bool h2job = j.kind == 4 || j.kind == 5 || j.kind == 6;
+  uint32_t wmax = 0;  // phase 1 of an h2 job: max|w| of its (source job's) filters
+  if (h2job && phase == 1) {
+    const long long first = j.a[6] ? (long long)j.a[6] - 1 : j.base / PREP_ITEMS;
+    const long long nblk = (items + PREP_ITEMS - 1) / PREP_ITEMS;
+    uint32_t m = 0;
+    for (long long b = threadIdx.x; b < nblk; b += 256) m = max(m, pmax[first + b]);
+    wmax = block_max_u32(m, red);
+    if (blk0 == j.base && threadIdx.x == 0) j.amax[0] = wmax;  // line 0 of the slot
+  }
   if (j.kind == 5) {  // h2 pack (uniform per block): max|w| (phase 0), then h + l (phase 1)
     const int cout = j.a[0], cin = j.a[1], taps = j.a[2], cout_p = j.a[3], cin_p = j.a[4];
     const bool fwd = j.a[5] == NSM_PACK_FWD;
-    if (phase == 0 && j.a[6]) return;  // the FWD job over the same weight fills the slot
-    const float s = phase ? exp2i(h2_exp(H2Scale{j.amax, 1.f})) : 0.f;
+    if (phase == 0 && j.a[6]) return;  // the FWD job over the same weight holds its maximum
+    const float s = phase ? exp2i(h2_exp_of(wmax, 1.f)) : 0.f;
     const int K = taps * (fwd ? cin_p : cout_p);  // row length (fp32 elements)
     bf16_t* out = (bf16_t*)j.dst;
     for (int r = 0; r < PREP_ITEMS / 256; ++r) {
@@ -2241,13 +2283,16 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
         o[8] = __builtin_bit_cast(unsigned short, (_Float16)(a - (float)h));
       }
     }
-    if (phase == 0) amax_flush(am, j.amax);
+    if (phase == 0) {
+      am = block_max_u32(am, red);
+      if (threadIdx.x == 0) pmax[blockIdx.x] = am;
+    }
     return;
   }
   if (j.kind == 4 || j.kind == 6) {  // uniform per block (6: single-plane f16 U)
     const int cout = j.a[0], cin = j.a[1], n_p = j.a[2], k_p = j.a[3], flip = j.a[4];
     if (phase == 0) {
-      if (j.a[6]) return;  // its slot is filled by the un-flipped job over the same filters
+      if (j.a[6]) return;  // the un-flipped job over the same filters holds its maximum
       for (int r = 0; r < PREP_ITEMS / 256; ++r) {
         const long long li = blk0 - j.base + r * 256 + threadIdx.x;
         if (li >= items) break;
@@ -2259,10 +2304,11 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
           for (int q = 0; q < 9; ++q) amax_fold(am, g[q]);
         }
       }
-      amax_flush(am, j.amax);
+      am = block_max_u32(am, red);
+      if (threadIdx.x == 0) pmax[blockIdx.x] = am;
       return;
     }
-    const float s = exp2i(h2_exp(H2Scale{j.amax, wino_beta(j.a[5], 2)}));
+    const float s = exp2i(h2_exp_of(wmax, wino_beta(j.a[5], 2)));
     bf16_t* U = (bf16_t*)j.dst;
     if (wide) {
       __shared__ __attribute__((aligned(16))) float stg[16 * 256];
@@ -2390,19 +2436,25 @@ extern "C" long long nsm_prep_items(const NsmPrepJob* j) {
 }
 
 extern "C" int nsm_prep_weights(const NsmPrepJob* jobs_dev, int njobs, long long total_items,
-                                int max_pass, void* stream) {
+                                int max_pass, uint32_t* pmax, uint32_t* zero0, int64_t nzero0,
+                                uint32_t* zero1, int64_t nzero1, void* stream) {
   NSM_CHECK_ARG(jobs_dev && njobs > 0 && total_items > 0 && total_items % PREP_ITEMS == 0,
                 "prep_weights: bad args");
   NSM_CHECK_ARG(total_items / PREP_ITEMS < (1ll << 31), "prep_weights: too many items");
-  // phase 0 (the max|w| pass of the h2 jobs, kinds 4 and 5) only where the
-  // table holds such jobs (max_pass): otherwise every block of it would return
+  NSM_CHECK_ARG(!max_pass || pmax, "prep_weights: the h2 / f16 jobs need pmax (one word per block)");
+  NSM_CHECK_ARG((nzero0 == 0 || zero0) && (nzero1 == 0 || zero1) && nzero0 >= 0 && nzero1 >= 0,
+                "prep_weights: zero ranges");
   static const bool wide = [] {  // NSM_PREP_WIDE=1: the U jobs by wino_weight_block
     const char* e = getenv("NSM_PREP_WIDE");
     return e && atoi(e) != 0;
   }();
-  for (int phase = max_pass ? 0 : 1; phase < 2; ++phase)
+  // phase 0 (the slot zeroing and the max|w| pass of the h2 / f16 jobs) where
+  // there is something to do: otherwise every block of it would return
+  const bool p0 = max_pass || nzero0 > 0 || nzero1 > 0;
+  for (int phase = p0 ? 0 : 1; phase < 2; ++phase)
     hipLaunchKernelGGL(prep_weights_kernel, dim3((unsigned)(total_items / PREP_ITEMS)), dim3(256), 0,
-                       as_stream(stream), jobs_dev, njobs, phase | (wide && phase ? 2 : 0));
+                       as_stream(stream), jobs_dev, njobs, phase | (wide && phase ? 2 : 0), pmax,
+                       zero0, (long long)nzero0, zero1, (long long)nzero1);
   NSM_LAUNCH_CHECK("prep_weights");
   return 0;
 }
@@ -3644,6 +3696,120 @@ extern "C" int nsm_wino_dual_f16(const void* dy, int lddy, int B, int H, int W, 
                      (bf16_t*)V, (bf16_t*)dM, H2Scale{amax_dy, wino_beta(4, 0)},
                      H2Scale{amax_dy, wino_beta(4, 1)});
   NSM_LAUNCH_CHECK("wino_dual_f16");
+  return 0;
+}
+
+// wino_dual_f16_kernel of a dY formed per element from the BN backward's
+// deferred form (nsm_wino_dual_bn_f16): each patch element's dY = k1 dz + k2
+// (y - mean) + k3 is rounded to bf16 exactly where nsm_bn_bwd_apply would
+// store it, then transformed as a loaded dY is
+template <int MT>
+__global__ void __launch_bounds__(256) wino_dual_bn_f16_kernel(
+    const bf16_t* __restrict__ g, int ldg, const bf16_t* __restrict__ y, int ldy, int H, int W, int C,
+    int TH, int TW, long long T, const float* __restrict__ scale, const float* __restrict__ shift,
+    float slope, const float* __restrict__ mask, const float* __restrict__ mean,
+    const float* __restrict__ coef, bf16_t* __restrict__ V, bf16_t* __restrict__ dM, H2Scale hv,
+    H2Scale hd) {
+  constexpr int A = MT + 2;
+  const int C4 = C / 4;
+  const long long total = T * C4;
+  const float sv = exp2i(h2_exp(hv)), sd = exp2i(h2_exp(hd));  // every lane
+  const size_t plane = (size_t)T * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const long long t = i / C4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    u32x2 raw[A][A], yr[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
+        const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const size_t p = (size_t)b * H * W + (in ? (size_t)yy * W + xx : 0);
+        raw[a][e] = *(const u32x2*)(g + p * ldg + c);
+        yr[a][e] = *(const u32x2*)(y + p * ldy + c);
+      }
+    const f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
+    const f32x4 mu = *(const f32x4*)(mean + c);
+    const f32x4 k1 = *(const f32x4*)(coef + c), k2 = *(const f32x4*)(coef + C + c),
+                k3 = *(const f32x4*)(coef + 2 * C + c);
+    const f32x4 mk = mask ? *(const f32x4*)(mask + (size_t)b * C + c) : f32x4{1.f, 1.f, 1.f, 1.f};
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
+        const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const f32x4 v = bf4_to_f32(yr[a][e]);
+        f32x4 dz = bf4_to_f32(raw[a][e]) * lrelu_grad_v4(v * sc + sh, slope);
+        if (mask) dz = dz * mk;
+        const f32x4 d = k1 * dz + k2 * (v - mu) + k3;
+        raw[a][e] = in ? u32x2{pack_bf2(d.x, d.y), pack_bf2(d.z, d.w)} : u32x2{0u, 0u};
+      }
+    {
+      f32x4 scv[A][A];
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        f32x4 d[A];
+#pragma unroll
+        for (int e = 0; e < A; ++e) d[e] = bf4_to_f32(raw[a][e]);
+        wcol_row<CBt<MT>>(scv, d, a);
+      }
+      bf16_t* out = V + (size_t)t * C + c;
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        f32x4 v[A];
+        wmat<CBt<MT>>(scv[a], v);
+#pragma unroll
+        for (int e = 0; e < A; ++e)
+          *(u32x2*)(out + (a * A + e) * plane) =
+              __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * sv, f16x4v));
+      }
+    }
+    f32x4 scm[A][MT];
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      f32x4 d[MT];
+#pragma unroll
+      for (int e = 0; e < MT; ++e) d[e] = bf4_to_f32(raw[a + 1][e + 1]);
+      wcol_row<CA<MT>>(scm, d, a);
+    }
+    bf16_t* out = dM + (size_t)t * C + c;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      f32x4 v[A];
+      wmat<CA<MT>>(scm[a], v);
+#pragma unroll
+      for (int e = 0; e < A; ++e)
+        *(u32x2*)(out + (a * A + e) * plane) =
+            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * sd, f16x4v));
+    }
+  }
+}
+
+extern "C" int nsm_wino_dual_bn_f16(const void* g, int ldg, const void* y, int ldy, int B, int H, int W,
+                                    int c_p, int tile, const float* scale, const float* shift,
+                                    float slope, const float* mask, const float* mean,
+                                    const float* coef, void* V, void* dM, const uint32_t* bound,
+                                    void* stream) {
+  NSM_CHECK_ARG(g && y && V && dM && scale && shift && mean && coef && bound && tile == 4 &&
+                    c_p % 32 == 0 && ldg % 4 == 0 && ldg >= c_p && ldy % 4 == 0 && ldy >= c_p,
+                "wino_dual_bn_f16: bad args (tile 4 only)");
+  NSM_CHECK_ARG(((uintptr_t)g % 8) == 0 && ((uintptr_t)y % 8) == 0 && ((uintptr_t)V % 16) == 0 &&
+                    ((uintptr_t)dM % 16) == 0,
+                "wino_dual_bn_f16: alignment");
+  WinoGeom gm;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, gm), "wino_dual_bn_f16: bad shape");
+  hipLaunchKernelGGL(wino_dual_bn_f16_kernel<4>, dim3(grid_1d(gm.T * c_p / 4)), dim3(256), 0,
+                     as_stream(stream), (const bf16_t*)g, ldg, (const bf16_t*)y, ldy, H, W, c_p, gm.TH,
+                     gm.TW, gm.T, scale, shift, slope, mask, mean, coef, (bf16_t*)V, (bf16_t*)dM,
+                     H2Scale{bound, wino_beta(4, 0)}, H2Scale{bound, wino_beta(4, 1)});
+  NSM_LAUNCH_CHECK("wino_dual_bn_f16");
   return 0;
 }
 

@@ -52,6 +52,7 @@ _SIGS = {
     "nsm_wino_output_bf16m_act": (I, [P, I, I, I, I, I, I, P, F, P, F, P, P, I, P, P, F, P]),
     "nsm_wino_dout_f16": (I, [P, I, I, I, I, I, I, P, P, P]),
     "nsm_wino_dual_f16": (I, [P, I, I, I, I, I, I, P, P, P, P]),
+    "nsm_wino_dual_bn_f16": (I, [P, I, P, I, I, I, I, I, I, P, P, F, P, P, P, P, P, P, P]),
     "nsm_wino_wgrad_f16_ws": (Z, [I, I, I, I, I, I]),
     "nsm_conv3x3_wgrad_wino_f16": (I, [P, P, I, I, I, I, I, I, I, I, P, P, Z, P, P, P]),
     "nsm_wino_wgrad_h2_ws": (Z, [I, I, I, I, I, I]),
@@ -149,7 +150,7 @@ _SIGS = {
     "nsm_dropout_masks": (I, [P, I, I, U64, P, P]),
     "nsm_stage_mark": (I, [I, P]),
     "nsm_prep_items": (L, [P]),
-    "nsm_prep_weights": (I, [P, I, L, I, P]),
+    "nsm_prep_weights": (I, [P, I, L, I, P, P, L, P, L, P]),
 }
 
 

@@ -506,6 +506,22 @@ def wino_dual_input_bn_h2(d, y, st, mask, B, H, W, tile, bound, slope=0.2):
     return Vd, dM
 
 
+def wino_dual_bn_f16(d, y, st, mask, B, H, W, bound, slope=0.2):
+    """wino_dual_f16 of d = DeferredBnBwd(dA1, coef) (bf16 BN input y, state
+    st, mask [B][C] or None): dY1 is formed per element (rounded to bf16 as
+    nsm_bn_bwd_apply stores it), never stored (nsm_wino_dual_bn_f16); bound:
+    the dY1 bound slot the finalize filled (the scale source of V and dM and
+    of the GEMMs reading them)."""
+    c_p = y.shape[1]
+    n = 36 * wino_tiles(B, H, W, 4) * c_p
+    V = torch.empty(n, dtype=H2, device=y.device)
+    dM = torch.empty(n, dtype=H2, device=y.device)
+    call("nsm_wino_dual_bn_f16", ptr(d.g), d.g.stride(0), ptr(y), y.stride(0), B, H, W, c_p, 4,
+         ptr(st.scale), ptr(st.shift), slope, ptr(mask), ptr(st.mean), ptr(d.coef), ptr(V), ptr(dM),
+         ptr(bound), stream())
+    return V, dM
+
+
 def conv3x3_wgrad_wino(dy, V, B, H, W, cin_p, cin, cout, dw, tile=4, tag=None, dM=None,
                        amax=(None, None)):
     """dw [cout, cin, 3, 3] of a 3x3 conv whose forward kept V (conv3x3_wino, same tile).
@@ -797,7 +813,7 @@ SUM_ROWS_ABOVE = int(os.environ.get("NSM_SUM_ROWS_ABOVE", "512"))  # BN-backward
 
 def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, dbias_prev,
                          recompute, slope=0.2, tag=None, defer=False, amax=(None, None),
-                         amax_out=None):
+                         amax_out=None, bound=None):
     """dY1 of a DoubleConv's first BN from dY2 (grad wrt the 1x1 conv output):
     the 1x1 input gradient dA1 = dY2 W2 with the BN + LeakyReLU + Dropout2d
     backward in its epilogue (nsm_conv1x1_dgrad_bnbwd) — the same values as
@@ -807,7 +823,10 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     nsm_bn_bwd_apply. defer=True (with recompute=False): DeferredBnBwd(dA1,
     coef) instead of dy, the apply pass left to the consumer. amax = (max|dY2|,
     max|w2d|) slots: the fp32 GEMM passes run the f16x2 split. amax_out: slot
-    receiving max|dY1| (fp32; the h2 scale source of its Winograd transforms)."""
+    receiving max|dY1| (fp32; the h2 scale source of its Winograd transforms).
+    bound=(k1dz slot, bound slot), both zeroed (bf16, defer): the GEMM records
+    max|scale*dz| and the finalize derives the dY1 bound from it, the scale
+    source of wino_dual_bn_f16."""
     from ._lib import lib
     M, cop = dY2.shape
     C = y.shape[1]
@@ -821,8 +840,10 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
             ptr(st.scale), ptr(st.shift), ptr(st.mean), ptr(st.invstd), ptr(mask), slope)
     ev = _probe(tag)
     am = _pair(amax) if dtc == NSM_F32 else (None, None)
+    k1dz, bslot = bound if bound is not None else (None, None)
+    assert bound is None or (dtc == NSM_BF16 and not recompute)
     call("nsm_conv1x1_dgrad_bnbwd", *args, 0 if recompute else 1, ptr(partial), None, ptr(dA1),
-         dA1.stride(0) if dA1 is not None else 0, dtc, *am, None, stream())
+         dA1.stride(0) if dA1 is not None else 0, dtc, *am, ptr(k1dz), stream())
     if nchunk > SUM_ROWS_ABOVE:
         G = -(-nchunk // SUM_ROWS_ABOVE)
         n2 = -(-nchunk // G)
@@ -831,7 +852,7 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
         partial, nchunk = buf, n2
     coef = empty(3 * C, device=y.device)
     call("nsm_bn_bwd_finalize", ptr(partial), nchunk, M, C, c_real, ptr(st.gamma), ptr(st.invstd),
-         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), None, None, stream())
+         ptr(dgamma), ptr(dbeta), ptr(dbias_prev), ptr(coef), ptr(k1dz), ptr(bslot), stream())
     if defer and not recompute:
         if ev is not None:
             ev.record()

@@ -56,6 +56,23 @@ def bf16_wino(cip, dtype, training):
             and cip >= BF16_WINO_MIN and cip % 128 == 0)
 
 
+PREP_ITEMS = 512   # items per block of nsm_prep_weights (nsm_prep_items rounds to it)
+
+
+def run_jobs(jobs, device):
+    """One nsm_prep_weights call over a list of NsmPrepJob (consecutive bases,
+    shared jobs with a[6] = the source job's first block + 1): the table and
+    the max|w| word per block made here (tests, standalone layouts)."""
+    total = sum(int(lib.nsm_prep_items(ctypes.byref(j))) for j in jobs)
+    raw = (NsmPrepJob * len(jobs))(*jobs)
+    table = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8).to(device)
+    pmax = torch.empty(total // PREP_ITEMS, dtype=torch.int32, device=device)
+    max_pass = int(any(j.kind in (KIND_WINO_H2, KIND_PACK_H2, KIND_WINO_F16) for j in jobs))
+    call("nsm_prep_weights", ptr(table), len(jobs), total, max_pass, ptr(pmax), None, 0, None, 0,
+         stream())
+    return table, pmax
+
+
 class LazyBlockWeights:
     """Layouts of one DoubleConv computed on demand (one launch each)."""
 
@@ -162,6 +179,10 @@ class StepWeights:
             j.kind = kind
             for i, v in enumerate(a):
                 j.a[i] = int(v)
+            if kind in (KIND_WINO_H2, KIND_PACK_H2, KIND_WINO_F16) and len(a) > 6 and a[6]:
+                # shares the maximum of the job just before it (same filters):
+                # a[6] = that job's first block + 1 (include/nsm.h)
+                j.a[6] = int(jobs[-1].base // PREP_ITEMS + 1)
             j.base = base
             j.src = src.data_ptr()
             j.dst = out.data_ptr()
@@ -271,14 +292,20 @@ class StepWeights:
         host = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8)
         self.table = host.to(dev)
         self.keep = keep
+        # one max|w| word per block of the launch (the h2 / f16 jobs' phase 0)
+        self.pmax = torch.empty(self.total // PREP_ITEMS, dtype=torch.int32, device=dev)
 
     def valid(self, mod):
         ps = list(mod.parameters())
         return len(ps) == len(self.ptrs) and all(p.data_ptr() == q for p, q in zip(ps, self.ptrs))
 
-    def run(self):
-        self.amax.zero_()
-        call("nsm_prep_weights", ptr(self.table), self.njobs, self.total, self.max_pass, stream())
+    def run(self, act_slots=None):
+        """The step's preparation launches. They zero this object's weight
+        slots and `act_slots` (the forward's activation-maximum slots, an
+        int32 tensor) before anything writes them: no fill launches."""
+        call("nsm_prep_weights", ptr(self.table), self.njobs, self.total, self.max_pass,
+             ptr(self.pmax), ptr(self.amax), self.amax.numel(), ptr(act_slots),
+             act_slots.numel() if act_slots is not None else 0, stream())
 
     def block(self, k):
         return self.blocks[k]

@@ -68,6 +68,10 @@ WGRAD_F16 = os.environ.get("NSM_WGRAD_F16", "1") != "0"
 # wino_input_f16 + wino_dout_f16 instead of from one read of dY1
 # (ops.wino_dual_f16; B=64 step 1581 / 1586 -> 1596 / 1604 frames/s A/B)
 BF16_DUAL = os.environ.get("NSM_BF16_DUAL", "1") != "0"
+# NSM_LAZY_DY1_F16=0: with BF16_DUAL, the bf16 F(4x4) layers' dY1 through
+# nsm_bn_bwd_apply (stored, then read by the dual transform) instead of formed
+# per element inside it (ops.wino_dual_bn_f16, scale from the finalize's bound)
+LAZY_DY1_F16 = os.environ.get("NSM_LAZY_DY1_F16", "1") != "0"
 # NSM_EVAL_FUSED=0: eval forward with separate BN-apply passes instead of the
 # BN + LeakyReLU (+ skip) in the conv epilogues (nsm_conv_fwd_act)
 EVAL_FUSED = os.environ.get("NSM_EVAL_FUSED", "1") != "0"
@@ -690,11 +694,17 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
     # dY1 is consumed only by its two Winograd transforms: leave the BN apply
     # to the dual transform kernel, dY1 is never stored
     lazy = s.V is not None and need_dx and DUAL_TRANSFORM and LAZY_DY1 and not h2
+    # bf16 F(4x4): dY1 formed inside the dual transform, scaled from the bound
+    # the finalize derives (AM_DY1B, from max|k1 dz| of the GEMM epilogue)
+    lazy16 = mode == 1 and _wino_f16(s) and need_dx and BF16_DUAL and LAZY_DY1_F16
     if mode:
+        if lazy16:
+            am_dy1 = _slot(s.am, AM_DY1B)
         dY1 = ops.conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, s.Y1, s.bn1, s.mask, ci, g[bn1m.weight],
                                        g[bn1m.bias], g[c0.bias], mode == 2,
-                                       tag=name + ".conv.4.dgrad", defer=lazy, amax=am_w2d,
-                                       amax_out=am_dy1)
+                                       tag=name + ".conv.4.dgrad", defer=lazy or lazy16,
+                                       amax=am_w2d, amax_out=None if lazy16 else am_dy1,
+                                       bound=(_slot(s.am, AM_K1DZ1), am_dy1) if lazy16 else None)
     else:
         dA1 = ops.conv_fwd(dY2, B, H, W, w2d, None, s.cip, 1, tag=name + ".conv.4.dgrad",
                            amax=am_w2d)
@@ -753,7 +763,9 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
                               amax=(am_dy1, s.pw.amax_w1(ops.PACK_DGRAD)),
                               tag=name + ".conv.0.dgrad")[0]
     elif s.Vf16 is not None:   # bf16 F(4x4): dY's transform, then the Winograd-domain GEMMs
-        if need_dx and BF16_DUAL:   # with the input gradient's V, from one read of dY1
+        if isinstance(dY1, ops.DeferredBnBwd):   # dY1 formed per element, never stored
+            Vd, dM = ops.wino_dual_bn_f16(dY1, s.Y1, s.bn1, s.mask, B, H, W, am_dy1)
+        elif need_dx and BF16_DUAL:   # with the input gradient's V, from one read of dY1
             Vd, dM = ops.wino_dual_f16(dY1, B, H, W, am_dy1)
         else:
             dM = ops.wino_dout_f16(dY1, B, H, W, am_dy1)
@@ -815,9 +827,10 @@ def block_shapes(Rh, Rw):
 PREP_BATCH = os.environ.get("NSM_PREP_BATCH", "1") != "0"
 
 
-def _step_weights(mod, dtype, Rh, Rw, training):
+def _step_weights(mod, dtype, Rh, Rw, training, act_slots=None):
     """The step's weight layouts, written by ONE prep launch (cached per
     signature; rebuilt when the parameters moved, e.g. FlatAdamW re-homing).
+    act_slots: the forward's activation-maximum slots, zeroed by that launch.
     NSM_PREP_BATCH=0: None (every block packs its own, one launch per layout)."""
     if not PREP_BATCH:
         return None
@@ -829,7 +842,7 @@ def _step_weights(mod, dtype, Rh, Rw, training):
     if sw is None or not sw.valid(mod):
         sw = cache[key] = StepWeights(mod, dtype, block_shapes(Rh, Rw), training,
                                       WINOGRAD_MIN_CHANNELS, wino_tile, h2=h2)
-    sw.run()
+    sw.run(act_slots)
     return sw
 
 
@@ -852,10 +865,12 @@ class _UnetFn(torch.autograd.Function):
             f"Unet expects {mod.conv2.conv[0].in_channels // 4} input channels, got {C}")
         cdt = mod.activation_dtype()
         masks, mask_max = _masks_for(mod, B, dev, training)
-        sw = _step_weights(mod, cdt, Rh, Rw, training)
         # per-step maxima of the f16x2 GEMM operands of every block (their
-        # producers fill them; zeroed here, one launch)
-        amax = ops.amax_slots(AM_PER_BLOCK * 10, dev) if sw else None
+        # producers fill them), zeroed by the weight preparation's first launch
+        amax = torch.empty(AM_PER_BLOCK * 10 * ops.AMAX_WORDS, dtype=torch.int32, device=dev)
+        sw = _step_weights(mod, cdt, Rh, Rw, training, act_slots=amax)
+        if sw is None:
+            amax = None
         w1_2 = sw.block(2).w1(ops.PACK_FWD) if sw and ops.pad32(
             mod.conv2.conv[0].in_channels) < WINOGRAD_MIN_CHANNELS else None
         if w1_2 is not None and w1_2.dtype == ops.H2:

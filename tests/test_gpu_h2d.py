@@ -205,7 +205,7 @@ def test_prep_kind5_matches_to_h2(ops, device):
     bitwise equal to nsm_to_h2 of the fp32 packs with the same max|w| slot."""
     import ctypes
     from nsm_amd import prep
-    from nsm_amd._lib import call, lib, ptr, stream
+    from nsm_amd._lib import lib
     g = torch.Generator().manual_seed(3)
     co, ci, cop, cip = 50, 70, 64, 96
     w = (torch.randn(co, ci, 1, 1, generator=g) * 0.3).to(device)
@@ -222,9 +222,7 @@ def test_prep_kind5_matches_to_h2(ops, device):
         base += int(lib.nsm_prep_items(ctypes.byref(j)))
         jobs.append(j)
         outs.append(out)
-    raw = (prep.NsmPrepJob * 2)(*jobs)
-    table = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8).to(device)
-    call("nsm_prep_weights", ptr(table), 2, base, 1, stream())
+    prep.run_jobs(jobs, device)
     ref_am = ops.absmax(w.reshape(-1))
     for mode, out in zip((ops.PACK_FWD, ops.PACK_DGRAD), outs):
         pk = ops.pack_conv_weight(w, cop, cip, mode)

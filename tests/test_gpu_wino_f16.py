@@ -5,8 +5,6 @@ against a float64 conv2d of the same bf16 input: its error stays within that of
 the direct bf16 implicit GEMM it replaces (the reference's bf16-autocast
 arithmetic for Unetmodel.py:21), and the BN partials written by the output
 transform are those of the bf16-rounded outputs."""
-import ctypes
-
 import pytest
 import torch
 import torch.nn.functional as F
@@ -17,7 +15,6 @@ pytestmark = pytest.mark.gpu
 def _prep_u(ops, w, cin_p, cout_p, device):
     """prep kind 6 (single-plane f16 U) through nsm_prep_weights, one job."""
     from nsm_amd import prep
-    from nsm_amd._lib import lib
     am = ops.amax_slots(1, device)
     U = torch.empty(36 * cout_p * cin_p, dtype=ops.H2, device=device)
     j = prep.NsmPrepJob()
@@ -28,10 +25,7 @@ def _prep_u(ops, w, cin_p, cout_p, device):
     j.src = w.data_ptr()
     j.dst = U.data_ptr()
     j.amax = am.data_ptr()
-    n = int(lib.nsm_prep_items(ctypes.byref(j)))
-    raw = (prep.NsmPrepJob * 1)(j)
-    table = torch.frombuffer(bytearray(bytes(raw)), dtype=torch.uint8).to(device)
-    ops.call("nsm_prep_weights", ops.ptr(table), 1, n, 1, ops.stream())
+    prep.run_jobs([j], device)
     torch.cuda.synchronize()
     return U, am
 
@@ -126,3 +120,41 @@ def test_wino_dual_f16_matches_separate_transforms(device, B, H, W, c):
     assert torch.equal(V.view(torch.int16), V0.view(torch.int16))
     assert torch.equal(dM.view(torch.int16), dM0.view(torch.int16))
     assert V.abs().max().item() > 0 and dM.abs().max().item() > 0
+
+
+@pytest.mark.parametrize("drop", [False, True])
+@pytest.mark.parametrize("B,H,W,c", [(2, 32, 32, 512), (1, 37, 29, 128), (3, 13, 22, 256)])
+def test_wino_dual_bn_f16_matches_apply_then_dual(device, B, H, W, c, drop):
+    """nsm_wino_dual_bn_f16 (the bf16 path's lazy dY1: the first BN's backward
+    formed per element inside the F(4x4) dual transform) writes the V and dM
+    of nsm_bn_bwd_apply's stored dY1 followed by nsm_wino_dual_f16, under the
+    same scale slot (the finalize's dY1 bound, which dominates max|dY1|):
+    equal up to FMA-contraction ulps of the per-element dY1."""
+    from nsm_amd import ops
+    g = torch.Generator().manual_seed(B * H * W + c + int(drop))
+    M = B * H * W
+    y = (torch.randn(M, c, generator=g) * 2 + 0.5).to(torch.bfloat16).to(device)
+    gr = (torch.randn(M, c, generator=g) * 1e-2).to(torch.bfloat16).to(device)
+    mask = ((torch.rand(B, c, generator=g) > 0.2).float() / 0.8).to(device) if drop else None
+    bn = torch.nn.BatchNorm2d(c).to(device)
+    with torch.no_grad():
+        bn.weight.copy_(torch.randn(c, generator=g))
+        bn.bias.uniform_(-0.2, 0.2)
+    st = ops.bn_train(y, bn, c, 0.1, 1e-5)
+    slots = ops.amax_slots(2, device)
+    k1dz, bnd = ops.amax_slot(slots, 0), ops.amax_slot(slots, 1)
+    z = [torch.zeros(c, device=device) for _ in range(6)]
+    d = ops.bn_bwd(gr, y, st, H * W, mask, c, *z[:3], defer=True, h2=(k1dz, bnd))
+    V1, dM1 = ops.wino_dual_bn_f16(d, y, st, mask, B, H, W, bnd)
+    dy = ops.bn_bwd(gr, y, st, H * W, mask, c, *z[3:])
+    V0, dM0 = ops.wino_dual_f16(dy, B, H, W, bnd)
+    torch.cuda.synchronize()
+    bound = torch.frombuffer(bytearray(bnd.cpu().numpy().tobytes()), dtype=torch.float32).max().item()
+    assert bound >= dy.float().abs().max().item()
+    for name, a, b in (("V", V1, V0), ("dM", dM1, dM0)):
+        a, b = a.float(), b.float()
+        diff = (a - b).abs()
+        frac = (diff > 0).float().mean().item()
+        print(f"{name}: mismatched {frac:.2e}, max diff {diff.max().item():.3e} of {b.abs().max().item():.3e}")
+        assert torch.isfinite(a).all() and b.abs().max().item() > 0
+        assert frac <= 2e-3 and diff.max().item() <= 2.0 ** -5 * b.abs().max().item(), (name, frac)
