@@ -225,10 +225,12 @@ int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int cout_p, int t
                          void* stream);
 /* The same GEMM / output transform with M held as f16 (half the bytes of the
  * GEMM's writes and the output transform's reads): nsm_wino_gemm_f16m writes
- * M16 [36][T][cout_p] f16 scaled by 2^-(15 + ceil log2 cin_p) in the operands'
- * scaled units (a static bound: |M16| <= 2^15, no maximum pass);
- * nsm_wino_output_bf16m takes the same scale slots / bounds and cin_p to undo
- * it. NSM_BF16_M16 selects this pair in the Python path. */
+ * M16 [36][T][cout_p] f16, each 64 x 64 tile of each component scaled by the
+ * power of two that puts ITS maximum at <= 2^15 (m16e [36][ceil(T/64)][cout_p/64]
+ * int32 receives the exponents, cout_p % 64 == 0), so a tile's values stay
+ * normal f16 down to 2^-29 of its own maximum; nsm_wino_output_bf16m reads the
+ * exponents and the same scale slots / bounds to undo it. NSM_BF16_M16 selects
+ * this pair in the Python path. */
 /* Both F(4x4) transforms of the bf16 output gradient dY from one read: V
  * (the input gradient's operand, as nsm_wino_input_f16 of dY) and dM (as
  * nsm_wino_dout_f16), scale source amax_dy for both. NSM_BF16_DUAL selects it
@@ -246,20 +248,20 @@ int nsm_wino_dual_bn_f16(const void* g, int ldg, const void* y, int ldy, int B, 
                          const float* mask, const float* mean, const float* coef, void* V, void* dM,
                          const uint32_t* bound, void* stream);
 int nsm_wino_gemm_f16m(const void* V, const void* U, int B, int H, int W, int cin_p, int cout_p,
-                       int tile, void* M16, const uint32_t* amax_v, float beta_v,
+                       int tile, void* M16, int* m16e, const uint32_t* amax_v, float beta_v,
                        const uint32_t* amax_u, float beta_u, void* stream);
-int nsm_wino_output_bf16m(const void* M16, int B, int H, int W, int cin_p, int cout_p, int tile,
-                          const uint32_t* amax_v, float beta_v, const uint32_t* amax_u,
-                          float beta_u, const float* bias, void* y, int ldy, float* partial,
-                          int nslot, void* stream);
+int nsm_wino_output_bf16m(const void* M16, const int* m16e, int B, int H, int W, int cin_p,
+                          int cout_p, int tile, const uint32_t* amax_v, float beta_v,
+                          const uint32_t* amax_u, float beta_u, const float* bias, void* y, int ldy,
+                          float* partial, int nslot, void* stream);
 /* eval: the same output transform writing lrelu(y*act_scale + act_shift,
  * slope) in bf16 (the DoubleConv's first BatchNorm from its running
  * statistics + LeakyReLU, Unetmodel.py:22-23, fused; the bf16 eval forward's
  * F(4x4) layers) */
-int nsm_wino_output_bf16m_act(const void* M16, int B, int H, int W, int cin_p, int cout_p, int tile,
-                              const uint32_t* amax_v, float beta_v, const uint32_t* amax_u,
-                              float beta_u, const float* bias, void* y, int ldy,
-                              const float* act_scale, const float* act_shift, float slope,
+int nsm_wino_output_bf16m_act(const void* M16, const int* m16e, int B, int H, int W, int cin_p,
+                              int cout_p, int tile, const uint32_t* amax_v, float beta_v,
+                              const uint32_t* amax_u, float beta_u, const float* bias, void* y,
+                              int ldy, const float* act_scale, const float* act_shift, float slope,
                               void* stream);
 /* Its weight gradient: dM = s (A dY A^T) of the bf16 output gradient dY as
  * [36][T][c_p] f16 (amax_dy: max|dY| from dY's producer, beta =

@@ -1525,10 +1525,12 @@ struct WinoAct {
 };
 
 // M16: M is the f16 output of the O16 GEMM (nsm_wino_gemm_f16m), scaled by
-// 2^(e_v + e_u - o16_exp(K)) against the true M
+// 2^(e_v + e_u + e_tile) against the true M, e_tile the exponent the GEMM
+// chose for each 64 x 64 tile of each component ([alpha^2][rows][N / 64])
 struct WinoM16 {
   H2Scale sv, su;
-  int K;
+  const int* e;
+  int rows;  // ceil(T / 64)
 };
 
 // The column pass streams M's rows (wcol_row: wmat2's bits with one row
@@ -1546,11 +1548,10 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
   constexpr int A = MT + 2, CW = WinoVec<MT>::W;
   using VT = typename WinoVec<MT>::T;
   static_assert(!M16 || (BFO && CW == 4), "f16 M: the bf16 path's F(4x4)");
-  float msc = 1.f;  // every lane reads the scale slots (wave reduction) before the loop
+  int ev = 0, eu = 0;  // every lane reads the scale slots (wave reduction) before the loop
   if constexpr (M16) {
-    int e = o16_exp(m16.K) - h2_exp(m16.sv);
-    e = e < -126 ? -126 : (e > 126 ? 126 : e);
-    msc = exp2i(e) * exp2i(-h2_exp(m16.su));
+    ev = h2_exp(m16.sv);
+    eu = h2_exp(m16.su);
   }
   const int N4 = N / CW;
   const long long total = T * N4;
@@ -1576,7 +1577,10 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
         if constexpr (M16) {
           const u32x2 h = *(const u32x2*)(in16 + (a * A + e) * plane);
           const f32x2 lo = unpack_h2(h.x), hi = unpack_h2(h.y);
-          row[e] = VT{lo.x, lo.y, hi.x, hi.y} * msc;
+          const int et = m16.e[((size_t)(a * A + e) * m16.rows + t / 64) * (N / 64) + c / 64];
+          int x = -et - ev;
+          x = x < -126 ? -126 : (x > 126 ? 126 : x);
+          row[e] = VT{lo.x, lo.y, hi.x, hi.y} * (exp2i(x) * exp2i(-eu));
         } else {
           row[e] = *(const VT*)(in + (a * A + e) * plane);
         }
@@ -3444,9 +3448,9 @@ extern "C" int nsm_wino_gemm_f16(const void* V, const void* U, int B, int H, int
 // the same GEMM writing M as f16 (O16: scale 2^-(15 + ceil log2 cin_p) in the
 // operands' scaled units; M16 [alpha^2][T][cout_p] f16, half of Mb's bytes)
 extern "C" int nsm_wino_gemm_f16m(const void* V, const void* U, int B, int H, int W, int cin_p,
-                                  int cout_p, int tile, void* M16, const uint32_t* amax_v,
+                                  int cout_p, int tile, void* M16, int* m16e, const uint32_t* amax_v,
                                   float beta_v, const uint32_t* amax_u, float beta_u, void* stream) {
-  NSM_CHECK_ARG(V && U && M16 && amax_v && amax_u && cin_p % 128 == 0 && cout_p % 128 == 0,
+  NSM_CHECK_ARG(V && U && M16 && m16e && amax_v && amax_u && cin_p % 128 == 0 && cout_p % 128 == 0,
                 "wino_gemm_f16m: bad args (cin_p, cout_p multiples of 128)");
   NSM_CHECK_ARG(((uintptr_t)V % 16) == 0 && ((uintptr_t)U % 16) == 0 && ((uintptr_t)M16 % 16) == 0,
                 "wino_gemm_f16m: 16B alignment");
@@ -3456,16 +3460,16 @@ extern "C" int nsm_wino_gemm_f16m(const void* V, const void* U, int B, int H, in
                     (long long)cout_p * cin_p < (1ll << 30),
                 "wino_gemm_f16m: operand too large");
   return wino_gemm_f16((const bf16_t*)V, (const bf16_t*)U, g.T, cin_p, cout_p, g.alpha2, (float*)M16,
-                       H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, as_stream(stream), true);
+                       H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, as_stream(stream), true, m16e);
 }
 
 // the output transform of nsm_wino_gemm_f16m's f16 M (same scale slots / bounds
 // as the GEMM call, cin_p its K) writing bf16 Y (+ the BN partials)
-extern "C" int nsm_wino_output_bf16m(const void* M16, int B, int H, int W, int cin_p, int cout_p,
-                                     int tile, const uint32_t* amax_v, float beta_v,
+extern "C" int nsm_wino_output_bf16m(const void* M16, const int* m16e, int B, int H, int W, int cin_p,
+                                     int cout_p, int tile, const uint32_t* amax_v, float beta_v,
                                      const uint32_t* amax_u, float beta_u, const float* bias,
                                      void* y, int ldy, float* partial, int nslot, void* stream) {
-  NSM_CHECK_ARG(M16 && y && amax_v && amax_u && tile == 4 && cin_p > 0 && cout_p % 32 == 0 &&
+  NSM_CHECK_ARG(M16 && m16e && y && amax_v && amax_u && tile == 4 && cin_p > 0 && cout_p % 64 == 0 &&
                     ldy % 4 == 0,
                 "wino_output_bf16m: bad args (tile 4 only)");
   WinoGeom g;
@@ -3477,7 +3481,7 @@ extern "C" int nsm_wino_output_bf16m(const void* M16, int B, int H, int W, int c
                   wino_stat_step(cout_p, tile));
     grid = dim3((unsigned)((long long)nslot * (cout_p / 4) / 256));
   }
-  const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, cin_p};
+  const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, m16e, (int)((g.T + 63) / 64)};
   hipStream_t s = as_stream(stream);
   if (partial)
     hipLaunchKernelGGL((wino_output_kernel<4, true, false, true, true>), grid, dim3(256), 0, s,
@@ -3495,17 +3499,17 @@ extern "C" int nsm_wino_output_bf16m(const void* M16, int B, int H, int W, int c
 // lrelu(BN(y)) in bf16, BN from the running statistics (act_scale, act_shift:
 // nsm_bn_eval's folded vectors) — the bf16 eval forward's first BatchNorm +
 // LeakyReLU of a DoubleConv (Unetmodel.py:21-23) in the 3x3 conv's epilogue
-extern "C" int nsm_wino_output_bf16m_act(const void* M16, int B, int H, int W, int cin_p, int cout_p,
-                                         int tile, const uint32_t* amax_v, float beta_v,
-                                         const uint32_t* amax_u, float beta_u, const float* bias,
-                                         void* y, int ldy, const float* act_scale,
+extern "C" int nsm_wino_output_bf16m_act(const void* M16, const int* m16e, int B, int H, int W,
+                                         int cin_p, int cout_p, int tile, const uint32_t* amax_v,
+                                         float beta_v, const uint32_t* amax_u, float beta_u,
+                                         const float* bias, void* y, int ldy, const float* act_scale,
                                          const float* act_shift, float slope, void* stream) {
-  NSM_CHECK_ARG(M16 && y && amax_v && amax_u && act_scale && act_shift && tile == 4 && cin_p > 0 &&
-                    cout_p % 32 == 0 && ldy % 4 == 0 && ldy >= cout_p,
+  NSM_CHECK_ARG(M16 && m16e && y && amax_v && amax_u && act_scale && act_shift && tile == 4 &&
+                    cin_p > 0 && cout_p % 64 == 0 && ldy % 4 == 0 && ldy >= cout_p,
                 "wino_output_bf16m_act: bad args (tile 4 only)");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_bf16m_act: bad shape");
-  const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, cin_p};
+  const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, m16e, (int)((g.T + 63) / 64)};
   const WinoAct act{act_scale, act_shift, slope, nullptr, 0};
   hipLaunchKernelGGL((wino_output_kernel<4, false, true, true, true>), dim3(grid_1d(g.T * (cout_p / 4))),
                      dim3(256), 0, as_stream(stream), (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T,

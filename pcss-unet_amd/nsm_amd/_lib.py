@@ -47,9 +47,9 @@ _SIGS = {
     "nsm_wino_input_f16": (I, [P, I, I, I, I, I, I, P, P, P]),
     "nsm_wino_gemm_f16": (I, [P, P, I, I, I, I, I, I, P, P, F, P, F, P]),
     "nsm_wino_output_bf16": (I, [P, I, I, I, I, I, P, P, I, P, I, P]),
-    "nsm_wino_gemm_f16m": (I, [P, P, I, I, I, I, I, I, P, P, F, P, F, P]),
-    "nsm_wino_output_bf16m": (I, [P, I, I, I, I, I, I, P, F, P, F, P, P, I, P, I, P]),
-    "nsm_wino_output_bf16m_act": (I, [P, I, I, I, I, I, I, P, F, P, F, P, P, I, P, P, F, P]),
+    "nsm_wino_gemm_f16m": (I, [P, P, I, I, I, I, I, I, P, P, P, F, P, F, P]),
+    "nsm_wino_output_bf16m": (I, [P, P, I, I, I, I, I, I, P, F, P, F, P, P, I, P, I, P]),
+    "nsm_wino_output_bf16m_act": (I, [P, P, I, I, I, I, I, I, P, F, P, F, P, P, I, P, P, F, P]),
     "nsm_wino_dout_f16": (I, [P, I, I, I, I, I, I, P, P, P]),
     "nsm_wino_dual_f16": (I, [P, I, I, I, I, I, I, P, P, P, P]),
     "nsm_wino_dual_bn_f16": (I, [P, I, P, I, I, I, I, I, I, P, P, F, P, P, P, P, P, P, P]),

@@ -395,9 +395,16 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     m16 = (BF16_M16 if m16 is None else m16) or act is not None
     bv, bu = wino_beta(4, 0), wino_beta(4, 2)
     Mb = torch.empty(36 * T * cout_p, dtype=H2 if m16 else torch.float32, device=x.device)
+    # f16 M: one scale exponent per 64 x 64 tile of each component
+    m16e = (torch.empty(36 * (-(-T // 64)) * (cout_p // 64), dtype=torch.int32, device=x.device)
+            if m16 else None)
     evg = _probe(tag + ".gemm" if tag else None)   # the batched MFMA GEMM alone
-    call("nsm_wino_gemm_f16m" if m16 else "nsm_wino_gemm_f16", ptr(V), ptr(U), B, H, W, cin_p,
-         cout_p, 4, ptr(Mb), ptr(amax[0]), bv, ptr(amax[1]), bu, st)
+    if m16:
+        call("nsm_wino_gemm_f16m", ptr(V), ptr(U), B, H, W, cin_p, cout_p, 4, ptr(Mb), ptr(m16e),
+             ptr(amax[0]), bv, ptr(amax[1]), bu, st)
+    else:
+        call("nsm_wino_gemm_f16", ptr(V), ptr(U), B, H, W, cin_p, cout_p, 4, ptr(Mb), ptr(amax[0]),
+             bv, ptr(amax[1]), bu, st)
     if evg is not None:
         evg.record()
     if not keep_v:
@@ -405,9 +412,9 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     y = torch.empty(B * H * W, cout_p, dtype=BF16, device=x.device)
     if act is not None:
         assert not stats
-        call("nsm_wino_output_bf16m_act", ptr(Mb), B, H, W, cin_p, cout_p, 4, ptr(amax[0]), bv,
-             ptr(amax[1]), bu, ptr(bias), ptr(y), y.stride(0), ptr(act.scale), ptr(act.shift), 0.2,
-             st)
+        call("nsm_wino_output_bf16m_act", ptr(Mb), ptr(m16e), B, H, W, cin_p, cout_p, 4,
+             ptr(amax[0]), bv, ptr(amax[1]), bu, ptr(bias), ptr(y), y.stride(0), ptr(act.scale),
+             ptr(act.shift), 0.2, st)
         if ev is not None:
             ev.record()
         return (y, None, V) if keep_v else (y, None)
@@ -417,8 +424,8 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
         part = Partials(empty(nslot * 3 * cout_p, device=x.device), nslot, 0)
     pb = ptr(part.buf) if part is not None else None
     if m16:
-        call("nsm_wino_output_bf16m", ptr(Mb), B, H, W, cin_p, cout_p, 4, ptr(amax[0]), bv,
-             ptr(amax[1]), bu, ptr(bias), ptr(y), y.stride(0), pb, nslot, st)
+        call("nsm_wino_output_bf16m", ptr(Mb), ptr(m16e), B, H, W, cin_p, cout_p, 4, ptr(amax[0]),
+             bv, ptr(amax[1]), bu, ptr(bias), ptr(y), y.stride(0), pb, nslot, st)
     else:
         call("nsm_wino_output_bf16", ptr(Mb), B, H, W, cout_p, 4, ptr(bias), ptr(y), y.stride(0),
              pb, nslot, st)

@@ -142,9 +142,12 @@ def test_configs2_b64_bf16_small_res_vs_oracle(device, spread):
     ref_xg, our_xg = _rel(xgbf, xg32), _rel(x.grad.cpu(), xg32)
     print(f"configs[2] B=64 128^2: out ours {our_out:.2e} ref-autocast {ref_out:.2e}; "
           f"x_grad ours {our_xg:.2e} ref {ref_xg:.2e}")
-    worst = max(((_rel(prm.grad.cpu(), g32[k]) - 1e-2) / max(_rel(gbf[k], g32[k]), 1e-12), k)
-                for k, prm in m.named_parameters()
-                if not (k.endswith(".0.bias") or k.endswith(".4.bias")))
+    ratios = sorted((((_rel(prm.grad.cpu(), g32[k]) - 1e-2) / max(_rel(gbf[k], g32[k]), 1e-12), k,
+                      round(_rel(prm.grad.cpu(), g32[k]), 4), round(_rel(gbf[k], g32[k]), 4))
+                     for k, prm in m.named_parameters()
+                     if not (k.endswith(".0.bias") or k.endswith(".4.bias"))), reverse=True)
+    print("worst grad ratios (ours - 0.01) / ref-autocast:", ratios[:6])
+    worst = ratios[0][:2]
     record_margin("configs2_b64_bf16_128" + ("_spread" if spread else ""), out_max_abs=our_out,
                   out_bound=1.5 * ref_out, x_grad_rel_l2=our_xg, x_grad_bound=1.5 * ref_xg,
                   worst_grad_ratio=worst[0], worst_grad=worst[1], grad_ratio_bound=1.5)
