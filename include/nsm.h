@@ -166,6 +166,9 @@ int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int W, int cin
  * zeroed first; NaN counts above +Inf): the maximum a GEMM operand needs when
  * its producer does not record it. */
 int nsm_absmax(const float* x, int64_t n, uint32_t* out, void* stream);
+/* p[0..n) = 0 (uint32 words): the activation-maximum slots of a forward whose
+ * weight preparation does not run (frozen inference weights, GraphedUnet) */
+int nsm_zero_u32(uint32_t* p, int64_t n, void* stream);
 /* the same over n bf16 values (x 16-B aligned): the input maximum of a bf16
  * F(4x4) Winograd conv whose input producer records none (the decoder's lazy
  * resampling, NSM_LAZY_DECODER=1) */

@@ -5,6 +5,7 @@
 //  * the output-range assertion of CustomLoss / PerturbationLoss
 //    (customLoss.py:131, pert_loss.py:131: min >= 0 and max <= 1, NaN fails)
 //    as a sticky device flag, so the check costs no host synchronisation.
+#include <algorithm>
 #include "nsm_common.h"
 
 namespace nsm {
@@ -101,6 +102,11 @@ __global__ void __launch_bounds__(256) dropout_masks_kernel(const int* __restric
 // profiling marker (nsm_stage_mark): no work, its grid encodes the stage
 __global__ void __launch_bounds__(64) stage_mark_kernel(int code) {}
 
+__global__ void __launch_bounds__(256) zero_u32_kernel(uint32_t* __restrict__ p, long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    p[i] = 0u;
+}
+
 }  // namespace nsm
 
 using namespace nsm;
@@ -109,6 +115,15 @@ extern "C" int nsm_stage_mark(int code, void* stream) {
   NSM_CHECK_ARG(code >= 0 && code < 4096, "stage_mark: bad code");
   hipLaunchKernelGGL(stage_mark_kernel, dim3(code + 1), dim3(64), 0, as_stream(stream), code);
   NSM_LAUNCH_CHECK("stage_mark");
+  return 0;
+}
+
+extern "C" int nsm_zero_u32(uint32_t* p, int64_t n, void* stream) {
+  NSM_CHECK_ARG(p && n > 0, "zero_u32: bad args");
+  const long long g = std::min<long long>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(zero_u32_kernel, dim3((unsigned)g), dim3(256), 0, as_stream(stream), p,
+                     (long long)n);
+  NSM_LAUNCH_CHECK("zero_u32");
   return 0;
 }
 

@@ -36,6 +36,7 @@ _SIGS = {
     "nsm_wino_gemm": (I, [P, P, I, I, I, I, I, I, P, P]),
     "nsm_wino_gemm_s": (I, [P, P, I, I, I, I, I, I, P, P, P, P]),
     "nsm_absmax": (I, [P, L, P, P]),
+    "nsm_zero_u32": (I, [P, L, P]),
     "nsm_absmax_bf16": (I, [P, L, P, P]),
     "nsm_pmc_calib": (I, [I, P, P, L, P]),
     "nsm_to_h2": (I, [P, L, I, P, F, P, P]),

@@ -15,6 +15,16 @@ the consumers' operand loaders apply (no separate BN pass exists in eval).
 
 The returned tensor is the graph's static output buffer: it is overwritten by
 the next call (clone it to keep it).
+
+Frozen weights (static_weights=True, default): the weight layouts of the step
+(the prep launches) and the eval BatchNorm vectors are prepared once, before
+the capture (unet.FrozenWeights), so a frame replays only the per-frame
+kernels — the reference's infer.py loads its weights once and runs frames.
+The parameters' and BN buffers' version counters are checked at each call:
+after any change (a torch optimizer step, load_state_dict, a FlatAdamW step or
+a training forward, which bump them) the kept layouts are rewritten in place
+(refresh()) before the replay, so the output always reflects the current
+weights.
 """
 import torch
 
@@ -22,25 +32,46 @@ from ._lib import require_gpu
 
 
 class GraphedUnet:
-    def __init__(self, model, example, warmup=2):
+    def __init__(self, model, example, warmup=2, static_weights=True):
+        from .unet import FrozenWeights
         require_gpu(example, "GraphedUnet example input")
         self.model = model
         self.was_training = model.training
         model.eval()
         self.shape, self.dtype = tuple(example.shape), example.dtype
         self.static_in = example.detach().clone()
+        self.frozen = FrozenWeights(model) if static_weights else None
         side = torch.cuda.Stream(device=example.device)
         side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side), torch.no_grad():
-            for _ in range(warmup):           # settle the caching allocator
-                model(self.static_in)
-        torch.cuda.current_stream().wait_stream(side)
-        self.graph = torch.cuda.CUDAGraph()
-        with torch.no_grad(), torch.cuda.graph(self.graph):
-            self.static_out = model(self.static_in)
+        if self.frozen is not None:
+            self.frozen.__enter__()
+        try:
+            with torch.cuda.stream(side), torch.no_grad():
+                for _ in range(warmup):           # settle the caching allocator (and the layouts)
+                    model(self.static_in)
+            torch.cuda.current_stream().wait_stream(side)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.no_grad(), torch.cuda.graph(self.graph):
+                self.static_out = model(self.static_in)
+        finally:
+            if self.frozen is not None:
+                self.frozen.__exit__(None, None, None)
         model.train(self.was_training)
         # the graph holds raw parameter / buffer addresses: replay must see the same storage
         self._ptrs = self._addresses()
+        self._vers = self._versions()
+
+    def _versions(self):
+        return [t._version for t in list(self.model.parameters()) + list(self.model.buffers())]
+
+    def refresh(self):
+        """Rewrite the frozen weight layouts / BN vectors from the current
+        parameters and running statistics (in place; eager, on the current
+        stream). Called automatically when a version counter moved."""
+        if self.frozen is not None:
+            with torch.no_grad():
+                self.frozen.refresh()
+        self._vers = self._versions()
 
     def _addresses(self):
         return [t.data_ptr() for t in list(self.model.parameters()) + list(self.model.buffers())]
@@ -50,6 +81,8 @@ class GraphedUnet:
             raise RuntimeError("GraphedUnet: the model's parameters or buffers were re-allocated "
                                "after capture (e.g. FlatAdamW re-homed them, or .to()); the "
                                "captured graph would read freed memory — capture again")
+        if self.frozen is not None and self._versions() != self._vers:
+            self.refresh()
 
     def __call__(self, x):
         if tuple(x.shape) != self.shape or x.dtype != self.dtype:

@@ -688,10 +688,16 @@ def bn_eval(bn_mod, C, c_real, eps, device, gamma=None, beta=None):
     st.gamma = gamma if gamma is not None else pad_vec(bn_mod.weight.detach(), C)
     beta = beta if beta is not None else pad_vec(bn_mod.bias.detach(), C)
     st.beta = beta
-    call("nsm_bn_finalize_eval", ptr(bn_mod.running_mean), ptr(bn_mod.running_var), ptr(st.gamma),
-         ptr(beta), C, c_real, eps, ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift),
-         stream())
+    bn_eval_into(st, bn_mod, C, c_real, eps)
     return st
+
+
+def bn_eval_into(st, bn_mod, C, c_real, eps):
+    """(Re)compute an eval BNState's vectors in place from the running
+    statistics and st.gamma / st.beta (nsm_bn_finalize_eval)."""
+    call("nsm_bn_finalize_eval", ptr(bn_mod.running_mean), ptr(bn_mod.running_var), ptr(st.gamma),
+         ptr(st.beta), C, c_real, eps, ptr(st.mean), ptr(st.invstd), ptr(st.scale), ptr(st.shift),
+         stream())
 
 
 def bn_act(y, st, slope=0.2, res=None, out=None, mask=None, HW=0, amax=None):

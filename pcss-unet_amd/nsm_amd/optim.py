@@ -129,6 +129,15 @@ FLAG_NAMES = ("skip", "repaired", "severe", "nonfinite", "huge", "postclip", "n_
               "n_zeroed")
 
 
+def _bump(params):
+    """The parameters were rewritten in place by HIP kernels, invisibly to
+    autograd's version counters: bump them, so caches keyed on the versions
+    (infer.GraphedUnet's frozen weight layouts) see the change."""
+    with torch.no_grad():
+        for p in params:
+            torch.autograd.graph.increment_version(p)
+
+
 class FlatAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=7e-4, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-3,
                  max_grad_norm=None, world_size=1, sanitize=False, grad_scale=1.0, seed=None):
@@ -230,6 +239,7 @@ class FlatAdamW(torch.optim.Optimizer):
                  ptr(self._blk_seg), ptr(self._blk_lo), ptr(self._blk_hi), self._nblk,
                  ptr(self._seg_coef), ptr(self.flags), ptr(self._step_dev), float(grp["lr"]),
                  float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]), st)
+            _bump(params)
             return None
         self.step_count += 1
         coef = None
@@ -241,6 +251,7 @@ class FlatAdamW(torch.optim.Optimizer):
         call("nsm_adamw_step", ptr(self.flat), ptr(g), ptr(self.exp_avg), ptr(self.exp_avg_sq), n,
              float(grp["lr"]), float(b1), float(b2), float(grp["eps"]), float(grp["weight_decay"]),
              self.step_count, ptr(coef), st)
+        _bump(params)
         return None
 
     def zero_grad(self, set_to_none=True):

@@ -497,7 +497,7 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
     ci, co = c0.in_channels, c4.out_channels
     cip, cop = ops.pad32(ci), ops.pad32(co)
     dtype = xin.dtype
-    bn1 = ops.bn_eval(bn1m, cip, ci, bn1m.eps, xin.device, gamma=pw.vec("g1"), beta=pw.vec("be1"))
+    bn1 = _bn_eval(bn1m, cip, ci, bn1m.eps, xin.device, pw.vec("g1"), pw.vec("be1"))
     b1 = pw.vec("b1")
     if cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
         tile = wino_tile(cip, H, W)
@@ -517,7 +517,7 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
         assert src_hw is None
         A1 = ops.conv_fwd_act(xin, B, H, W, pw.w1(ops.PACK_FWD), b1, cip, 3, bn1, slope=SLOPE,
                               tag=name + ".conv.0.fwd")
-    bn2 = ops.bn_eval(bn2m, cop, co, bn2m.eps, xin.device, gamma=pw.vec("g2"), beta=pw.vec("be2"))
+    bn2 = _bn_eval(bn2m, cop, co, bn2m.eps, xin.device, pw.vec("g2"), pw.vec("be2"))
     Z = ops.conv_fwd_act(A1, B, H, W, pw.w2(ops.PACK_FWD), pw.vec("b2"), cop, 1, bn2, res=res,
                          slope=SLOPE, tag=name + ".conv.4.fwd")
     s = _BlockSaved()
@@ -604,7 +604,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
                            bound=(_slot(am, AM_A1), mask_max if mask is not None else 1.0)
                            if h2x else None)
     else:
-        bn1 = ops.bn_eval(bn1m, cip, ci, eps1, xin.device, gamma=pw.vec("g1"), beta=pw.vec("be1"))
+        bn1 = _bn_eval(bn1m, cip, ci, eps1, xin.device, pw.vec("g1"), pw.vec("be1"))
     A1 = None
     if h2x:
         A1 = ops.bn_act_h2(Y1, bn1, SLOPE, mask=mask, HW=H * W, bound=_slot(am, AM_A1))
@@ -624,7 +624,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
         bn2 = ops.bn_train(Y2, bn2m, co, bn2m.momentum, eps2, part=part2, gamma=pw.vec("g2"),
                            beta=pw.vec("be2"))
     else:
-        bn2 = ops.bn_eval(bn2m, cop, co, eps2, xin.device, gamma=pw.vec("g2"), beta=pw.vec("be2"))
+        bn2 = _bn_eval(bn2m, cop, co, eps2, xin.device, pw.vec("g2"), pw.vec("be2"))
     s = _BlockSaved()
     s.X, s.Y1, s.Y2, s.bn1, s.bn2, s.mask = X, Y1, Y2, bn1, bn2, mask
     s.pw = pw
@@ -830,6 +830,65 @@ def block_shapes(Rh, Rw):
 PREP_BATCH = os.environ.get("NSM_PREP_BATCH", "1") != "0"
 
 
+class FrozenWeights:
+    """Inference with frozen weights (nsm_amd.infer.GraphedUnet): inside
+    `with FrozenWeights(model):` the first eval forward prepares the weight
+    layouts (the prep launches) and the eval BatchNorm vectors (one
+    nsm_bn_finalize_eval per BN) as usual and keeps them; later forwards skip
+    those launches (a graph captured then holds only the per-frame work: the
+    reference's infer.py loads its weights once, infer.py:40-60). The kept
+    buffers stay valid while the weights and BN statistics do: refresh()
+    rewrites them in place (same addresses, so a captured graph stays valid)
+    after any change."""
+
+    def __init__(self, mod):
+        self.mod = mod
+        self.sws = {}      # key -> StepWeights (persistent output buffers)
+        self.bn = {}       # (id(bn module), C) -> (bn module, C, c_real, eps, BNState)
+        self.ready = False
+
+    def __enter__(self):
+        global _FROZEN
+        if _FROZEN is not None:
+            raise RuntimeError("FrozenWeights contexts do not nest")
+        _FROZEN = self
+        return self
+
+    def __exit__(self, *exc):
+        global _FROZEN
+        _FROZEN = None
+        return False
+
+    def bn_eval(self, bn_mod, C, c_real, eps, device, gamma, beta):
+        key = (id(bn_mod), C)
+        ent = self.bn.get(key)
+        if ent is None:
+            st = ops.bn_eval(bn_mod, C, c_real, eps, device, gamma=gamma, beta=beta)
+            self.bn[key] = (bn_mod, C, c_real, eps, st)
+            return st
+        return ent[4]
+
+    def refresh(self):
+        """Rewrite the kept weight layouts and BN vectors from the module's
+        current parameters and running statistics (same buffers)."""
+        for sw in self.sws.values():
+            if not sw.valid(self.mod):
+                raise RuntimeError("FrozenWeights.refresh: the parameters were re-allocated "
+                                   "(e.g. FlatAdamW re-homed them); build a new one")
+            sw.run()
+        for bn_mod, C, c_real, eps, st in self.bn.values():
+            ops.bn_eval_into(st, bn_mod, C, c_real, eps)
+
+
+_FROZEN = None
+
+
+def _bn_eval(bn_mod, C, c_real, eps, device, gamma, beta):
+    if _FROZEN is not None:
+        return _FROZEN.bn_eval(bn_mod, C, c_real, eps, device, gamma, beta)
+    return ops.bn_eval(bn_mod, C, c_real, eps, device, gamma=gamma, beta=beta)
+
+
 def _step_weights(mod, dtype, Rh, Rw, training, act_slots=None):
     """The step's weight layouts, written by ONE prep launch (cached per
     signature; rebuilt when the parameters moved, e.g. FlatAdamW re-homing).
@@ -845,6 +904,15 @@ def _step_weights(mod, dtype, Rh, Rw, training, act_slots=None):
     if sw is None or not sw.valid(mod):
         sw = cache[key] = StepWeights(mod, dtype, block_shapes(Rh, Rw), training,
                                       WINOGRAD_MIN_CHANNELS, wino_tile, h2=h2)
+    fz = _FROZEN if not training else None
+    if fz is not None and fz.ready and fz.sws.get(key) is sw:
+        # frozen inference weights: the layouts are kept; only the forward's
+        # activation-maximum slots need zeroing
+        if act_slots is not None:
+            call("nsm_zero_u32", ptr(act_slots), act_slots.numel(), stream())
+        return sw
+    if fz is not None:
+        fz.sws[key] = sw
     sw.run(act_slots)
     return sw
 
@@ -950,6 +1018,15 @@ class _UnetFn(torch.autograd.Function):
         with ops.stage("head.fwd"):
             out = ops.head_fwd(z9, B, Rh, Rw, mod.conv10.weight.detach(), mod.conv10.bias.detach())
 
+        if _FROZEN is not None and not training:
+            _FROZEN.ready = True   # layouts and BN vectors kept from this forward on
+        if training:
+            # the running statistics changed in place (HIP kernels): bump their
+            # version counters so version-keyed caches (GraphedUnet) see it
+            for bm in mod.modules():
+                if isinstance(bm, nn.BatchNorm2d):
+                    for b in (bm.running_mean, bm.running_var, bm.num_batches_tracked):
+                        torch.autograd.graph.increment_version(b)
         ctx.mod = mod
         ctx.saved_blocks = saved
         ctx.ups = ups

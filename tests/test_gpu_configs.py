@@ -234,6 +234,37 @@ def test_configs4_graphed_1080p_equals_eager(device, dtype):
     assert torch.equal(gu(x2), e2)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_graphed_unet_frozen_weights_follow_changes(device, dtype):
+    """GraphedUnet's frozen weight layouts / eval BN vectors (prepared once,
+    outside the graph): bitwise equal to the eager forward, and again after the
+    weights change by a torch in-place op, after a FlatAdamW step on the same
+    storage and after a training forward moved the BN running statistics (the
+    version counters trigger the in-place refresh)."""
+    import nsm_amd
+    m = build(device, 7, 0.2, make_state(7, 42)).set_compute_dtype(dtype)
+    opt = nsm_amd.FlatAdamW(m.parameters(), lr=1e-3)    # re-home first: the graph keeps addresses
+    x = torch.randn(2, 7, 256, 320, device=device)
+    gu = nsm_amd.GraphedUnet(m, x)
+
+    def eager():
+        m.eval()
+        with torch.no_grad():
+            return m(x)
+
+    assert torch.equal(gu(x), eager())
+    with torch.no_grad():
+        m.conv6.conv[0].weight.mul_(1.5)
+        m.conv3.conv[5].bias.add_(0.25)
+    assert torch.equal(gu(x), eager())
+    m.train()
+    out = m(x.clone().requires_grad_(True))        # moves the running statistics
+    nsm_amd.CustomLoss(device, 0.9, vgg_weights=False)(out, torch.rand_like(out)).backward()
+    opt.step()
+    opt.zero_grad()
+    assert torch.equal(gu(x), eager())
+
+
 def test_graphed_unet_detects_rehomed_params(device):
     import nsm_amd
     m = nsm_amd.Unet(in_ch=7).to(device)
