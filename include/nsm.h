@@ -220,6 +220,12 @@ int nsm_wino_dual_input_h2(const float* dy, int lddy, int B, int H, int W, int c
  * nsm_wino_output_stats, nsm_wino_stat_slots). tile 4 only. */
 int nsm_wino_input_f16(const void* x, int ldx, int B, int H, int W, int cin_p, int tile, void* V,
                        const uint32_t* amax_x, void* stream);
+/* nsm_wino_input_f16 of the align_corners bilinear resize of x (bf16 [B][hi][wi]
+ * [cin_p] NHWC, ld ldx) to H x W (the decoder's x2 upsample, Unetmodel.py:
+ * 122-130), sampled per patch element and rounded to bf16 as the materialised
+ * upsample would be; amax_x: max|x| (it bounds the upsample too). */
+int nsm_wino_input_f16_resize(const void* x, int ldx, int B, int hi, int wi, int H, int W,
+                              int cin_p, int tile, void* V, const uint32_t* amax_x, void* stream);
 int nsm_wino_gemm_f16(const void* V, const void* U, int B, int H, int W, int cin_p, int cout_p,
                       int tile, float* Mb, const uint32_t* amax_v, float beta_v,
                       const uint32_t* amax_u, float beta_u, void* stream);

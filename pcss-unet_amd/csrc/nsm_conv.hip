@@ -3416,6 +3416,108 @@ __global__ void __launch_bounds__(256) wino_input_f16_kernel(const bf16_t* __res
   }
 }
 
+// wino_input_f16_kernel of the decoder's x2 upsample of x (bf16 [B][hi][wi][C]
+// NHWC, align_corners bilinear, Unetmodel.py:122-130) sampled per patch
+// element: each value is interpolated in fp32 as resize_fwd8_kernel does and
+// rounded to bf16 (what the materialised upsample would hold), then
+// transformed; the upsampled tensor is never written or re-read. Source rows
+// are x-interpolated once and kept while consecutive patch rows reuse them
+// (a tile's 6 patch rows of a x2 upsample touch ~4 source rows).
+template <int MT>
+__global__ void __launch_bounds__(256) wino_input_f16_up_kernel(
+    const bf16_t* __restrict__ x, int ld, int hi, int wi, float sh, float sw, int H, int W, int C,
+    int TH, int TW, long long T, bf16_t* __restrict__ V, H2Scale hsc) {
+  constexpr int A = MT + 2;
+  const int C4 = C / 4;
+  const long long total = T * C4;
+  const float hs = exp2i(h2_exp(hsc));  // every lane (amax_read: a wave reduction)
+  const size_t plane = (size_t)T * C;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    const long long t = i / C4;
+    const int tx = (int)(t % TW);
+    const long long r = t / TW;
+    const int ty = (int)(r % TH);
+    const long long b = r / TH;
+    int x0[A], x1[A];
+    float lx0[A], lx1[A];
+#pragma unroll
+    for (int e = 0; e < A; ++e)
+      lin_idx(sw, min(max(MT * tx - 1 + e, 0), W - 1), wi, x0[e], x1[e], lx0[e], lx1[e]);
+    f32x4 h0[A], h1[A];
+    int ya = -1, yb = -1;  // source rows held in h0, h1
+    f32x4 sc[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const int yy = MT * ty - 1 + a;
+      int y0, y1;
+      float ly0, ly1;
+      lin_idx(sh, min(max(yy, 0), H - 1), hi, y0, y1, ly0, ly1);
+      if (y0 != ya) {
+        if (y0 == yb) {
+#pragma unroll
+          for (int e = 0; e < A; ++e) h0[e] = h1[e];
+        } else {
+          const bf16_t* r0 = x + ((size_t)b * hi + y0) * wi * ld + c;
+#pragma unroll
+          for (int e = 0; e < A; ++e)
+            h0[e] = lx0[e] * ld4(r0 + (size_t)x0[e] * ld) + lx1[e] * ld4(r0 + (size_t)x1[e] * ld);
+        }
+        ya = y0;
+      }
+      if (y1 != yb) {
+        if (y1 == ya) {
+#pragma unroll
+          for (int e = 0; e < A; ++e) h1[e] = h0[e];
+        } else {
+          const bf16_t* r1 = x + ((size_t)b * hi + y1) * wi * ld + c;
+#pragma unroll
+          for (int e = 0; e < A; ++e)
+            h1[e] = lx0[e] * ld4(r1 + (size_t)x0[e] * ld) + lx1[e] * ld4(r1 + (size_t)x1[e] * ld);
+        }
+        yb = y1;
+      }
+      const bool rin = (unsigned)yy < (unsigned)H;
+      f32x4 d[A];
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const bool in = rin && (unsigned)(MT * tx - 1 + e) < (unsigned)W;
+        const f32x4 v = ly0 * h0[e] + ly1 * h1[e];
+        d[e] = in ? f32x4{round_bf(v.x), round_bf(v.y), round_bf(v.z), round_bf(v.w)}
+                  : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      wcol_row<CBt<MT>>(sc, d, a);
+    }
+    bf16_t* out = V + (size_t)t * C + c;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      f32x4 v[A];
+      wmat<CBt<MT>>(sc[a], v);
+#pragma unroll
+      for (int e = 0; e < A; ++e)
+        *(u32x2*)(out + (a * A + e) * plane) =
+            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * hs, f16x4v));
+    }
+  }
+}
+
+extern "C" int nsm_wino_input_f16_resize(const void* x, int ldx, int B, int hi, int wi, int H, int W,
+                                         int cin_p, int tile, void* V, const uint32_t* amax_x,
+                                         void* stream) {
+  NSM_CHECK_ARG(x && V && amax_x && tile == 4 && cin_p % 32 == 0 && ldx % 4 == 0 && ldx >= cin_p &&
+                    hi > 0 && wi > 0,
+                "wino_input_f16_resize: bad args (tile 4 only)");
+  NSM_CHECK_ARG(((uintptr_t)x % 8) == 0 && ((uintptr_t)V % 16) == 0, "wino_input_f16_resize: alignment");
+  WinoGeom g;
+  NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input_f16_resize: bad shape");
+  hipLaunchKernelGGL(wino_input_f16_up_kernel<4>, dim3(grid_1d(g.T * cin_p / 4)), dim3(256), 0,
+                     as_stream(stream), (const bf16_t*)x, ldx, hi, wi, ac_scale(hi, H), ac_scale(wi, W),
+                     H, W, cin_p, g.TH, g.TW, g.T, (bf16_t*)V, H2Scale{amax_x, wino_beta(4, 0)});
+  NSM_LAUNCH_CHECK("wino_input_f16_resize");
+  return 0;
+}
+
 extern "C" int nsm_wino_input_f16(const void* x, int ldx, int B, int H, int W, int cin_p, int tile,
                                   void* V, const uint32_t* amax_x, void* stream) {
   NSM_CHECK_ARG(x && V && amax_x && tile == 4 && cin_p % 32 == 0 && ldx % 4 == 0 && ldx >= cin_p,

@@ -46,6 +46,7 @@ _SIGS = {
     "nsm_wino_dual_input_h2": (I, [P, I, I, I, I, I, I, P, P, P, P]),
     "nsm_wino_dual_input_bn_h2": (I, [P, I, P, I, I, I, I, I, I, P, P, F, P, P, P, P, P, P, P]),
     "nsm_wino_input_f16": (I, [P, I, I, I, I, I, I, P, P, P]),
+    "nsm_wino_input_f16_resize": (I, [P, I, I, I, I, I, I, I, I, P, P, P]),
     "nsm_wino_gemm_f16": (I, [P, P, I, I, I, I, I, I, P, P, F, P, F, P]),
     "nsm_wino_output_bf16": (I, [P, I, I, I, I, I, P, P, I, P, I, P]),
     "nsm_wino_gemm_f16m": (I, [P, P, I, I, I, I, I, I, P, P, P, F, P, F, P]),

@@ -369,7 +369,7 @@ BF16_M16 = os.environ.get("NSM_BF16_M16", "1") != "0"
 
 
 def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, keep_v=False,
-                     m16=None, v_in=None, act=None):
+                     m16=None, v_in=None, act=None, src_hw=None):
     """The bf16 path's 3x3 (pad 1) forward by Winograd F(4x4,3x3) on single-plane
     scaled f16 operands (nsm_wino_input_f16 / _gemm_f16 / _output_bf16): x
     [B*H*W, cin_p] bf16, U the prep-kind-6 filters [36][cout_p][cin_p] f16,
@@ -378,7 +378,9 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     as f16 (nsm_wino_gemm_f16m / _output_bf16m) instead of fp32; v_in: V
     already formed from x (wino_dual_f16), the input transform skipped.
     act: eval BNState — the output transform writes lrelu(BN(y)) instead of y
-    (nsm_wino_output_bf16m_act; f16 M, no statistics).
+    (nsm_wino_output_bf16m_act; f16 M, no statistics). src_hw=(hi, wi): x is
+    [B*hi*wi, cin_p], convolved after the align_corners resize to H x W that
+    the input transform samples (nsm_wino_input_f16_resize; amax[0] = max|x|).
     Returns (y bf16 [B*H*W, cout_p], Partials of the rounded y | None) and,
     with keep_v, V (the weight gradient's operand)."""
     from ._lib import lib
@@ -389,7 +391,14 @@ def conv3x3_wino_f16(x, B, H, W, U, bias, cout_p, amax, stats=True, tag=None, ke
     ev = _probe(tag)
     if v_in is not None:
         V = v_in
+    elif src_hw is not None:
+        hi, wi = src_hw
+        assert x.shape[0] == B * hi * wi, (x.shape, B, hi, wi)
+        V = torch.empty(36 * T * cin_p, dtype=H2, device=x.device)
+        call("nsm_wino_input_f16_resize", ptr(x), x.stride(0), B, hi, wi, H, W, cin_p, 4, ptr(V),
+             ptr(amax[0]), st)
     else:
+        assert x.shape[0] == B * H * W, (x.shape, B, H, W)
         V = torch.empty(36 * T * cin_p, dtype=H2, device=x.device)
         call("nsm_wino_input_f16", ptr(x), x.stride(0), B, H, W, cin_p, 4, ptr(V), ptr(amax[0]), st)
     m16 = (BF16_M16 if m16 is None else m16) or act is not None

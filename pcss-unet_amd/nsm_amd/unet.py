@@ -27,6 +27,7 @@ import torch.nn as nn
 
 from . import ops, optim
 from ._lib import call, ptr, require_gpu, stream
+from . import prep
 from .prep import H2_WINO, LazyBlockWeights, StepWeights
 
 SLOPE = 0.2
@@ -483,11 +484,19 @@ def _is_h2(U):
     return U is not None and U.dtype == ops.H2
 
 
-def fuses_resize(blk, dtype):
+def fuses_resize(blk, dtype, training=True):
     """True when the block's 3x3 conv runs on Winograd and can sample the
-    decoder's x2 upsample inside its input transform (UP_IN_WINO)."""
-    return (UP_IN_WINO and dtype == torch.float32
-            and ops.pad32(blk.conv[0].in_channels) >= WINOGRAD_MIN_CHANNELS)
+    decoder's x2 upsample inside its input transform (UP_IN_WINO): the fp32
+    layers from WINOGRAD_MIN_CHANNELS, the bf16 path's F(4x4) f16 layers
+    (prep.bf16_wino; nsm_wino_input_f16_resize)."""
+    cip = ops.pad32(blk.conv[0].in_channels)
+    if not UP_IN_WINO:
+        return False
+    if dtype == torch.float32:
+        return cip >= WINOGRAD_MIN_CHANNELS
+    # (bf16 training: the weight gradient must come from the kept V, as the
+    # block input itself is never materialised)
+    return PREP_BATCH and prep.bf16_wino(cip, dtype, training) and (WGRAD_F16 or not training)
 
 
 def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
@@ -507,12 +516,12 @@ def _block_eval_fused(blk, xin, B, H, W, pw, name, src_hw, res, am=None):
     elif _has_f16_u(pw) and am is not None:
         # bf16 eval: Winograd F(4x4) on f16 operands, BN + LeakyReLU in the
         # output transform; the V scale from max|x| (the fused epilogues that
-        # wrote x record none)
-        assert src_hw is None
+        # wrote x record none; with src_hw, x is the source of the decoder's
+        # upsample the input transform samples, and bounds it)
         ops.absmax(xin, _slot(am, AM_X))
         A1 = ops.conv3x3_wino_f16(xin, B, H, W, pw.Uf16(), b1, cip,
                                   amax=(_slot(am, AM_X), pw.amax_Uf16()), stats=False,
-                                  tag=name + ".conv.0.fwd", act=bn1)[0]
+                                  tag=name + ".conv.0.fwd", act=bn1, src_hw=src_hw)[0]
     else:
         assert src_hw is None
         A1 = ops.conv_fwd_act(xin, B, H, W, pw.w1(ops.PACK_FWD), b1, cip, 3, bn1, slope=SLOPE,
@@ -545,7 +554,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
     xin = X if src is None else src[0]
     src_hw = None if src is None else (src[1], src[2])
     assert xin.shape[1] == (2 * cip if xin.dtype == ops.H2 else cip), (xin.shape, cip)
-    assert src is None or fuses_resize(blk, xin.dtype)
+    assert src is None or fuses_resize(blk, xin.dtype, training)
     dtype = xin.dtype
     if pw is None:
         pw = LazyBlockWeights(blk, dtype)
@@ -573,10 +582,11 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
             part1 = ops.bn_partials(Y1)
     elif _has_f16_u(pw):
         # bf16: Winograd F(4x4) forward on single-plane scaled f16 operands
+        # (src: the decoder's x2 upsample sampled by the input transform)
         keep = WGRAD_F16 and training
-        r = ops.conv3x3_wino_f16(X, B, H, W, pw.Uf16(), b1, cip,
+        r = ops.conv3x3_wino_f16(xin, B, H, W, pw.Uf16(), b1, cip,
                                  amax=(_slot(am, AM_X), pw.amax_Uf16()), stats=training,
-                                 tag=name + ".conv.0.fwd", keep_v=keep)
+                                 tag=name + ".conv.0.fwd", keep_v=keep, src_hw=src_hw)
         Y1, part1 = r[0], r[1]
         Vf16 = r[2] if keep else None
         if training and part1 is None:
@@ -989,8 +999,11 @@ class _UnetFn(torch.autograd.Function):
                     if up is None:
                         cur = cur.materialise(SLOPE) if lazy else cur
                         up = ops.up2_resize(cur, B, h, w, th, tw)
-                elif fuses_resize(mod.block(k), cdt):  # sampled by the Winograd input transform
-                    cur = cur.materialise(SLOPE) if lazy else cur
+                elif fuses_resize(mod.block(k), cdt, training):  # sampled by the input transform
+                    if lazy:
+                        cur = cur.materialise(SLOPE)
+                        if amax is not None:   # (bn_act of a Lazy records no maximum)
+                            ops.absmax(cur, _x_slot(amax, k))
                     up, src = None, (cur, h, w)
                 elif lazy:                 # the previous block output computed on load
                     up = ops.resize_act(cur, B, h, w, h2, w2, SLOPE)

@@ -158,3 +158,32 @@ def test_wino_dual_bn_f16_matches_apply_then_dual(device, B, H, W, c, drop):
         print(f"{name}: mismatched {frac:.2e}, max diff {diff.max().item():.3e} of {b.abs().max().item():.3e}")
         assert torch.isfinite(a).all() and b.abs().max().item() > 0
         assert frac <= 2e-3 and diff.max().item() <= 2.0 ** -5 * b.abs().max().item(), (name, frac)
+
+
+@pytest.mark.parametrize("B,hi,wi,c", [(2, 16, 16, 512), (1, 17, 30, 512), (3, 8, 11, 1024)])
+def test_wino_input_f16_resize_matches_materialised_upsample(device, B, hi, wi, c):
+    """nsm_wino_input_f16_resize (the decoder's x2 upsample sampled inside the
+    F(4x4) input transform, each value rounded to bf16) equals the transform
+    of the materialised bf16 upsample (nsm_resize_fwd, then nsm_wino_input_f16)
+    under the same scale slot, up to FMA-contraction ulps of the interpolation."""
+    from nsm_amd import ops
+    g = torch.Generator().manual_seed(B * hi * wi + c)
+    x = torch.randn(B * hi * wi, c, generator=g).to(torch.bfloat16).to(device)
+    H, W = 2 * hi, 2 * wi
+    am = ops.amax_slots(1, device)
+    ops.absmax(x, am)
+    T = ops.wino_tiles(B, H, W, 4)
+    V1 = torch.empty(36 * T * c, dtype=ops.H2, device=device)
+    ops.call("nsm_wino_input_f16_resize", ops.ptr(x), x.stride(0), B, hi, wi, H, W, c, 4, ops.ptr(V1),
+             ops.ptr(am), ops.stream())
+    up = ops.resize(x, B, hi, wi, H, W)
+    V0 = torch.empty_like(V1)
+    ops.call("nsm_wino_input_f16", ops.ptr(up), up.stride(0), B, H, W, c, 4, ops.ptr(V0), ops.ptr(am),
+             ops.stream())
+    torch.cuda.synchronize()
+    a, b = V1.float(), V0.float()
+    diff = (a - b).abs()
+    frac = (diff > 0).float().mean().item()
+    print(f"mismatched {frac:.2e}, max diff {diff.max().item():.3e} of {b.abs().max().item():.3e}")
+    assert b.abs().max().item() > 0 and torch.isfinite(a).all()
+    assert frac <= 2e-3 and diff.max().item() <= 2.0 ** -6 * b.abs().max().item()
