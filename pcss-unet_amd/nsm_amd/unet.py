@@ -766,7 +766,7 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
                                tag=name + ".conv.0.wgrad", dM=dM,
                                amax=(_slot(s.am, AM_DM), _slot(s.am, AM_V)))
         s.V = None
-    elif s.X.dtype == ops.H2:   # direct 3x3 on h2 operands (dY1 from the BN backward)
+    elif s.X is not None and s.X.dtype == ops.H2:   # direct 3x3 on h2 operands (dY1 from the BN backward)
         assert dY1.dtype == ops.H2
         ops.conv3x3_wgrad_h2(dY1, s.X, B, H, W, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad",
                              amax=(am_dy1, _slot(s.am, AM_X)))
