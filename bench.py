@@ -389,15 +389,16 @@ def vgg_roofline(B, H, W, conv_ms, gemm_ms, launches, amax):
                            "direct_equiv_tflops": round(alg / (conv_ms * 1e-3) / 1e12, 1)}}
 
 
-def direct_roofline(B, H, W, kern_ms, launches):
-    """Roofline object of conv6.conv.0 forward as one bf16 implicit GEMM
+def direct_roofline(B, H, W, kern_ms, launches, f16=False):
+    """Roofline object of conv6.conv.0 forward as one bf16 (f16) implicit GEMM
     (M = B*(H/8)*(W/8) pixels, N = 1024, K = 9*1024)."""
     M = B * (H // 8) * (W // 8)
     k_flops = conv_flops(B, H // 8, W // 8, 1024, 1024, 3)
     k_bytes = (2 * M * 1024 + 9 * 1024 * 1024) * 2
     achieved = k_flops / (kern_ms * 1e-3) / 1e12
-    return {"kernel": f"conv6.conv.0.fwd bf16 implicit-GEMM 3x3 (nsm_conv_fwd_bf16: M={M} "
-                      f"N=1024 K=9216)",
+    fn = "nsm_conv_fwd_f16" if f16 else "nsm_conv_fwd_bf16"
+    return {"kernel": f"conv6.conv.0.fwd {'f16' if f16 else 'bf16'} implicit-GEMM 3x3 ({fn}: "
+                      f"M={M} N=1024 K=9216)",
             "bound": "mfma", "achieved": round(achieved, 2), "peak": BF16_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / BF16_PEAK_TFLOPS, 4),
             "avg_launch_ms": round(kern_ms, 4), "launches": launches,
@@ -497,7 +498,7 @@ def run_train(args):
     C, H, W = args.in_ch, args.res, args.res
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(C, H, W, frames=args.batch)
-        if args.dtype == "bf16":
+        if args.dtype in ("bf16", "f16"):
             res["cpu_baseline"]["sample"] += " (fp32: the reference's CPU path)"
     if rank == 0:
         emit(res, args)
@@ -553,6 +554,11 @@ def secondary_configs(args, world, rank, dev):
     kws = [dict(workload="train", dtype="bf16", batch=64, steps=max(10, args.steps // 5),
                 warmup=3)]
     if world == 1:
+        # the reference's own GPU precision mode (fp16 autocast + GradScaler,
+        # main.py:175,257-259,281,368) at configs[2]'s batch
+        kws += [dict(workload="train", dtype="f16", batch=64, steps=max(10, args.steps // 5),
+                     warmup=3)]
+    if world == 1:
         # the reference-faithful step: CustomLoss with its VGG19 perceptual
         # term (customLoss.py:137; random-init VGG weights, value unpinned)
         kws += [dict(workload="train", dtype="f32", batch=8, steps=max(5, args.steps // 10),
@@ -582,10 +588,14 @@ def train_measure(args, world, rank, dev):
 
     torch.manual_seed(1234 + rank)
     B, C, H, W = args.batch, args.in_ch, args.res, args.res
-    bf16 = args.dtype == "bf16"
+    bf16 = args.dtype in ("bf16", "f16")   # the 16-bit storage paths
+    f16 = args.dtype == "f16"
     model = nsm_amd.Unet(in_ch=C, dropout_rate=0.2).to(dev).train()
     if bf16:
-        model.set_compute_dtype(torch.bfloat16)
+        model.set_compute_dtype(torch.float16 if f16 else torch.bfloat16)
+    # f16: GradScaler's loss scale (main.py:175,281; its initial 2^16, held
+    # fixed here), unscaled inside the tail (main.py:361-368)
+    loss_scale = 65536.0 if f16 else 1.0
     if world > 1:  # identical initial weights on every rank (DDP semantics)
         with torch.no_grad():
             for p in model.parameters():
@@ -596,7 +606,7 @@ def train_measure(args, world, rank, dev):
     # the reference's whole step tail (main.py:287-423) on the device: sanitise,
     # per-parameter clips, clip_grad_norm_(1.0) (epoch 0 of 200), AdamW
     opt = nsm_amd.FlatAdamW(model.parameters(), lr=7e-4, weight_decay=1e-3, max_grad_norm=1.0,
-                            world_size=world, sanitize=True)
+                            world_size=world, sanitize=True, grad_scale=loss_scale)
     opt.set_epoch(0, 200)
     crit = nsm_amd.CustomLoss(dev, alpha=0.9, vgg_weights="random" if args.vgg else False)
     g = torch.Generator(device=dev).manual_seed(rank)
@@ -606,7 +616,7 @@ def train_measure(args, world, rank, dev):
     def step():
         out = model(x)
         loss = crit(out, y, x)
-        loss.backward()
+        (loss * loss_scale if f16 else loss).backward()
         if world > 1:
             # the exposed part of the overlapped all-reduce: how long the compute
             # stream waits for RCCL after the backward (HIP events)
@@ -652,13 +662,14 @@ def train_measure(args, world, rank, dev):
     pipe_mult, peak = pipe_products(bf16)
     if bf16:
         from nsm_amd.prep import BF16_WINO, BF16_WINO_MIN
-        work = stage_work(C, H, W, B, bytes_per=2, wino_min=BF16_WINO_MIN if BF16_WINO else 1 << 30)
-        roof = (wino_f16_roofline(B, H, W, kern_ms, gemm_ms, len(evs)) if BF16_WINO and gemm_ms
-                else direct_roofline(B, H, W, kern_ms, len(evs)))
+        wino = BF16_WINO and not f16   # f16: direct convolutions only (its parity anchor)
+        work = stage_work(C, H, W, B, bytes_per=2, wino_min=BF16_WINO_MIN if wino else 1 << 30)
+        roof = (wino_f16_roofline(B, H, W, kern_ms, gemm_ms, len(evs)) if wino and gemm_ms
+                else direct_roofline(B, H, W, kern_ms, len(evs), f16))
         traffic, traffic_src = (load_traffic("traffic_conv6_fwd_gemm_bf16.json" if BF16_WINO
-                                             else "traffic_conv6_fwd_bf16.json") if B == 64 and full
-                                else (None, None))
-        tag = f"b{B}_bf16"
+                                             else "traffic_conv6_fwd_bf16.json")
+                                if B == 64 and full and not f16 else (None, None))
+        tag = f"b{B}_{args.dtype}"
     else:
         work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=wino_tile)
         traffic, traffic_src = (load_traffic("traffic_conv6_fwd_gemm_f32.json") if B == 8 and full
@@ -681,9 +692,13 @@ def train_measure(args, world, rank, dev):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if bf16 else "f32",
+        "dtype": args.dtype if bf16 else "f32",
         "data": "synthetic (x~N(0,1), labels integers(0,256)/255), random-init weights",
-        "config": {"workload": (f"configs[2]: batch={B}/GPU {C}x{H}x{W} bf16 (fp32 accumulate, "
+        "config": {"workload": (f"batch={B}/GPU {C}x{H}x{W} f16 (fp16-autocast mode: direct "
+                                "convolutions on f16 operands, f16 activations, fp32 accumulate, "
+                                "BN stats, params, grads; loss scale 2^16 unscaled in the tail) "
+                                "train step " if f16 else
+                                f"configs[2]: batch={B}/GPU {C}x{H}x{W} bf16 (fp32 accumulate, "
                                 "BN stats, params, grads) train step " if bf16 else
                                 f"configs[1]: batch={B}/GPU {C}x{H}x{W} fp32 train step ")
                                + "(fwd + 0.9*L1" + (" + 0.1*VGG19 perceptual (random-init weights)"
@@ -742,10 +757,11 @@ def infer_measure(args, world, rank, dev):
     torch.manual_seed(1234 + rank)
     B, C = args.batch, args.in_ch
     H, W = (1080, 1920) if args.workload == "infer1080" else (256, 256)
-    bf16 = args.dtype == "bf16"
+    bf16 = args.dtype in ("bf16", "f16")   # the 16-bit storage paths
+    f16 = args.dtype == "f16"
     model = nsm_amd.Unet(in_ch=C, dropout_rate=0.2).to(dev).eval()
     if bf16:
-        model.set_compute_dtype(torch.bfloat16)
+        model.set_compute_dtype(torch.float16 if f16 else torch.bfloat16)
     g = torch.Generator(device=dev).manual_seed(rank)
     x = torch.randn(B, C, H, W, device=dev, generator=g)
     graphed = nsm_amd.GraphedUnet(model, x)
@@ -770,8 +786,12 @@ def infer_measure(args, world, rank, dev):
     times = {st: mean_ms(nops.PROBES.pop(st + ".fwd")) for st in STAGES}
     pipe_mult, peak = pipe_products(bf16)
     if bf16:
-        work = stage_work(C, H, W, B, bytes_per=2, wino_min=1 << 30, passes=1)
-        roof = direct_roofline(B, H, W, mean_ms(evs), len(evs))
+        from nsm_amd.prep import BF16_WINO, BF16_WINO_EVAL, BF16_WINO_MIN
+        wino = BF16_WINO and BF16_WINO_EVAL and not f16   # bf16 eval: F(4x4) at >= 512 channels
+        work = stage_work(C, H, W, B, bytes_per=2, wino_min=BF16_WINO_MIN if wino else 1 << 30,
+                          passes=1)
+        roof = (wino_f16_roofline(B, H, W, mean_ms(evs), mean_ms(gevs), len(evs)) if wino and gevs
+                else direct_roofline(B, H, W, mean_ms(evs), len(evs), f16))
     else:
         work = stage_work(C, H, W, B, wino_min=WINOGRAD_MIN_CHANNELS, tile=wino_tile, passes=1)
         roof = dominant_roofline(B, H, W, mean_ms(evs), mean_ms(gevs), len(evs), wino_tile(1024, H // 8, W // 8))
@@ -789,7 +809,7 @@ def infer_measure(args, world, rank, dev):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "bf16" if bf16 else "f32",
+        "dtype": args.dtype if bf16 else "f32",
         "data": "synthetic (x~N(0,1)), random-init weights, eval-mode BN (running stats)",
         "config": {"workload": f"{cfg}: batch={B}/GPU {C}x{H}x{W} {args.dtype} eval forward, "
                                "one hipGraph replay per step",
@@ -838,8 +858,9 @@ def main():
     ap.add_argument("--workload", choices=["train", "infer1080", "infer256"], default="train")
     ap.add_argument("--no-secondary", action="store_true",
                     help="train, N=1: skip the other configs measured after the headline one")
-    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32",
-                    help="bf16: configs[2] (use --batch 64)")
+    ap.add_argument("--dtype", choices=["f32", "bf16", "f16"], default="f32",
+                    help="bf16: configs[2] (use --batch 64); f16: the reference's fp16-autocast "
+                         "mode (train only)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--vgg", action="store_true",
                     help="train: include CustomLoss's VGG19 perceptual term (customLoss.py:7-90)")

@@ -38,6 +38,7 @@ extern "C" {
  * its NHWC tensors in that type and computes in fp32 */
 #define NSM_F32 0
 #define NSM_BF16 1
+#define NSM_F16 2  /* IEEE half storage (the fp16-autocast mode) */
 
 /* An operand-maximum slot (the `amax` arguments below): NSM_AMAX_WORDS uint32,
  * zeroed before its producer runs. It holds max|x| of one fp32 GEMM operand as
@@ -71,7 +72,8 @@ int nsm_pad_vec(const float* v, int n, int n_p, float* out, void* stream);
  * cout_p] float16), amax (required) = the slot that receives max|w| (beta 1),
  * a[6] as kind 4 (the FWD job of the same weight); kind 6: Winograd U as a
  * single-plane scaled f16 tensor [alpha^2][n_p][k_p] (the bf16 path's F(4x4)
- * forward, nsm_wino_gemm_f16), a and amax as kind 4. `base` = the job's first
+ * forward, nsm_wino_gemm_f16), a and amax as kind 4; kind 7: pack IEEE half
+ * (the fp16-autocast mode's NSM_F16 convolutions), a as kind 1. `base` = the job's first
  * item in the launch (jobs in ascending base order, consecutive);
  * nsm_prep_items() = the job's extent in the launch (its item count rounded up
  * to whole 512-item blocks: add it to get the next base; total_items = the
@@ -681,7 +683,8 @@ int nsm_conv_fwd_bf16(const void* x, int ldx, int B, int H, int W, int cin_p, co
  * max|scale * dz|, the k1 term of the dY1 bound nsm_bn_bwd_finalize derives
  * (the scale source of nsm_wino_dual_bn_f16).
  * Replaces ConvolutionBackward(conv.4) + BatchNorm/LeakyReLU/Dropout2d
- * backward of conv.1-3 (autograd of Unetmodel.py:21-26). dtype NSM_F32 | NSM_BF16. */
+ * backward of conv.1-3 (autograd of Unetmodel.py:21-26). dtype NSM_F32 | NSM_BF16 |
+ * NSM_F16 (the 16-bit ones: dy2, w2d, y1, out in it). */
 int nsm_conv1x1_dgrad_bnbwd(const void* dy2, int lddy2, int B, int H, int W, int cop,
                             const void* w2d, int cip, const void* y1, int ldy1,
                             const float* scale, const float* shift, const float* mean,
@@ -698,7 +701,7 @@ int nsm_conv1x1_bnbwd_chunks(int B, int H, int W, int cip, int dtype);
  * act_shift, slope) (+ res: the decoder's additive skip, :125-137), round =
  * the storage dtype's (the value the unfused conv -> bn_act pair stores in
  * between); act_scale / act_shift from nsm_bn_finalize_eval. dtype NSM_F32 |
- * NSM_BF16 (x, wpk, y, res in it). */
+ * NSM_BF16 | NSM_F16 (x, wpk, y, res in it). */
 int nsm_conv_fwd_act(const void* x, int ldx, int B, int H, int W, int cin_p, const void* wpk,
                      const float* bias, int cout_p, int ksize, void* y, int ldy,
                      const float* act_scale, const float* act_shift, float slope, const void* res,
@@ -714,6 +717,26 @@ int nsm_conv_wgrad_bf16(const void* dy, int lddy, const void* x, int ldx, int B,
                         int cin_p, int cout_p, int ksize, const float* pro_scale,
                         const float* pro_shift, const float* pro_mask, float slope, float* ws,
                         size_t ws_floats, int cin, int cout, float* dw, void* stream);
+
+/* ---- f16 convolutions (the reference's GPU precision, fp16 autocast:
+ * main.py:257-259) ------------------------------------------------------------
+ * The bf16 entries above on IEEE-half storage (v_mfma_f32_32x32x16_f16 /
+ * 16x16x32_f16, fp32 accumulation; values rounded to nearest even, beyond
+ * 65504 to +-Inf as in the reference's fp16 tensors): the same kernels,
+ * compiled a second time with the f16 conversions (csrc/nsm_conv_s16.inc in
+ * namespace nsm_h). BN-partial rows and the weight-gradient workspace:
+ * nsm_conv_stat_rows_bf16 / nsm_conv_wgrad_bf16_ws (the tile plans are the
+ * same). */
+int nsm_pack_conv_weight_f16(const float* w, int cout, int cin, int ksize, int cout_p, int cin_p,
+                             int mode, void* out, void* stream);
+int nsm_conv_fwd_f16(const void* x, int ldx, int B, int H, int W, int cin_p, const void* wpk,
+                     const float* bias, int cout_p, int ksize, void* y, int ldy,
+                     const float* pro_scale, const float* pro_shift, const float* pro_mask,
+                     float slope, float* stats, void* stream);
+int nsm_conv_wgrad_f16(const void* dy, int lddy, const void* x, int ldx, int B, int H, int W,
+                       int cin_p, int cout_p, int ksize, const float* pro_scale,
+                       const float* pro_shift, const float* pro_mask, float slope, float* ws,
+                       size_t ws_floats, int cin, int cout, float* dw, void* stream);
 
 /* ---- VGG19 perceptual loss (customLoss.py:7-90, forward only) ------------
  * nsm_vgg_prep: out[2B*H*W][32] NHWC = (nan_to_num(clamp(v,0,1)) - mean)/denom

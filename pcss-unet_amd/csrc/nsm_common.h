@@ -216,6 +216,37 @@ __device__ __forceinline__ u32x2 pack_f16x4(f32x4 v) {
   return u32x2{pack_h2(f32x2{v.x, v.y}), pack_h2(f32x2{v.z, v.w})};
 }
 
+// ---- f16 storage (NSM_F16 tensors, the fp16-autocast mode) -----------------
+// raw IEEE half words behind a distinct element type, so the elementwise
+// templates instantiate for it beside float and bf16_t; RNE conversions
+// (values beyond 65504 become +-Inf, as in the reference's fp16 tensors)
+struct f16_t {
+  unsigned short bits;
+};
+__device__ __forceinline__ float h_lo(uint32_t w) { return (float)__builtin_bit_cast(f16x2, w).x; }
+__device__ __forceinline__ float h_hi(uint32_t w) { return (float)__builtin_bit_cast(f16x2, w).y; }
+__device__ __forceinline__ uint32_t pack_hh(float a, float b) { return pack_h2(f32x2{a, b}); }
+__device__ __forceinline__ f32x4 ld4(const f16_t* p) {
+  const u32x2 w = *(const u32x2*)p;
+  return f32x4{h_lo(w.x), h_hi(w.x), h_lo(w.y), h_hi(w.y)};
+}
+__device__ __forceinline__ void st4(f16_t* p, f32x4 v) {
+  *(u32x2*)p = u32x2{pack_hh(v.x, v.y), pack_hh(v.z, v.w)};
+}
+__device__ __forceinline__ F8 ld8(const f16_t* p) {
+  const u32x4 w = *(const u32x4*)p;
+  return F8{f32x4{h_lo(w.x), h_hi(w.x), h_lo(w.y), h_hi(w.y)},
+            f32x4{h_lo(w.z), h_hi(w.z), h_lo(w.w), h_hi(w.w)}};
+}
+__device__ __forceinline__ void st8(f16_t* p, F8 v) {
+  *(u32x4*)p = u32x4{pack_hh(v.a.x, v.a.y), pack_hh(v.a.z, v.a.w), pack_hh(v.b.x, v.b.y),
+                     pack_hh(v.b.z, v.b.w)};
+}
+__device__ __forceinline__ float ld1(const f16_t* p) { return h_lo((uint32_t)p->bits); }
+__device__ __forceinline__ void st1(f16_t* p, float v) {
+  p->bits = (unsigned short)(pack_hh(v, 0.f) & 0xFFFFu);
+}
+
 __device__ __forceinline__ void split4h(f32x4 v, float s, u32x2& h, u32x2& l) {
   const f32x2 a = f32x2{v.x, v.y} * s, b = f32x2{v.z, v.w} * s;
   h = u32x2{pack_h2(a), pack_h2(b)};

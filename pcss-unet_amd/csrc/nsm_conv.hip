@@ -2032,7 +2032,8 @@ __host__ __device__ inline long long nsm_prep_items_dev(const NsmPrepJob& j) {
   switch (j.kind) {
     case 0:
     case 1:
-    case 5: return (long long)j.a[3] * j.a[4] * j.a[2];
+    case 5:
+    case 7: return (long long)j.a[3] * j.a[4] * j.a[2];
     case 2:
     case 4:
     case 6: return (long long)j.a[2] * j.a[3];
@@ -2348,7 +2349,7 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
     const long long li = blk0 - j.base + r * 256 + threadIdx.x;
     if (li >= items) break;
     const int idx = (int)li;
-    if (j.kind <= 1) {
+    if (j.kind <= 1 || j.kind == 7) {
       const int cout = j.a[0], cin = j.a[1], taps = j.a[2], cout_p = j.a[3], cin_p = j.a[4];
       float v;
       if (j.a[5] == NSM_PACK_FWD) {
@@ -2362,8 +2363,10 @@ __global__ void __launch_bounds__(256) prep_weights_kernel(const NsmPrepJob* __r
       if (j.kind == 0) {
         ((float*)j.dst)[idx] = v;
         amax_fold(am, v);
-      } else {
+      } else if (j.kind == 1) {
         ((bf16_t*)j.dst)[idx] = (bf16_t)(pack_bf2(v, 0.f) & 0xFFFFu);
+      } else {  // 7: IEEE half
+        ((bf16_t*)j.dst)[idx] = (bf16_t)(pack_hh(v, 0.f) & 0xFFFFu);
       }
     } else if (j.kind == 2) {
       float* U = (float*)j.dst;
@@ -3082,7 +3085,31 @@ static int wgrad_wino_finish(float* slab, const WinoWgradPlan& pl, int nb, int M
   return 0;
 }
 
-namespace nsm {
+// The 16-bit conv body twice: bf16 (namespace nsm_bf) and f16 (nsm_h). Not
+// nested in nsm: argument-dependent lookup on nsm's types (F8) would otherwise
+// see nsm's bf16 helpers beside nsm_h's f16 ones.
+namespace nsm_bf {
+using namespace nsm;
+__device__ __forceinline__ f32x16 mfma_s16_32(bf16x8 a, bf16x8 b, f32x16 c, int, int, int) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma_s16_16(bf16x8 a, bf16x8 b, f32x4 c, int, int, int) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+// bits of a value already rounded to bf16 (round_bf)
+__device__ __forceinline__ bf16_t s16_bits(float v) { return (bf16_t)(__float_as_uint(v) >> 16); }
+__device__ __forceinline__ void st8s(bf16_t* p, F8 v) { nsm::st8(p, v); }
+#include "nsm_conv_s16.inc"
+}  // namespace nsm_bf
+namespace nsm_h {
+using namespace nsm;
+#include "nsm_fmt_f16.h"
+#include "nsm_conv_s16.inc"
+}  // namespace nsm_h
+
+using namespace nsm;
+using namespace nsm_bf;
+
 #include "nsm_conv_bf16.inc"
 #include "nsm_conv_h2.inc"
 #include "nsm_conv_h2d.inc"

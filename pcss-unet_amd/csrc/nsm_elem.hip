@@ -487,6 +487,13 @@ __device__ __forceinline__ F8 as_stored8(F8 v);
 template <>
 __device__ __forceinline__ F8 as_stored8<float>(F8 v) { return v; }
 template <>
+__device__ __forceinline__ F8 as_stored8<f16_t>(F8 v) {
+  const u32x4 w = u32x4{pack_hh(v.a.x, v.a.y), pack_hh(v.a.z, v.a.w), pack_hh(v.b.x, v.b.y),
+                        pack_hh(v.b.z, v.b.w)};
+  return F8{f32x4{h_lo(w.x), h_hi(w.x), h_lo(w.y), h_hi(w.y)},
+            f32x4{h_lo(w.z), h_hi(w.z), h_lo(w.w), h_hi(w.w)}};
+}
+template <>
 __device__ __forceinline__ F8 as_stored8<bf16_t>(F8 v) {
   const u32x4 w = u32x4{pack_bf2(v.a.x, v.a.y), pack_bf2(v.a.z, v.a.w), pack_bf2(v.b.x, v.b.y),
                         pack_bf2(v.b.z, v.b.w)};
@@ -1480,6 +1487,9 @@ static void dispatch_sep_bwd(const SepPlan& pl, int B, size_t lds, hipStream_t s
   (pl.R == 4 ? NSM_SEP(T, RED, 4) : pl.R == 2 ? NSM_SEP(T, RED, 2) : NSM_SEP(T, RED, 1))
   if (dtype == NSM_BF16) {
     if (rp) NSM_SEP_R(bf16_t, true); else NSM_SEP_R(bf16_t, false);
+  }
+  else if (dtype == NSM_F16) {
+    if (rp) NSM_SEP_R(f16_t, true); else NSM_SEP_R(f16_t, false);
   } else {
     if (rp) NSM_SEP_R(float, true); else NSM_SEP_R(float, false);
   }
@@ -1904,6 +1914,9 @@ extern "C" int nsm_bn_stats(const void* y, int ld, int M, int C, float* partial,
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(bn_stats_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(bf16_t, y), ld, M, C, r.cl, r.rl, r.rpc, partial);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(bn_stats_kernel<f16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(f16_t, y), ld, M, C, r.cl, r.rl, r.rpc, partial);
   else
     hipLaunchKernelGGL(bn_stats_kernel<float>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, y), ld, M, C, r.cl, r.rl, r.rpc, partial);
@@ -1996,6 +2009,10 @@ extern "C" int nsm_bn_act(const void* y, int ldy, int M, int C, const float* sca
     hipLaunchKernelGGL(bn_act_kernel<bf16_t>, g, b, 0, as_stream(stream), NSM_CT(bf16_t, y), ldy,
                        M, C / 8, fh, scale, shift, slope, mask, NSM_CT(bf16_t, res), ldres,
                        NSM_T(bf16_t, out), ldo, amax);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(bn_act_kernel<f16_t>, g, b, 0, as_stream(stream), NSM_CT(f16_t, y), ldy,
+                       M, C / 8, fh, scale, shift, slope, mask, NSM_CT(f16_t, res), ldres,
+                       NSM_T(f16_t, out), ldo, amax);
   else
     hipLaunchKernelGGL(bn_act_kernel<float>, g, b, 0, as_stream(stream), NSM_CT(float, y), ldy, M,
                        C / 8, fh, scale, shift, slope, mask, NSM_CT(float, res), ldres,
@@ -2036,6 +2053,11 @@ extern "C" int nsm_bn_bwd_reduce(const void* g, int ldg, const void* y, int ldy,
                        NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, make_fastdiv(HW),
                        scale, shift, slope, mask, mean, invstd, r.cl, r.rl, r.rpc, partial,
                        amax_k1dz);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(bn_bwd_reduce_kernel<f16_t>, gr, dim3(256), 0, as_stream(stream),
+                       NSM_CT(f16_t, g), ldg, NSM_CT(f16_t, y), ldy, M, C, make_fastdiv(HW),
+                       scale, shift, slope, mask, mean, invstd, r.cl, r.rl, r.rpc, partial,
+                       amax_k1dz);
   else
     hipLaunchKernelGGL(bn_bwd_reduce_kernel<float>, gr, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, make_fastdiv(HW), scale,
@@ -2074,6 +2096,10 @@ extern "C" int nsm_bn_bwd_apply(const void* g, int ldg, const void* y, int ldy, 
     hipLaunchKernelGGL(bn_bwd_apply_kernel<bf16_t>, gr, b, 0, as_stream(stream),
                        NSM_CT(bf16_t, g), ldg, NSM_CT(bf16_t, y), ldy, M, C, C / 8, fh, scale,
                        shift, slope, mask, mean, coef, NSM_T(bf16_t, dy), lddy, amax);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<f16_t>, gr, b, 0, as_stream(stream),
+                       NSM_CT(f16_t, g), ldg, NSM_CT(f16_t, y), ldy, M, C, C / 8, fh, scale,
+                       shift, slope, mask, mean, coef, NSM_T(f16_t, dy), lddy, amax);
   else
     hipLaunchKernelGGL(bn_bwd_apply_kernel<float>, gr, b, 0, as_stream(stream),
                        NSM_CT(float, g), ldg, NSM_CT(float, y), ldy, M, C, C / 8, fh, scale,
@@ -2115,6 +2141,10 @@ extern "C" int nsm_bn_act_pool(const void* y, int B, int H, int W, int C, const 
     hipLaunchKernelGGL(bn_act_pool_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(bf16_t, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,
                        NSM_T(bf16_t, z), NSM_T(bf16_t, pooled), amax);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(bn_act_pool_kernel<f16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(f16_t, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,
+                       NSM_T(f16_t, z), NSM_T(f16_t, pooled), amax);
   else
     hipLaunchKernelGGL(bn_act_pool_kernel<float>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, y), B, H, W, C / 8, f8, fw, fh, scale, shift, slope,
@@ -2133,6 +2163,9 @@ extern "C" int nsm_avgpool2_fwd(const void* x, int B, int H, int W, int C, void*
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(avgpool2_fwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(bf16_t, x), B, H, W, C / 8, f8, fw, fh, NSM_T(bf16_t, y));
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(avgpool2_fwd_kernel<f16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(f16_t, x), B, H, W, C / 8, f8, fw, fh, NSM_T(f16_t, y));
   else
     hipLaunchKernelGGL(avgpool2_fwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, x), B, H, W, C / 8, f8, fw, fh, NSM_T(float, y));
@@ -2154,6 +2187,10 @@ static int avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, const vo
   if (dtype == NSM_BF16) {
     if (rp) hipLaunchKernelGGL((avgpool2_bwd_add_kernel<bf16_t, true>), g, dim3(256), 0, s, A_(bf16_t));
     else hipLaunchKernelGGL((avgpool2_bwd_add_kernel<bf16_t, false>), g, dim3(256), 0, s, A_(bf16_t));
+  }
+  else if (dtype == NSM_F16) {
+    if (rp) hipLaunchKernelGGL((avgpool2_bwd_add_kernel<f16_t, true>), g, dim3(256), 0, s, A_(f16_t));
+    else hipLaunchKernelGGL((avgpool2_bwd_add_kernel<f16_t, false>), g, dim3(256), 0, s, A_(f16_t));
   } else {
     if (rp) hipLaunchKernelGGL((avgpool2_bwd_add_kernel<float, true>), g, dim3(256), 0, s, A_(float));
     else hipLaunchKernelGGL((avgpool2_bwd_add_kernel<float, false>), g, dim3(256), 0, s, A_(float));
@@ -2182,6 +2219,8 @@ static bool rows_resize() {
   do {                                                                          \
     if (dtype == NSM_BF16)                                                      \
       hipLaunchKernelGGL(KER<bf16_t>, g, dim3(256), 0, s, __VA_ARGS__(bf16_t)); \
+    else if (dtype == NSM_F16)                                                  \
+      hipLaunchKernelGGL(KER<f16_t>, g, dim3(256), 0, s, __VA_ARGS__(f16_t));   \
     else                                                                        \
       hipLaunchKernelGGL(KER<float>, g, dim3(256), 0, s, __VA_ARGS__(float));   \
   } while (0)
@@ -2224,7 +2263,7 @@ static int resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, in
     const size_t slds = pl.lcb8 < 0 ? 0
                                     : (size_t)pl.R * Wo * (8 << pl.lcb8) * 4 +
                                           (size_t)Wi * (RS_W + 2) * 4;
-    if (sep_resize() && dtype != NSM_BF16 && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * Hi < (1ll << 31)) {
+    if (sep_resize() && dtype == NSM_F32 && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * Hi < (1ll << 31)) {
       dispatch_sep_bwd<false>(pl, B, slds, s, dy, Hi, Wi, C, dx, Ho, Wo, sh, sw, 0.f, 0.f, rp,
                               dtype);
     } else if (Wi <= U2_MAXW && (long long)B * Hi < (1ll << 31) && rows_resize()) {
@@ -2235,6 +2274,10 @@ static int resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, in
       if (dtype == NSM_BF16) {
         if (rp) hipLaunchKernelGGL((resize_bwd_rows_kernel<bf16_t, true>), gr, dim3(256), lds, s, A_(bf16_t));
         else hipLaunchKernelGGL((resize_bwd_rows_kernel<bf16_t, false>), gr, dim3(256), lds, s, A_(bf16_t));
+      }
+      else if (dtype == NSM_F16) {
+        if (rp) hipLaunchKernelGGL((resize_bwd_rows_kernel<f16_t, true>), gr, dim3(256), lds, s, A_(f16_t));
+        else hipLaunchKernelGGL((resize_bwd_rows_kernel<f16_t, false>), gr, dim3(256), lds, s, A_(f16_t));
       } else {
         if (rp) hipLaunchKernelGGL((resize_bwd_rows_kernel<float, true>), gr, dim3(256), lds, s, A_(float));
         else hipLaunchKernelGGL((resize_bwd_rows_kernel<float, false>), gr, dim3(256), lds, s, A_(float));
@@ -2279,6 +2322,10 @@ extern "C" int nsm_resize_fwd_act(const void* y2, int B, int Hi, int Wi, int C, 
     hipLaunchKernelGGL((resize_fwd8_kernel<bf16_t, true>), g, dim3(256), 0, s,
                        NSM_CT(bf16_t, y2), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh,
                        NSM_T(bf16_t, out), Ho, Wo, sh, sw, act);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL((resize_fwd8_kernel<f16_t, true>), g, dim3(256), 0, s,
+                       NSM_CT(f16_t, y2), Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh,
+                       NSM_T(f16_t, out), Ho, Wo, sh, sw, act);
   else
     hipLaunchKernelGGL((resize_fwd8_kernel<float, true>), g, dim3(256), 0, s, NSM_CT(float, y2),
                        Hi, Wi, C / 8, (uint32_t)tot8, f8, fw, fh, NSM_T(float, out), Ho, Wo, sh,
@@ -2308,11 +2355,15 @@ extern "C" int nsm_up2_resize_fwd_act(const void* y2, int B, int h, int w, int C
   const ActSrc act{scale, shift, res, slope};
   const int lcb8 = sep_lcb8(C, w);
   const size_t slds = lcb8 < 0 ? 0 : (size_t)w * (8 << lcb8) * 4 + (size_t)tw * 16;
-  if (sep_resize() && dtype != NSM_BF16 && lcb8 >= 0 && slds <= 65536) {
+  if (sep_resize() && dtype == NSM_F32 && lcb8 >= 0 && slds <= 65536) {
     const dim3 gs((unsigned)rows, (unsigned)(C / (8 << lcb8)));
     if (dtype == NSM_BF16)
       hipLaunchKernelGGL((up2_resize_fwd_sep_kernel<bf16_t, true>), gs, dim3(256), slds, s,
                          NSM_CT(bf16_t, y2), h, w, C, lcb8, NSM_T(bf16_t, out), th, tw, a, b, c,
+                         d, act);
+    else if (dtype == NSM_F16)
+      hipLaunchKernelGGL((up2_resize_fwd_sep_kernel<f16_t, true>), gs, dim3(256), slds, s,
+                         NSM_CT(f16_t, y2), h, w, C, lcb8, NSM_T(f16_t, out), th, tw, a, b, c,
                          d, act);
     else
       hipLaunchKernelGGL((up2_resize_fwd_sep_kernel<float, true>), gs, dim3(256), slds, s,
@@ -2321,6 +2372,10 @@ extern "C" int nsm_up2_resize_fwd_act(const void* y2, int B, int h, int w, int C
   } else if (dtype == NSM_BF16)
     hipLaunchKernelGGL((up2_resize_fwd_rows_kernel<bf16_t, true>), gr, dim3(256), lds, s,
                        NSM_CT(bf16_t, y2), h, w, C / 8, f8, NSM_T(bf16_t, out), th, tw, a, b, c,
+                       d, act);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL((up2_resize_fwd_rows_kernel<f16_t, true>), gr, dim3(256), lds, s,
+                       NSM_CT(f16_t, y2), h, w, C / 8, f8, NSM_T(f16_t, out), th, tw, a, b, c,
                        d, act);
   else
     hipLaunchKernelGGL((up2_resize_fwd_rows_kernel<float, true>), gr, dim3(256), lds, s,
@@ -2351,11 +2406,13 @@ extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, voi
     const dim3 gr((unsigned)rows, (unsigned)segs);
     const int lcb8 = sep_lcb8(C, w);
     const size_t slds = lcb8 < 0 ? 0 : (size_t)w * (8 << lcb8) * 4 + (size_t)tw * 16;
-    if (sep_resize() && dtype != NSM_BF16 && lcb8 >= 0 && slds <= 65536) {
+    if (sep_resize() && dtype == NSM_F32 && lcb8 >= 0 && slds <= 65536) {
       const dim3 gs((unsigned)rows, (unsigned)(C / (8 << lcb8)));
 #define A_(T) NSM_CT(T, x), h, w, C, lcb8, NSM_T(T, y), th, tw, a, b, c, d
       if (dtype == NSM_BF16)
         hipLaunchKernelGGL(up2_resize_fwd_sep_kernel<bf16_t>, gs, dim3(256), slds, s, A_(bf16_t));
+      else if (dtype == NSM_F16)
+        hipLaunchKernelGGL(up2_resize_fwd_sep_kernel<f16_t>, gs, dim3(256), slds, s, A_(f16_t));
       else
         hipLaunchKernelGGL(up2_resize_fwd_sep_kernel<float>, gs, dim3(256), slds, s, A_(float));
 #undef A_
@@ -2363,6 +2420,8 @@ extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, voi
 #define A_(T) NSM_CT(T, x), h, w, C / 8, f8, NSM_T(T, y), th, tw, a, b, c, d
     if (dtype == NSM_BF16)
       hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<bf16_t>, gr, dim3(256), lds, s, A_(bf16_t));
+    else if (dtype == NSM_F16)
+      hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<f16_t>, gr, dim3(256), lds, s, A_(f16_t));
     else
       hipLaunchKernelGGL(up2_resize_fwd_rows_kernel<float>, gr, dim3(256), lds, s, A_(float));
 #undef A_
@@ -2392,7 +2451,7 @@ static int up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, 
   const size_t slds = pl.lcb8 < 0 ? 0
                                   : (size_t)pl.R * tw * (8 << pl.lcb8) * 4 +
                                         (size_t)w * (RS_W + 2) * 4;
-  if (sep_resize() && dtype != NSM_BF16 && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * h < (1ll << 31)) {
+  if (sep_resize() && dtype == NSM_F32 && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * h < (1ll << 31)) {
     dispatch_sep_bwd<true>(pl, B, slds, s, dy, h, w, C, dx, th, tw, a, b, c, d, rp, dtype);
   } else if (w <= U2_MAXW && (long long)B * h < (1ll << 31)) {
     NSM_CHECK_ARG(!rp || 256 % (C / 8) == 0, "up2_resize_bwd: fused BN reduction needs C/8 | 256");
@@ -2402,6 +2461,10 @@ static int up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, 
     if (dtype == NSM_BF16) {
       if (rp) hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<bf16_t, true>), gr, dim3(256), lds, s, A_(bf16_t));
       else hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<bf16_t, false>), gr, dim3(256), lds, s, A_(bf16_t));
+    }
+    else if (dtype == NSM_F16) {
+      if (rp) hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<f16_t, true>), gr, dim3(256), lds, s, A_(f16_t));
+      else hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<f16_t, false>), gr, dim3(256), lds, s, A_(f16_t));
     } else {
       if (rp) hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<float, true>), gr, dim3(256), lds, s, A_(float));
       else hipLaunchKernelGGL((up2_resize_bwd_rows_kernel<float, false>), gr, dim3(256), lds, s, A_(float));
@@ -2478,6 +2541,9 @@ extern "C" int nsm_input_prep(const float* x, int B, int C, int H, int W, void* 
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(input_prep_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
                        NSM_T(bf16_t, out), cp, (uint32_t)npix, fw, fh, nullptr);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(input_prep_kernel<f16_t>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
+                       NSM_T(f16_t, out), cp, (uint32_t)npix, fw, fh, nullptr);
   else
     hipLaunchKernelGGL(input_prep_kernel<float>, g, dim3(256), 0, as_stream(stream), x, B, C, H, W,
                        NSM_T(float, out), cp, (uint32_t)npix, fw, fh, amax);
@@ -2511,6 +2577,9 @@ extern "C" int nsm_input_grad(const void* dX, int B, int C, int H, int W, int cp
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(input_grad_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(bf16_t, dX), B, C, H, W, cp, dx);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(input_grad_kernel<f16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(f16_t, dX), B, C, H, W, cp, dx);
   else
     hipLaunchKernelGGL(input_grad_kernel<float>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, dX), B, C, H, W, cp, dx);
@@ -2526,6 +2595,9 @@ extern "C" int nsm_head_fwd(const void* z, int ldz, int B, int Rh, int Rw, const
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(bf16_t, z), ldz, B, Rh, Rw, w10, b10, out);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(head_fwd_kernel<f16_t>, g, dim3(256), 0, as_stream(stream),
+                       NSM_CT(f16_t, z), ldz, B, Rh, Rw, w10, b10, out);
   else
     hipLaunchKernelGGL(head_fwd_kernel<float>, g, dim3(256), 0, as_stream(stream),
                        NSM_CT(float, z), ldz, B, Rh, Rw, w10, b10, out);
@@ -2547,6 +2619,9 @@ extern "C" int nsm_head_bwd(const float* gout, const float* out, const void* z, 
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(nblk), dim3(256), 0, s, gout, out,
                        NSM_CT(bf16_t, z), ldz, B, Rh, Rw, w10, NSM_T(bf16_t, dz), partial);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(head_bwd_kernel<f16_t>, dim3(nblk), dim3(256), 0, s, gout, out,
+                       NSM_CT(f16_t, z), ldz, B, Rh, Rw, w10, NSM_T(f16_t, dz), partial);
   else
     hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(nblk), dim3(256), 0, s, gout, out,
                        NSM_CT(float, z), ldz, B, Rh, Rw, w10, NSM_T(float, dz), partial);

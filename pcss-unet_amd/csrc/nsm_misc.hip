@@ -146,6 +146,9 @@ extern "C" int nsm_nchw_to_nhwc(const float* x, int B, int C, int H, int W, void
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, grid, dim3(256), 0, s, x, C, HW, cp,
                        (bf16_t*)y, ldy);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<f16_t>, grid, dim3(256), 0, s, x, C, HW, cp,
+                       (f16_t*)y, ldy);
   else
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, grid, dim3(256), 0, s, x, C, HW, cp, (float*)y,
                        ldy);
@@ -161,6 +164,9 @@ extern "C" int nsm_nhwc_to_nchw(const void* z, int ldz, int B, int C, int H, int
   hipStream_t s = as_stream(stream);
   if (dtype == NSM_BF16)
     hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16_t>, grid, dim3(256), 0, s, (const bf16_t*)z, ldz,
+                       C, HW, x);
+  else if (dtype == NSM_F16)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<f16_t>, grid, dim3(256), 0, s, (const f16_t*)z, ldz,
                        C, HW, x);
   else
     hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, grid, dim3(256), 0, s, (const float*)z, ldz, C,

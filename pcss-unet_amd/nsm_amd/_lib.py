@@ -140,6 +140,10 @@ _SIGS = {
     "nsm_conv_wgrad_bf16_ws": (Z, [I, I, I, I, I, I]),
     "nsm_conv_stat_rows_bf16": (I, [I, I, I, I]),
     "nsm_conv_wgrad_bf16": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
+    # the fp16-autocast mode: the same entries on IEEE-half storage
+    "nsm_pack_conv_weight_f16": (I, [P, I, I, I, I, I, I, P, P]),
+    "nsm_conv_fwd_f16": (I, [P, I, I, I, I, I, P, P, I, I, P, I, P, P, P, F, P, P]),
+    "nsm_conv_wgrad_f16": (I, [P, I, P, I, I, I, I, I, I, I, P, P, P, F, P, Z, I, I, P, P]),
     "nsm_maxpool2_fwd": (I, [P, I, I, I, I, P, P]),
     "nsm_tail_chunk": (L, []),
     "nsm_tail_plan": (I, [P, I, P, P, P, P, I]),

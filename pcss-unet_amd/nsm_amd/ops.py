@@ -12,16 +12,25 @@ from ._lib import call, ptr, stream
 
 F32 = torch.float32
 BF16 = torch.bfloat16
+# storage of NSM_F16 activations (the fp16-autocast mode): IEEE half bits held
+# in int16 tensors, so that they are never taken for the h2 operands
+# (torch.float16, H2 below) the fp32 path's producers write
+F16S = torch.int16
 PACK_FWD, PACK_DGRAD = 0, 1
-NSM_F32, NSM_BF16 = 0, 1
+NSM_F32, NSM_BF16, NSM_F16 = 0, 1, 2
+S16 = (BF16, F16S)   # the 16-bit storage dtypes (csrc/nsm_conv_s16.inc, compiled for both)
 
 
 def dt(t):
-    """C-ABI dtype code of an activation tensor (include/nsm.h NSM_F32/NSM_BF16)."""
+    """C-ABI dtype code of an activation tensor (include/nsm.h NSM_F32 /
+    NSM_BF16 / NSM_F16)."""
     if t.dtype == BF16:
         return NSM_BF16
+    if t.dtype == F16S:
+        return NSM_F16
     if t.dtype != F32:
-        raise TypeError(f"activations must be float32 or bfloat16, got {t.dtype}")
+        raise TypeError(f"activations must be float32, bfloat16 or f16 storage (int16), "
+                        f"got {t.dtype}")
     return NSM_F32
 
 
@@ -61,7 +70,8 @@ def pack_conv_weight(w, cout_p, cin_p, mode, dtype=F32):
     cout, cin, k, _ = w.shape
     taps = k * k
     out = torch.empty(cout_p * taps * cin_p, dtype=dtype, device=w.device)
-    fn = "nsm_pack_conv_weight_bf16" if dtype == BF16 else "nsm_pack_conv_weight"
+    fn = {BF16: "nsm_pack_conv_weight_bf16", F16S: "nsm_pack_conv_weight_f16"}.get(
+        dtype, "nsm_pack_conv_weight")
     call(fn, ptr(w), cout, cin, k, cout_p, cin_p, mode, ptr(out), stream())
     return out
 
@@ -202,7 +212,7 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
         sc, sh, mk = pro
     part = None
     if stats:
-        rows_fn = lib.nsm_conv_stat_rows_bf16 if x.dtype == BF16 else lib.nsm_conv_stat_rows
+        rows_fn = lib.nsm_conv_stat_rows_bf16 if x.dtype in S16 else lib.nsm_conv_stat_rows
         rpc = rows_fn(B, H, W, cout_p)
         nchunk = -(-M // rpc)
         part = Partials(empty(nchunk * 2 * cout_p, device=x.device), nchunk, rpc)
@@ -212,6 +222,8 @@ def conv_fwd_bn(x, B, H, W, wpk, bias, cout_p, ksize, pro=None, out=None, tag=No
             ptr(part.buf) if part is not None else None)
     if x.dtype == BF16:
         call("nsm_conv_fwd_bf16", *args, stream())
+    elif x.dtype == F16S:
+        call("nsm_conv_fwd_f16", *args, stream())
     else:
         call("nsm_conv_fwd_stats", *args, *_pair(amax), stream())
     if ev is not None:
@@ -576,7 +588,7 @@ def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None, amax=(N
     amax = (max|dy|, max|x|) slots: the fp32 GEMM runs the f16x2 split."""
     from ._lib import lib
     cout_p, cin_p = dy.shape[1], x.shape[1]
-    bf = dy.dtype == BF16
+    bf = dy.dtype in S16
     if x.dtype != dy.dtype:
         raise TypeError("conv_wgrad: dy and x must share a dtype")
     n = int((lib.nsm_conv_wgrad_bf16_ws if bf else lib.nsm_conv_wgrad_ws)(B, H, W, cin_p, cout_p,
@@ -589,7 +601,7 @@ def conv_wgrad(dy, x, B, H, W, ksize, cin, cout, dw, pro=None, tag=None, amax=(N
     args = (ptr(dy), dy.stride(0), ptr(x), x.stride(0), B, H, W, cin_p, cout_p, ksize, ptr(sc),
             ptr(sh), ptr(mk), 0.2, ptr(ws), n, cin, cout, ptr(dw))
     if bf:
-        call("nsm_conv_wgrad_bf16", *args, stream())
+        call("nsm_conv_wgrad_bf16" if dy.dtype == BF16 else "nsm_conv_wgrad_f16", *args, stream())
     else:
         call("nsm_conv_wgrad", *args, *_pair(amax), stream())
     if ev is not None:
@@ -863,7 +875,7 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     ev = _probe(tag)
     am = _pair(amax) if dtc == NSM_F32 else (None, None)
     k1dz, bslot = bound if bound is not None else (None, None)
-    assert bound is None or (dtc == NSM_BF16 and not recompute)
+    assert bound is None or (dtc != NSM_F32 and not recompute)
     call("nsm_conv1x1_dgrad_bnbwd", *args, 0 if recompute else 1, ptr(partial), None, ptr(dA1),
          dA1.stride(0) if dA1 is not None else 0, dtc, *am, ptr(k1dz), stream())
     if nchunk > SUM_ROWS_ABOVE:

@@ -27,6 +27,7 @@ class NsmPrepJob(ctypes.Structure):
 
 KIND_PACK_F32, KIND_PACK_BF16, KIND_WINO, KIND_PAD, KIND_WINO_H2, KIND_PACK_H2 = 0, 1, 2, 3, 4, 5
 KIND_WINO_F16 = 6
+KIND_PACK_F16 = 7   # IEEE half pack (the fp16-autocast mode's direct convolutions)
 # NSM_H2=0: the fp32 training step keeps fp32 Winograd operands (the GEMMs
 # split them in-kernel, nsm_conv_split16.inc) instead of the pre-split h2
 # tensors their producers write (nsm_conv_h2.inc)
@@ -205,7 +206,7 @@ class StepWeights:
                                ("be2", bn2.bias, cop)):
                 pb.t[name] = (t.detach() if t.numel() == n else
                               add(KIND_PAD, (t.numel(), n), t, n, torch.float32))
-            pk = KIND_PACK_BF16 if dtype == torch.bfloat16 else KIND_PACK_F32
+            pk = {torch.bfloat16: KIND_PACK_BF16, ops.F16S: KIND_PACK_F16}.get(dtype, KIND_PACK_F32)
             modes = (ops.PACK_FWD, ops.PACK_DGRAD) if training else (ops.PACK_FWD,)
             if cip >= wino_min and dtype == torch.float32:
                 tile = wino_tile(cip, h, w)

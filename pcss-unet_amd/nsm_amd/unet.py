@@ -136,14 +136,14 @@ def bnb_mode(cip, cop, dtype, h2=False):
     892 us, conv2 462 -> 533 us fused), while conv6/7/8 gain 77-170 us each."""
     if BNB_MODE == 0:
         return 0
-    if dtype == torch.bfloat16 and (cop % 64 or cip < 128):
+    if dtype in ops.S16 and (cop % 64 or cip < 128):
         return 0 if BNB_MODE == 2 else 1
     if BNB_MODE == 1:
         return 1
     # fp32-product rate of the pass: bf16 ~0.6 PF; fp32 register-path f16x2
     # split ~0.12 PF; fp32 on h2 operands (nsm_conv_h2d.inc) ~1 PF of f16 MFMA
     # work = ~0.3 PF of fp32 products
-    s, rate = (2, 6e14) if dtype == torch.bfloat16 else (4, 3e14 if h2 else 1.2e14)
+    s, rate = (2, 6e14) if dtype in ops.S16 else (4, 3e14 if h2 else 1.2e14)
     return 2 if (2 * cip - cop) * s / 5e12 > 2 * cip * cop / rate else 1
 ENCODER = (2, 3, 4, 5)
 DECODER = (6, 7, 8, 9)
@@ -160,13 +160,23 @@ def _warn_once(key, msg):
         warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
 
-def _check_autocast():
-    """main.py:257 runs the GPU step under fp16 autocast; this path has fp32 and
-    bf16 kernels only (bf16 under bf16 autocast), so fp16 requests run fp32."""
-    if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.float16:
-        _warn_once("fp16", "nsm_amd: fp16 autocast requested (main.py:257); the MI355X path "
-                   "computes in fp32 here (use torch.autocast('cuda', dtype=torch.bfloat16) or "
-                   "Unet.set_compute_dtype(torch.bfloat16) for the bf16 kernels)")
+def _storage_dtype(dtype):
+    """Activation storage of a compute dtype: fp32, bf16, or ops.F16S (IEEE
+    half bits in int16) for torch.float16."""
+    return ops.F16S if dtype == torch.float16 else dtype
+
+
+def _autocast_dtype():
+    """The storage dtype a torch.autocast('cuda') region asks for: bf16 under
+    bf16 autocast; f16 under fp16 autocast (the reference's own GPU mode,
+    main.py:257-259: direct convolutions on f16 operands, f16 activations and
+    activation gradients, fp32 accumulation / BN statistics / parameters /
+    weight gradients); fp32 outside autocast."""
+    if torch.is_autocast_enabled("cuda"):
+        adt = torch.get_autocast_dtype("cuda")
+        if adt in (torch.bfloat16, torch.float16):
+            return _storage_dtype(adt)
+    return torch.float32
 
 
 def _nhwc(x, cp, dtype):
@@ -207,8 +217,7 @@ class _DoubleConvFn(torch.autograd.Function):
         if C != ci:
             raise ValueError(f"DoubleConv expects {ci} channels, got {C}")
         training = blk.training
-        dtype = (torch.bfloat16 if torch.is_autocast_enabled("cuda")
-                 and torch.get_autocast_dtype("cuda") == torch.bfloat16 else torch.float32)
+        dtype = _autocast_dtype()
         X = _nhwc(x, ops.pad32(ci), dtype)
         p = blk.conv[3].p
         mask = _dropout_mask(p, B, ci, x.device) if training and p > 0 else None
@@ -217,7 +226,9 @@ class _DoubleConvFn(torch.autograd.Function):
         ctx.blk, ctx.s, ctx.shape, ctx.training = blk, s, (B, C, H, W), training
         ctx.params = params
         out = _nchw(z, B, co, H, W)
-        return out.to(dtype) if dtype != torch.float32 else out
+        if dtype == torch.float32:
+            return out
+        return out.to(torch.float16 if dtype == ops.F16S else dtype)
 
     @staticmethod
     def backward(ctx, gout):
@@ -253,7 +264,6 @@ class DoubleConv(nn.Module):
 
     def forward(self, x):
         require_gpu(x, "DoubleConv input")
-        _check_autocast()
         return _DoubleConvFn.apply(x, self, *tuple(self.parameters()))
 
 
@@ -286,25 +296,27 @@ class Unet(nn.Module):
         # data parallel: (group, src) when forward broadcasts rank 0's BN buffers
         self._bn_broadcast = None
         self._bn_flat_cache = None
-        # activation storage / MFMA dtype: None = fp32, or bf16 inside a
-        # torch.autocast(dtype=torch.bfloat16) region; set_compute_dtype() pins it
+        # activation storage / MFMA dtype: None = fp32, or bf16 / f16 inside a
+        # torch.autocast(dtype=torch.bfloat16 / float16) region; set_compute_dtype() pins it
         self.compute_dtype = None
 
     def set_compute_dtype(self, dtype):
-        """torch.float32 (exact fp32 MFMA, Winograd for the deep convs) or
+        """torch.float32 (exact fp32 MFMA, Winograd for the deep convs),
         torch.bfloat16 (BASELINE config 3: bf16 activations and MFMA products,
-        fp32 accumulation / BN statistics / parameters / gradients)."""
-        if dtype not in (None, torch.float32, torch.bfloat16):
+        fp32 accumulation / BN statistics / parameters / gradients) or
+        torch.float16 (the reference's fp16-autocast mode, main.py:257-259:
+        direct convolutions on f16 operands, f16 activations and activation
+        gradients, the same fp32 accumulation and state)."""
+        if dtype not in (None, torch.float32, torch.bfloat16, torch.float16):
             raise ValueError(f"unsupported compute dtype {dtype}")
         self.compute_dtype = dtype
         return self
 
     def activation_dtype(self):
+        """Storage dtype of the activations: fp32, bf16 or ops.F16S."""
         if self.compute_dtype is not None:
-            return self.compute_dtype
-        if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
-            return torch.bfloat16
-        return torch.float32
+            return _storage_dtype(self.compute_dtype)
+        return _autocast_dtype()
 
     def overlap_grad_allreduce(self, group=None, enable=True):
         """Data-parallel overlap: the backward starts the RCCL
@@ -377,7 +389,6 @@ class Unet(nn.Module):
         params = tuple(self.parameters())
         for p in params[:1]:
             require_gpu(p, "Unet parameters")
-        _check_autocast()
         if "hooks" not in _WARNED and any(m._backward_hooks or m._backward_pre_hooks
                                           for m in self.modules() if m is not self):
             # main.py:207-222 registers a logging hook on every leaf module
@@ -621,7 +632,7 @@ def _block_fwd(blk, X, B, H, W, training, mask, name="", pw=None, src=None, fuse
         Y2, part2 = ops.conv1x1_h2(A1, w2, b2, cop, stats=True,
                                    amax=(_slot(am, AM_A1), pw.amax_w2(ops.PACK_FWD)),
                                    tag=name + ".conv.4.fwd")
-    elif BF16_MATERIALIZE_ACT if dtype == torch.bfloat16 else F32_MATERIALIZE_ACT:
+    elif BF16_MATERIALIZE_ACT if dtype in ops.S16 else F32_MATERIALIZE_ACT:
         # the same fp32 arithmetic and bf16 rounding as the fused operand prologue
         A1 = ops.bn_act(Y1, bn1, SLOPE, mask=mask, HW=H * W, amax=_slot(am, AM_A1))
         Y2, part2 = ops.conv_fwd_bn(A1, B, H, W, w2, b2, cop, 1, tag=name + ".conv.4.fwd",

@@ -10,7 +10,6 @@
     weights directly;
   * main.py:257's fp16 autocast region: this path has fp32 and bf16 kernels,
     so it warns and runs fp32 (bitwise the fp32 result)."""
-import warnings
 
 import pytest
 import torch
@@ -83,21 +82,3 @@ def test_vgg_from_torchvision_checkpoint(device, tmp_path):
     assert abs(loss - (0.9 * l1 + 0.1 * want)) <= 1e-6 * abs(loss)
     ref = V.vgg_loss(sd, o.cpu(), t.cpu()).item()   # the oracle on the same weights
     assert abs(got - ref) <= 2e-5 * abs(ref)
-
-
-def test_fp16_autocast_warns_and_runs_fp32(device):
-    import nsm_amd
-    from nsm_amd import unet as U
-    torch.manual_seed(0)
-    m = nsm_amd.Unet(in_ch=4, dropout_rate=0.0).to(device).eval()
-    x = torch.randn(1, 4, 64, 64, device=device)
-    with torch.no_grad():
-        ref = m(x)
-    U._WARNED.discard("fp16")
-    with warnings.catch_warnings(record=True) as w:
-        warnings.simplefilter("always")
-        with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
-            out = m(x)
-    assert any("fp16 autocast" in str(x.message) for x in w), [str(x.message) for x in w]
-    assert out.dtype == torch.float32
-    assert torch.equal(out, ref)
