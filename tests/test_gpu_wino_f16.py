@@ -31,7 +31,11 @@ def _prep_u(ops, w, cin_p, cout_p, device):
 
 
 @pytest.mark.parametrize("m16", [False, True])
+# (2, 32, 32, 512, 1024): the shape of the r04 fault record (call_r4_27, a
+# pre-commit library; tests/test_gpu_guard.py audits it with guard regions);
+# (3, 21, 27, 512, 1024): ragged tiles with co > ci
 @pytest.mark.parametrize("B,H,W,ci,co", [(2, 32, 32, 512, 512), (1, 37, 29, 512, 1024),
+                                        (2, 32, 32, 512, 1024), (3, 21, 27, 512, 1024),
                                         (4, 16, 16, 1024, 512), (64, 8, 8, 512, 1024)])
 def test_conv3x3_wino_f16_vs_direct_bf16(device, B, H, W, ci, co, m16):
     from nsm_amd import ops
