@@ -632,6 +632,19 @@ def train_measure(args, world, rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # one process: the whole step (forward, loss, backward, the device tail)
+    # replayed from one HIP graph (nsm_amd.GraphedTrainStep: dropout masks from
+    # the graph-safe generator, new every replay); the kernel / stage timings
+    # below come from eager steps of the same shapes (HIP events cannot be read
+    # from inside a replayed graph). NSM_GRAPH_STEP=0: eager timed steps.
+    graphed = None
+    if world == 1 and os.environ.get("NSM_GRAPH_STEP", "1") != "0":
+        graphed = nsm_amd.GraphedTrainStep(model, crit, opt, x, y, loss_scale=loss_scale,
+                                           warmup=1)
+        for _ in range(args.warmup):
+            graphed()
+        torch.cuda.synchronize()
+        elapsed = timed(graphed, args.steps, world, dev)
 
     probe_tag = "conv6.conv.0.fwd"
     nops.PROBES[probe_tag] = []
@@ -645,7 +658,12 @@ def train_measure(args, world, rank, dev):
     dp_tags = ("dp.bn_broadcast", "dp.allreduce_wait")
     for t in dp_tags:
         nops.PROBES[t] = []
-    elapsed = timed(step, args.steps, world, dev)
+    if graphed is None:
+        elapsed = timed(step, args.steps, world, dev)
+    else:   # eager probe steps (not timed)
+        for _ in range(min(args.steps, 10)):
+            step()
+        torch.cuda.synchronize()
     dp_ms = {t: mean_ms(nops.PROBES.pop(t)) for t in dp_tags}
     evs = nops.PROBES.pop(probe_tag)
     kern_ms = mean_ms(evs)
@@ -713,6 +731,9 @@ def train_measure(args, world, rank, dev):
         "stages": stage_table(work, times, pipe_mult, peak, measured),
         "stage_pmc_source": measured_src,
         "roofline": roof,
+        "step_execution": ("one hipGraph replay per step (nsm_amd.GraphedTrainStep); kernel and "
+                           "stage times from eager steps of the same shapes" if graphed is not None
+                           else "eager"),
     }
     if world > 1:
         res["dp"] = {"bn_broadcast_ms": round(dp_ms["dp.bn_broadcast"], 4),

@@ -650,6 +650,11 @@ int nsm_range_flag(const float* o, int64_t n, float lo, float hi, int* flag, voi
  * c < c_j and 0 for c_j <= c < cp_j, u ~ U[0,1) from a counter-based hash of
  * (seed, j, b, c). desc (device) = njobs x {off, c, cp, keep as float bits}. */
 int nsm_dropout_masks(const int* desc, int njobs, int B, uint64_t seed, float* out, void* stream);
+/* The same with the seed read from device memory (seed[0]): a HIP graph that
+ * captures it draws new masks on every replay when the word is rewritten by a
+ * captured producer (nsm_amd: torch's graph-safe generator). */
+int nsm_dropout_masks_dev(const int* desc, int njobs, int B, const int64_t* seed, float* out,
+                          void* stream);
 /* Profiling marker: an empty kernel of (code + 1) workgroups of 64 lanes.
  * With NSM_STAGE_MARKS=1 the host brackets each encoder/decoder stage
  * (Unetmodel.py:104-148) with markers (code = stage id, 0 = stage end), so a

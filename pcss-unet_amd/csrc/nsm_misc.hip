@@ -79,11 +79,16 @@ __device__ __forceinline__ uint32_t hash32(uint64_t x) {
   return (uint32_t)x;
 }
 
+// seed_dev (nsm_dropout_masks_dev): the seed read from device memory, so a
+// captured graph draws new masks on every replay (torch's graph-safe generator
+// writes it there)
 __global__ void __launch_bounds__(256) dropout_masks_kernel(const int* __restrict__ desc, int njobs,
                                                             int B, uint64_t seed,
-                                                            float* __restrict__ out) {
+                                                            float* __restrict__ out,
+                                                            const int64_t* __restrict__ seed_dev) {
   const int j = blockIdx.y;
   if (j >= njobs) return;
+  if (seed_dev) seed = (uint64_t)seed_dev[0];
   const int off = desc[4 * j], creal = desc[4 * j + 1], cp = desc[4 * j + 2];
   const float keep = __int_as_float(desc[4 * j + 3]);
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < B * cp; i += gridDim.x * blockDim.x) {
@@ -131,8 +136,17 @@ extern "C" int nsm_dropout_masks(const int* desc, int njobs, int B, uint64_t see
                                  void* stream) {
   NSM_CHECK_ARG(desc && out && njobs > 0 && B > 0, "dropout_masks: bad args");
   hipLaunchKernelGGL(dropout_masks_kernel, dim3(8, njobs), dim3(256), 0, as_stream(stream), desc,
-                     njobs, B, seed, out);
+                     njobs, B, seed, out, nullptr);
   NSM_LAUNCH_CHECK("dropout_masks");
+  return 0;
+}
+
+extern "C" int nsm_dropout_masks_dev(const int* desc, int njobs, int B, const int64_t* seed,
+                                     float* out, void* stream) {
+  NSM_CHECK_ARG(desc && out && seed && njobs > 0 && B > 0, "dropout_masks_dev: bad args");
+  hipLaunchKernelGGL(dropout_masks_kernel, dim3(8, njobs), dim3(256), 0, as_stream(stream), desc,
+                     njobs, B, 0ull, out, seed);
+  NSM_LAUNCH_CHECK("dropout_masks_dev");
   return 0;
 }
 

@@ -10,6 +10,7 @@ from .losses import (CustomLoss, EnhancedCustomLoss, L1Loss, PerturbationLoss,  
                      l1_loss, measure_temporal_instability)
 from .optim import FlatAdamW, allreduce_grads, flat_grad  # noqa: F401
 from .infer import GraphedUnet  # noqa: F401
+from .step import GraphedTrainStep  # noqa: F401
 from .vgg import MultiLayerVGGLoss  # noqa: F401
 
 __version__ = "0.1.0"

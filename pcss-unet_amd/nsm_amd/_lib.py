@@ -154,6 +154,7 @@ _SIGS = {
     "nsm_nhwc_to_nchw": (I, [P, I, I, I, I, I, P, I, P]),
     "nsm_range_flag": (I, [P, L, F, F, P, P]),
     "nsm_dropout_masks": (I, [P, I, I, U64, P, P]),
+    "nsm_dropout_masks_dev": (I, [P, I, I, P, P, P]),
     "nsm_stage_mark": (I, [I, P]),
     "nsm_prep_items": (L, [P]),
     "nsm_prep_weights": (I, [P, I, L, I, P, P, L, P, L, P]),

@@ -79,18 +79,28 @@ class _RangeCheck:
                                  "customLoss.py:131")
 
     def launch(self, o):
-        if self.event is not None and self.event.query():
-            self._raise_if_set()
         if self.flag is None or self.flag.device != o.device:
             self.flag = torch.zeros(1, dtype=torch.int32, device=o.device)
             self.host = torch.zeros(1, dtype=torch.int32).pin_memory()
             self.event = torch.cuda.Event()
+        if torch.cuda.is_current_stream_capturing():
+            # a captured step (GraphedTrainStep): the sticky device flag only —
+            # no event, no copy; check() reads the flag itself
+            call("nsm_range_flag", ptr(o), o.numel(), 0.0, 1.0, ptr(self.flag), stream())
+            self.captured = True
+            return
+        if self.event.query():
+            self._raise_if_set()
         call("nsm_range_flag", ptr(o), o.numel(), 0.0, 1.0, ptr(self.flag), stream())
         self.host.copy_(self.flag, non_blocking=True)
         self.event.record()
 
     def check(self):
-        if self.event is not None:
+        if getattr(self, "captured", False):
+            torch.cuda.current_stream().synchronize()
+            self.host.copy_(self.flag)
+            self._raise_if_set()
+        elif self.event is not None:
             self.event.synchronize()
             self._raise_if_set()
 

@@ -1,0 +1,105 @@
+"""One whole training step replayed from a HIP graph.
+
+The reference's step (main.py:255-423: forward under autocast, the loss,
+`scaler.scale(loss).backward()`, the NaN/Inf census and repair, the
+per-parameter clips, clip_grad_norm_, AdamW) is ~200 kernel launches on this
+path; `GraphedTrainStep` captures forward + loss + backward + the FlatAdamW
+device tail once and replays them as one graph, so the launches no longer pay
+the host's per-launch cost nor the gaps between dispatches.
+
+What the graph holds fixed, and how the step stays the reference's:
+  * inputs: `step.x` / `step.y` are static buffers — copy each batch into them
+    (`step(x, y)` does it);
+  * Dropout2d masks: drawn from torch's graph-safe CUDA generator inside the
+    graph (unet._masks_for -> nsm_dropout_masks_dev), new masks every replay;
+  * the CustomLoss range assert: its sticky device flag only
+    (`loss_fn.check_range_now()` reads it);
+  * hyper-parameters passed as kernel arguments (lr, betas, eps, weight decay,
+    max_norm, the loss scale): the step re-captures when one of them changes
+    (an epoch's LambdaLR / max_norm schedule costs one capture);
+  * parameter / buffer addresses: FlatAdamW's flat storage keeps them; a
+    re-allocation raises.
+The constructor runs `warmup` eager steps on (x, y) to settle the caches,
+then restores parameters, AdamW moments, the tail's counters and the BN
+buffers, so building the step changes no training state. Single process only
+(the data-parallel all-reduce stays eager)."""
+import torch
+
+from ._lib import require_gpu
+
+
+class GraphedTrainStep:
+    def __init__(self, model, loss_fn, optimizer, x, y, loss_scale=1.0, warmup=3):
+        require_gpu(x, "GraphedTrainStep input")
+        if model._grad_allreduce is not None or model._bn_broadcast is not None:
+            raise ValueError("GraphedTrainStep: single process only (the data-parallel "
+                             "all-reduce and BN broadcast run eagerly)")
+        self.model, self.loss_fn, self.opt = model, loss_fn, optimizer
+        self.loss_scale = float(loss_scale)
+        self.x = x.detach().clone().requires_grad_(x.requires_grad)
+        self.y = y.detach().clone()
+        self.warmup = warmup
+        self.graph = None
+        self._capture()
+
+    def _hyper(self):
+        g = self.opt.param_groups[0]
+        return (float(g["lr"]), tuple(g["betas"]), float(g["eps"]), float(g["weight_decay"]),
+                self.opt.max_grad_norm, self.opt.grad_scale, self.loss_scale)
+
+    def _addresses(self):
+        return [t.data_ptr() for t in list(self.model.parameters()) + list(self.model.buffers())]
+
+    def _body(self):
+        out = self.model(self.x)
+        loss = self.loss_fn(out, self.y, self.x)
+        (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
+        self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
+        self.x.grad = None
+        return loss.detach()
+
+    def _state(self):
+        """Everything a step writes besides its scratch: parameters and AdamW
+        moments (FlatAdamW's flat buffers), the tail's device counters and
+        flags, the BN running statistics and counts."""
+        o = self.opt
+        ts = [o.flat, o.exp_avg, o.exp_avg_sq, o._step_dev, o.flags, o.stat]
+        return ts + [b for b in self.model.buffers()]
+
+    def _capture(self, warmup=None):
+        warmup = self.warmup if warmup is None else warmup
+        side = torch.cuda.Stream(device=self.x.device)
+        side.wait_stream(torch.cuda.current_stream())
+        saved = [t.detach().clone() for t in self._state()]
+        with torch.cuda.stream(side):
+            for _ in range(warmup):   # allocator, weight-layout and mask-descriptor caches
+                self._body()
+        torch.cuda.current_stream().wait_stream(side)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):   # recorded, not run
+            self.loss = self._body()
+        # the warm-up steps leave no trace: the model and optimizer are as
+        # they were before the constructor
+        with torch.no_grad():
+            for t, v in zip(self._state(), saved):
+                t.copy_(v)
+        self._hyp = self._hyper()
+        self._ptrs = self._addresses()
+
+    def __call__(self, x=None, y=None):
+        """One step: copy the batch in (if given), replay; returns the loss
+        tensor (device, unscaled). The first call after a hyper-parameter
+        change re-captures first (no eager steps: the caches are warm)."""
+        if x is not None:
+            self.x.detach().copy_(x)
+        if y is not None:
+            self.y.copy_(y)
+        if self._addresses() != self._ptrs:
+            raise RuntimeError("GraphedTrainStep: parameters or buffers were re-allocated after "
+                               "capture — build a new step")
+        if self._hyper() != self._hyp:
+            self.graph = None
+            self._capture(warmup=0)   # the caches are warm
+        self.graph.replay()
+        return self.loss

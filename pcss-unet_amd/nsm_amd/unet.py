@@ -446,8 +446,15 @@ def _masks_for(mod, B, device, training):
         dev_desc = cache.get(key)
         if dev_desc is None:
             dev_desc = cache[key] = torch.tensor(desc, dtype=torch.int32).to(device)
-        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        call("nsm_dropout_masks", ptr(dev_desc), len(jobs), B, seed, ptr(flat), stream())
+        if torch.cuda.is_current_stream_capturing():
+            # a captured step (GraphedTrainStep): the seed drawn on the device by
+            # torch's graph-safe generator, so every replay draws new masks
+            seed_t = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64, device=device)
+            call("nsm_dropout_masks_dev", ptr(dev_desc), len(jobs), B, ptr(seed_t), ptr(flat),
+                 stream())
+        else:
+            seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+            call("nsm_dropout_masks", ptr(dev_desc), len(jobs), B, seed, ptr(flat), stream())
         off = 0
         for k, ci, cp, keep in jobs:
             masks[k] = flat[off:off + B * cp].view(B, cp)
