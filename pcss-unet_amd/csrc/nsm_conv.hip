@@ -1239,6 +1239,9 @@ __device__ __forceinline__ float vfma(float c, float x, float a) { return __buil
 __device__ __forceinline__ f32x4 vfma(float c, f32x4 x, f32x4 a) {
   return __builtin_elementwise_fma(f32x4{c, c, c, c}, x, a);
 }
+__device__ __forceinline__ f32x2 vfma(float c, f32x2 x, f32x2 a) {
+  return __builtin_elementwise_fma(f32x2{c, c}, x, a);
+}
 
 template <class C, int NO, int NI, typename T>
 __device__ __forceinline__ void wmat(const T (&x)[NI], T (&y)[NO]) {
@@ -3389,22 +3392,57 @@ typedef _Float16 f16x4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ f32x4 bf4_to_f32(u32x2 w) {
   return f32x4{bf_lo(w.x), bf_hi(w.x), bf_lo(w.y), bf_hi(w.y)};
 }
+// Channels per thread of the bf16 path's F(4x4) transforms (BfLane<CW>): the
+// 6x6 tile's column-pass accumulators are 36 lane vectors, 144 VGPRs at 4
+// channels (1-2 waves / SIMD, the x2-upsample form spilling to AGPRs) and 72
+// at 2 (3-4 waves / SIMD). Same per-channel arithmetic either way.
+template <int CW> struct BfLane;
+template <> struct BfLane<4> {
+  using V = f32x4;
+  using W = u32x2;  // 4 bf16
+  __device__ static W raw(const bf16_t* p) { return *(const W*)p; }
+  __device__ static V cvt(W w) { return bf4_to_f32(w); }
+  __device__ static V ld(const bf16_t* p) { return cvt(raw(p)); }
+  __device__ static V rbf(V v) { return V{round_bf(v.x), round_bf(v.y), round_bf(v.z), round_bf(v.w)}; }
+  __device__ static void st16(bf16_t* p, V v) {  // IEEE half
+    *(u32x2*)p = __builtin_bit_cast(u32x2, __builtin_convertvector(v, f16x4v));
+  }
+};
+template <> struct BfLane<2> {
+  using V = f32x2;
+  using W = uint32_t;  // 2 bf16
+  __device__ static W raw(const bf16_t* p) { return *(const W*)p; }
+  __device__ static V cvt(W w) { return V{bf_lo(w), bf_hi(w)}; }
+  __device__ static V ld(const bf16_t* p) { return cvt(raw(p)); }
+  __device__ static V rbf(V v) { return V{round_bf(v.x), round_bf(v.y)}; }
+  __device__ static void st16(bf16_t* p, V v) { *(uint32_t*)p = pack_h2(v); }
+};
+// NSM_F16_TX_CW: 2 (default) or 4 channels per thread in those transforms
+static int f16_tx_cw() {
+  static int v = [] {
+    const char* e = getenv("NSM_F16_TX_CW");
+    return e && atoi(e) == 4 ? 4 : 2;
+  }();
+  return v;
+}
 
 // V [alpha^2][T][C] f16 = s B^T d B of the bf16 NHWC input x (zero padding), 4
 // channels per thread, the column pass streamed over the patch rows
-template <int MT>
+template <int MT, int CW>
 __global__ void __launch_bounds__(256) wino_input_f16_kernel(const bf16_t* __restrict__ x, int ld,
                                                              int H, int W, int C, int TH, int TW,
                                                              long long T, bf16_t* __restrict__ V,
                                                              H2Scale hsc) {
   constexpr int A = MT + 2;
-  const int C4 = C / 4;
+  using L = BfLane<CW>;
+  using LV = typename L::V;
+  const int C4 = C / CW;
   const long long total = T * C4;
   const float hs = exp2i(h2_exp(hsc));  // every lane (amax_read: a wave reduction)
   const size_t plane = (size_t)T * C;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
+    const int c = (int)(i % C4) * CW;
     const long long t = i / C4;
     const int tx = (int)(t % TW);
     const long long r = t / TW;
@@ -3412,33 +3450,32 @@ __global__ void __launch_bounds__(256) wino_input_f16_kernel(const bf16_t* __res
     const long long b = r / TH;
     // the whole patch's loads go out first: unconditional (an element outside
     // the image reads the image's first pixel, then counts as 0)
-    u32x2 raw[A][A];
+    typename L::W raw[A][A];
 #pragma unroll
     for (int a = 0; a < A; ++a)
 #pragma unroll
       for (int e = 0; e < A; ++e) {
         const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
         const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-        raw[a][e] = *(const u32x2*)(x + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
-        if (!in) raw[a][e] = u32x2{0u, 0u};
+        raw[a][e] = L::raw(x + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
+        if (!in) raw[a][e] = typename L::W{};
       }
-    f32x4 sc[A][A];
+    LV sc[A][A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      f32x4 d[A];
+      LV d[A];
 #pragma unroll
-      for (int e = 0; e < A; ++e) d[e] = bf4_to_f32(raw[a][e]);
+      for (int e = 0; e < A; ++e) d[e] = L::cvt(raw[a][e]);
       wcol_row<CBt<MT>>(sc, d, a);
     }
     bf16_t* out = V + (size_t)t * C + c;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      f32x4 v[A];
+      LV v[A];
       wmat<CBt<MT>>(sc[a], v);
 #pragma unroll
       for (int e = 0; e < A; ++e)
-        *(u32x2*)(out + (a * A + e) * plane) =
-            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * hs, f16x4v));
+        L::st16(out + (a * A + e) * plane, v[e] * hs);
     }
   }
 }
@@ -3450,18 +3487,20 @@ __global__ void __launch_bounds__(256) wino_input_f16_kernel(const bf16_t* __res
 // transformed; the upsampled tensor is never written or re-read. Source rows
 // are x-interpolated once and kept while consecutive patch rows reuse them
 // (a tile's 6 patch rows of a x2 upsample touch ~4 source rows).
-template <int MT>
+template <int MT, int CW>
 __global__ void __launch_bounds__(256) wino_input_f16_up_kernel(
     const bf16_t* __restrict__ x, int ld, int hi, int wi, float sh, float sw, int H, int W, int C,
     int TH, int TW, long long T, bf16_t* __restrict__ V, H2Scale hsc) {
   constexpr int A = MT + 2;
-  const int C4 = C / 4;
+  using L = BfLane<CW>;
+  using LV = typename L::V;
+  const int C4 = C / CW;
   const long long total = T * C4;
   const float hs = exp2i(h2_exp(hsc));  // every lane (amax_read: a wave reduction)
   const size_t plane = (size_t)T * C;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
+    const int c = (int)(i % C4) * CW;
     const long long t = i / C4;
     const int tx = (int)(t % TW);
     const long long r = t / TW;
@@ -3472,9 +3511,9 @@ __global__ void __launch_bounds__(256) wino_input_f16_up_kernel(
 #pragma unroll
     for (int e = 0; e < A; ++e)
       lin_idx(sw, min(max(MT * tx - 1 + e, 0), W - 1), wi, x0[e], x1[e], lx0[e], lx1[e]);
-    f32x4 h0[A], h1[A];
+    LV h0[A], h1[A];
     int ya = -1, yb = -1;  // source rows held in h0, h1
-    f32x4 sc[A][A];
+    LV sc[A][A];
 #pragma unroll
     for (int a = 0; a < A; ++a) {
       const int yy = MT * ty - 1 + a;
@@ -3489,7 +3528,7 @@ __global__ void __launch_bounds__(256) wino_input_f16_up_kernel(
           const bf16_t* r0 = x + ((size_t)b * hi + y0) * wi * ld + c;
 #pragma unroll
           for (int e = 0; e < A; ++e)
-            h0[e] = lx0[e] * ld4(r0 + (size_t)x0[e] * ld) + lx1[e] * ld4(r0 + (size_t)x1[e] * ld);
+            h0[e] = lx0[e] * L::ld(r0 + (size_t)x0[e] * ld) + lx1[e] * L::ld(r0 + (size_t)x1[e] * ld);
         }
         ya = y0;
       }
@@ -3501,30 +3540,28 @@ __global__ void __launch_bounds__(256) wino_input_f16_up_kernel(
           const bf16_t* r1 = x + ((size_t)b * hi + y1) * wi * ld + c;
 #pragma unroll
           for (int e = 0; e < A; ++e)
-            h1[e] = lx0[e] * ld4(r1 + (size_t)x0[e] * ld) + lx1[e] * ld4(r1 + (size_t)x1[e] * ld);
+            h1[e] = lx0[e] * L::ld(r1 + (size_t)x0[e] * ld) + lx1[e] * L::ld(r1 + (size_t)x1[e] * ld);
         }
         yb = y1;
       }
       const bool rin = (unsigned)yy < (unsigned)H;
-      f32x4 d[A];
+      LV d[A];
 #pragma unroll
       for (int e = 0; e < A; ++e) {
         const bool in = rin && (unsigned)(MT * tx - 1 + e) < (unsigned)W;
-        const f32x4 v = ly0 * h0[e] + ly1 * h1[e];
-        d[e] = in ? f32x4{round_bf(v.x), round_bf(v.y), round_bf(v.z), round_bf(v.w)}
-                  : f32x4{0.f, 0.f, 0.f, 0.f};
+        const LV v = ly0 * h0[e] + ly1 * h1[e];
+        d[e] = in ? L::rbf(v) : LV{};
       }
       wcol_row<CBt<MT>>(sc, d, a);
     }
     bf16_t* out = V + (size_t)t * C + c;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      f32x4 v[A];
+      LV v[A];
       wmat<CBt<MT>>(sc[a], v);
 #pragma unroll
       for (int e = 0; e < A; ++e)
-        *(u32x2*)(out + (a * A + e) * plane) =
-            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * hs, f16x4v));
+        L::st16(out + (a * A + e) * plane, v[e] * hs);
     }
   }
 }
@@ -3538,9 +3575,11 @@ extern "C" int nsm_wino_input_f16_resize(const void* x, int ldx, int B, int hi, 
   NSM_CHECK_ARG(((uintptr_t)x % 8) == 0 && ((uintptr_t)V % 16) == 0, "wino_input_f16_resize: alignment");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input_f16_resize: bad shape");
-  hipLaunchKernelGGL(wino_input_f16_up_kernel<4>, dim3(grid_1d(g.T * cin_p / 4)), dim3(256), 0,
-                     as_stream(stream), (const bf16_t*)x, ldx, hi, wi, ac_scale(hi, H), ac_scale(wi, W),
-                     H, W, cin_p, g.TH, g.TW, g.T, (bf16_t*)V, H2Scale{amax_x, wino_beta(4, 0)});
+  const int cw = f16_tx_cw();
+  hipLaunchKernelGGL((cw == 2 ? wino_input_f16_up_kernel<4, 2> : wino_input_f16_up_kernel<4, 4>),
+                     dim3(grid_1d(g.T * cin_p / cw)), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)x, ldx, hi, wi, ac_scale(hi, H), ac_scale(wi, W), H, W, cin_p,
+                     g.TH, g.TW, g.T, (bf16_t*)V, H2Scale{amax_x, wino_beta(4, 0)});
   NSM_LAUNCH_CHECK("wino_input_f16_resize");
   return 0;
 }
@@ -3552,9 +3591,11 @@ extern "C" int nsm_wino_input_f16(const void* x, int ldx, int B, int H, int W, i
   NSM_CHECK_ARG(((uintptr_t)x % 8) == 0 && ((uintptr_t)V % 16) == 0, "wino_input_f16: alignment");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input_f16: bad shape");
-  hipLaunchKernelGGL(wino_input_f16_kernel<4>, dim3(grid_1d(g.T * cin_p / 4)), dim3(256), 0,
-                     as_stream(stream), (const bf16_t*)x, ldx, H, W, cin_p, g.TH, g.TW, g.T,
-                     (bf16_t*)V, H2Scale{amax_x, wino_beta(4, 0)});
+  const int cw = f16_tx_cw();
+  hipLaunchKernelGGL((cw == 2 ? wino_input_f16_kernel<4, 2> : wino_input_f16_kernel<4, 4>),
+                     dim3(grid_1d(g.T * cin_p / cw)), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)x, ldx, H, W, cin_p, g.TH, g.TW, g.T, (bf16_t*)V,
+                     H2Scale{amax_x, wino_beta(4, 0)});
   NSM_LAUNCH_CHECK("wino_input_f16");
   return 0;
 }
@@ -3676,51 +3717,52 @@ extern "C" int nsm_wino_output_bf16(const float* Mb, int B, int H, int W, int co
 // dM [alpha^2][T][C] f16 = s (A dY A^T) of the bf16 output gradient (the
 // weight gradient's transform of dY, as wino_dout_kernel), 4 channels per
 // thread, the interior's loads first, the column pass streamed
-template <int MT>
+template <int MT, int CW>
 __global__ void __launch_bounds__(256) wino_dout_f16_kernel(const bf16_t* __restrict__ dy, int ld,
                                                             int H, int W, int C, int TH, int TW,
                                                             long long T, bf16_t* __restrict__ dM,
                                                             H2Scale hsc) {
   constexpr int A = MT + 2;
-  const int C4 = C / 4;
+  using L = BfLane<CW>;
+  using LV = typename L::V;
+  const int C4 = C / CW;
   const long long total = T * C4;
   const float hs = exp2i(h2_exp(hsc));  // every lane (amax_read: a wave reduction)
   const size_t plane = (size_t)T * C;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
+    const int c = (int)(i % C4) * CW;
     const long long t = i / C4;
     const int tx = (int)(t % TW);
     const long long r = t / TW;
     const int ty = (int)(r % TH);
     const long long b = r / TH;
-    u32x2 raw[MT][MT];
+    typename L::W raw[MT][MT];
 #pragma unroll
     for (int a = 0; a < MT; ++a)
 #pragma unroll
       for (int e = 0; e < MT; ++e) {
         const int yy = MT * ty + a, xx = MT * tx + e;
         const bool in = yy < H && xx < W;
-        raw[a][e] = *(const u32x2*)(dy + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
-        if (!in) raw[a][e] = u32x2{0u, 0u};
+        raw[a][e] = L::raw(dy + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
+        if (!in) raw[a][e] = typename L::W{};
       }
-    f32x4 sc[A][MT];
+    LV sc[A][MT];
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
-      f32x4 d[MT];
+      LV d[MT];
 #pragma unroll
-      for (int e = 0; e < MT; ++e) d[e] = bf4_to_f32(raw[a][e]);
+      for (int e = 0; e < MT; ++e) d[e] = L::cvt(raw[a][e]);
       wcol_row<CA<MT>>(sc, d, a);
     }
     bf16_t* out = dM + (size_t)t * C + c;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      f32x4 v[A];
+      LV v[A];
       wmat<CA<MT>>(sc[a], v);
 #pragma unroll
       for (int e = 0; e < A; ++e)
-        *(u32x2*)(out + (a * A + e) * plane) =
-            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * hs, f16x4v));
+        L::st16(out + (a * A + e) * plane, v[e] * hs);
     }
   }
 }
@@ -3732,9 +3774,11 @@ extern "C" int nsm_wino_dout_f16(const void* dy, int lddy, int B, int H, int W, 
   NSM_CHECK_ARG(((uintptr_t)dy % 8) == 0 && ((uintptr_t)dM % 16) == 0, "wino_dout_f16: alignment");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_dout_f16: bad shape");
-  hipLaunchKernelGGL(wino_dout_f16_kernel<4>, dim3(grid_1d(g.T * c_p / 4)), dim3(256), 0,
-                     as_stream(stream), (const bf16_t*)dy, lddy, H, W, c_p, g.TH, g.TW, g.T,
-                     (bf16_t*)dM, H2Scale{amax_dy, wino_beta(4, 1)});
+  const int cw = f16_tx_cw();
+  hipLaunchKernelGGL((cw == 2 ? wino_dout_f16_kernel<4, 2> : wino_dout_f16_kernel<4, 4>),
+                     dim3(grid_1d(g.T * c_p / cw)), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)dy, lddy, H, W, c_p, g.TH, g.TW, g.T, (bf16_t*)dM,
+                     H2Scale{amax_dy, wino_beta(4, 1)});
   NSM_LAUNCH_CHECK("wino_dout_f16");
   return 0;
 }
@@ -3744,73 +3788,73 @@ extern "C" int nsm_wino_dout_f16(const void* dy, int lddy, int B, int H, int W, 
 // d B of the 6x6 patch (the input gradient's operand, zero padding) and dM =
 // s_d A dY A^T of its 4x4 interior (the weight gradient's), both scales from
 // max|dY| (betas 0 and 1). wino_input_f16 + wino_dout_f16 read dY twice.
-template <int MT>
+template <int MT, int CW>
 __global__ void __launch_bounds__(256) wino_dual_f16_kernel(const bf16_t* __restrict__ dy, int ld,
                                                             int H, int W, int C, int TH, int TW,
                                                             long long T, bf16_t* __restrict__ V,
                                                             bf16_t* __restrict__ dM, H2Scale hv,
                                                             H2Scale hd) {
   constexpr int A = MT + 2;
-  const int C4 = C / 4;
+  using L = BfLane<CW>;
+  using LV = typename L::V;
+  const int C4 = C / CW;
   const long long total = T * C4;
   // every lane (amax_read: a wave reduction)
   const float sv = exp2i(h2_exp(hv)), sd = exp2i(h2_exp(hd));
   const size_t plane = (size_t)T * C;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
+    const int c = (int)(i % C4) * CW;
     const long long t = i / C4;
     const int tx = (int)(t % TW);
     const long long r = t / TW;
     const int ty = (int)(r % TH);
     const long long b = r / TH;
-    u32x2 raw[A][A];
+    typename L::W raw[A][A];
 #pragma unroll
     for (int a = 0; a < A; ++a)
 #pragma unroll
       for (int e = 0; e < A; ++e) {
         const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
         const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-        raw[a][e] = *(const u32x2*)(dy + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
-        if (!in) raw[a][e] = u32x2{0u, 0u};
+        raw[a][e] = L::raw(dy + ((size_t)b * H * W + (in ? (size_t)yy * W + xx : 0)) * ld + c);
+        if (!in) raw[a][e] = typename L::W{};
       }
     {
-      f32x4 sc[A][A];
+      LV sc[A][A];
 #pragma unroll
       for (int a = 0; a < A; ++a) {
-        f32x4 d[A];
+        LV d[A];
 #pragma unroll
-        for (int e = 0; e < A; ++e) d[e] = bf4_to_f32(raw[a][e]);
+        for (int e = 0; e < A; ++e) d[e] = L::cvt(raw[a][e]);
         wcol_row<CBt<MT>>(sc, d, a);
       }
       bf16_t* out = V + (size_t)t * C + c;
 #pragma unroll
       for (int a = 0; a < A; ++a) {
-        f32x4 v[A];
+        LV v[A];
         wmat<CBt<MT>>(sc[a], v);
 #pragma unroll
         for (int e = 0; e < A; ++e)
-          *(u32x2*)(out + (a * A + e) * plane) =
-              __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * sv, f16x4v));
+          L::st16(out + (a * A + e) * plane, v[e] * sv);
       }
     }
-    f32x4 sc[A][MT];
+    LV sc[A][MT];
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
-      f32x4 d[MT];
+      LV d[MT];
 #pragma unroll
-      for (int e = 0; e < MT; ++e) d[e] = bf4_to_f32(raw[a + 1][e + 1]);
+      for (int e = 0; e < MT; ++e) d[e] = L::cvt(raw[a + 1][e + 1]);
       wcol_row<CA<MT>>(sc, d, a);
     }
     bf16_t* out = dM + (size_t)t * C + c;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      f32x4 v[A];
+      LV v[A];
       wmat<CA<MT>>(sc[a], v);
 #pragma unroll
       for (int e = 0; e < A; ++e)
-        *(u32x2*)(out + (a * A + e) * plane) =
-            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * sd, f16x4v));
+        L::st16(out + (a * A + e) * plane, v[e] * sd);
     }
   }
 }
@@ -3824,10 +3868,11 @@ extern "C" int nsm_wino_dual_f16(const void* dy, int lddy, int B, int H, int W, 
                 "wino_dual_f16: alignment");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_dual_f16: bad shape");
-  hipLaunchKernelGGL(wino_dual_f16_kernel<4>, dim3(grid_1d(g.T * c_p / 4)), dim3(256), 0,
-                     as_stream(stream), (const bf16_t*)dy, lddy, H, W, c_p, g.TH, g.TW, g.T,
-                     (bf16_t*)V, (bf16_t*)dM, H2Scale{amax_dy, wino_beta(4, 0)},
-                     H2Scale{amax_dy, wino_beta(4, 1)});
+  const int cw = f16_tx_cw();
+  hipLaunchKernelGGL((cw == 2 ? wino_dual_f16_kernel<4, 2> : wino_dual_f16_kernel<4, 4>),
+                     dim3(grid_1d(g.T * c_p / cw)), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)dy, lddy, H, W, c_p, g.TH, g.TW, g.T, (bf16_t*)V, (bf16_t*)dM,
+                     H2Scale{amax_dy, wino_beta(4, 0)}, H2Scale{amax_dy, wino_beta(4, 1)});
   NSM_LAUNCH_CHECK("wino_dual_f16");
   return 0;
 }
