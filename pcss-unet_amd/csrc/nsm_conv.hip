@@ -1222,6 +1222,7 @@ __device__ __forceinline__ float vlrelu(float v, float s) { return lrelu(v, s); 
 __device__ __forceinline__ f32x4 vlrelu(f32x4 v, float s) {
   return f32x4{lrelu(v.x, s), lrelu(v.y, s), lrelu(v.z, s), lrelu(v.w, s)};
 }
+__device__ __forceinline__ f32x2 vlrelu(f32x2 v, float s) { return f32x2{lrelu(v.x, s), lrelu(v.y, s)}; }
 __device__ __forceinline__ float vrelu(float v) { return fmaxf(v, 0.f); }
 __device__ __forceinline__ f32x4 vrelu(f32x4 v) {
   return f32x4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
@@ -1540,7 +1541,9 @@ struct WinoM16 {
 // live): F(6x6) 138 -> 128 VGPRs, 3 -> 4 waves per SIMD
 // BFO (the bf16 path, nsm_wino_output_bf16): y holds bf16; the BN partials are
 // of the bf16-rounded outputs, as the direct bf16 convolution's epilogue
-template <int MT, bool STATS, bool ACT = false, bool BFO = false, bool M16 = false>
+// CWX: channels per thread (0: WinoVec<MT>::W; 2: the bf16 path's f16-M form
+// at half the accumulator registers, BfLane's reason)
+template <int MT, bool STATS, bool ACT = false, bool BFO = false, bool M16 = false, int CWX = 0>
 __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
                                                           int W, int TH, int TW, long long T,
                                                           const float* __restrict__ bias,
@@ -1548,9 +1551,10 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
                                                           float* __restrict__ partial,
                                                           WinoAct act = WinoAct{},
                                                           WinoM16 m16 = WinoM16{}) {
-  constexpr int A = MT + 2, CW = WinoVec<MT>::W;
-  using VT = typename WinoVec<MT>::T;
-  static_assert(!M16 || (BFO && CW == 4), "f16 M: the bf16 path's F(4x4)");
+  constexpr int A = MT + 2, CW = CWX ? CWX : WinoVec<MT>::W;
+  using VT = std::conditional_t<CW == 2, f32x2, typename WinoVec<MT>::T>;
+  static_assert(CWX == 0 || (BFO && M16 && (CW == 2 || CW == 4)), "CWX: the f16-M bf16 form");
+  static_assert(!M16 || (BFO && (CW == 4 || CW == 2)), "f16 M: the bf16 path's F(4x4)");
   int ev = 0, eu = 0;  // every lane reads the scale slots (wave reduction) before the loop
   if constexpr (M16) {
     ev = h2_exp(m16.sv);
@@ -1578,12 +1582,17 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
 #pragma unroll
       for (int e = 0; e < A; ++e) {
         if constexpr (M16) {
-          const u32x2 h = *(const u32x2*)(in16 + (a * A + e) * plane);
-          const f32x2 lo = unpack_h2(h.x), hi = unpack_h2(h.y);
           const int et = m16.e[((size_t)(a * A + e) * m16.rows + t / 64) * (N / 64) + c / 64];
           int x = -et - ev;
           x = x < -126 ? -126 : (x > 126 ? 126 : x);
-          row[e] = VT{lo.x, lo.y, hi.x, hi.y} * (exp2i(x) * exp2i(-eu));
+          if constexpr (CW == 2) {
+            const f32x2 lo = unpack_h2(*(const uint32_t*)(in16 + (a * A + e) * plane));
+            row[e] = VT{lo.x, lo.y} * (exp2i(x) * exp2i(-eu));
+          } else {
+            const u32x2 h = *(const u32x2*)(in16 + (a * A + e) * plane);
+            const f32x2 lo = unpack_h2(h.x), hi = unpack_h2(h.y);
+            row[e] = VT{lo.x, lo.y, hi.x, hi.y} * (exp2i(x) * exp2i(-eu));
+          }
         } else {
           row[e] = *(const VT*)(in + (a * A + e) * plane);
         }
@@ -1610,13 +1619,18 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
         if (MT * tx + e < W) {
           o[a][e] = o[a][e] + bv;
           if constexpr (BFO) {
-            static_assert(std::is_same<VT, f32x4>::value, "bf16 output: F(4x4) / F(2x2)");
+            static_assert(CW == 4 || CW == 2, "bf16 output: F(4x4) / F(2x2)");
             // ACT (the bf16 eval path): lrelu(BN(y)) from the running statistics,
             // rounded once to bf16 (the skip add is on the block output, not here)
             VT q = o[a][e];
             if constexpr (ACT) q = vlrelu(q * asc + ash, act.slope);
-            o[a][e] = VT{round_bf(q.x), round_bf(q.y), round_bf(q.z), round_bf(q.w)};
-            st4((bf16_t*)y + ro + (size_t)e * ldy, o[a][e]);
+            if constexpr (CW == 2) {
+              o[a][e] = VT{round_bf(q.x), round_bf(q.y)};
+              *(uint32_t*)((bf16_t*)y + ro + (size_t)e * ldy) = pack_bf2(o[a][e].x, o[a][e].y);
+            } else {
+              o[a][e] = VT{round_bf(q.x), round_bf(q.y), round_bf(q.z), round_bf(q.w)};
+              st4((bf16_t*)y + ro + (size_t)e * ldy, o[a][e]);
+            }
             if (STATS) ts = ts + o[a][e];
             continue;
           }
@@ -3644,23 +3658,30 @@ extern "C" int nsm_wino_output_bf16m(const void* M16, const int* m16e, int B, in
                 "wino_output_bf16m: bad args (tile 4 only)");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_bf16m: bad shape");
-  dim3 grid(grid_1d(g.T * (cout_p / 4)));
+  // (the partial slots: nslot x N channels whatever the width; the grid's
+  // threads, nslot x N / cw, each keep one channel group)
+  const int cw = f16_tx_cw();
+  dim3 grid(grid_1d(g.T * (cout_p / cw)));
   if (partial) {
     NSM_CHECK_ARG(nslot > 0 && nslot % wino_stat_step(cout_p, tile) == 0 && nslot <= (1 << 20),
                   "wino_output_bf16m: nslot %d not a multiple of %d", nslot,
                   wino_stat_step(cout_p, tile));
-    grid = dim3((unsigned)((long long)nslot * (cout_p / 4) / 256));
+    grid = dim3((unsigned)((long long)nslot * (cout_p / cw) / 256));
   }
   const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, m16e, (int)((g.T + 63) / 64)};
   hipStream_t s = as_stream(stream);
-  if (partial)
-    hipLaunchKernelGGL((wino_output_kernel<4, true, false, true, true>), grid, dim3(256), 0, s,
-                       (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, partial,
-                       WinoAct{}, m16);
-  else
-    hipLaunchKernelGGL((wino_output_kernel<4, false, false, true, true>), grid, dim3(256), 0, s,
-                       (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, nullptr,
-                       WinoAct{}, m16);
+#define NSM_OUT16(STATS_, CW_)                                                                      \
+  hipLaunchKernelGGL((wino_output_kernel<4, STATS_, false, true, true, CW_>), grid, dim3(256), 0, s, \
+                     (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy,        \
+                     STATS_ ? partial : nullptr, WinoAct{}, m16)
+  if (partial) {
+    if (cw == 2) NSM_OUT16(true, 2);
+    else NSM_OUT16(true, 4);
+  } else {
+    if (cw == 2) NSM_OUT16(false, 2);
+    else NSM_OUT16(false, 4);
+  }
+#undef NSM_OUT16
   NSM_LAUNCH_CHECK("wino_output_bf16m");
   return 0;
 }
@@ -3681,9 +3702,17 @@ extern "C" int nsm_wino_output_bf16m_act(const void* M16, const int* m16e, int B
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_bf16m_act: bad shape");
   const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, m16e, (int)((g.T + 63) / 64)};
   const WinoAct act{act_scale, act_shift, slope, nullptr, 0};
-  hipLaunchKernelGGL((wino_output_kernel<4, false, true, true, true>), dim3(grid_1d(g.T * (cout_p / 4))),
-                     dim3(256), 0, as_stream(stream), (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T,
-                     bias, (float*)y, ldy, nullptr, act, m16);
+  const int cw = f16_tx_cw();
+  if (cw == 2)
+    hipLaunchKernelGGL((wino_output_kernel<4, false, true, true, true, 2>),
+                       dim3(grid_1d(g.T * (cout_p / 2))), dim3(256), 0, as_stream(stream),
+                       (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, nullptr,
+                       act, m16);
+  else
+    hipLaunchKernelGGL((wino_output_kernel<4, false, true, true, true, 4>),
+                       dim3(grid_1d(g.T * (cout_p / 4))), dim3(256), 0, as_stream(stream),
+                       (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy, nullptr,
+                       act, m16);
   NSM_LAUNCH_CHECK("wino_output_bf16m_act");
   return 0;
 }
