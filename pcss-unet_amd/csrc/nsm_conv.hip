@@ -3421,6 +3421,8 @@ template <> struct BfLane<4> {
   __device__ static void st16(bf16_t* p, V v) {  // IEEE half
     *(u32x2*)p = __builtin_bit_cast(u32x2, __builtin_convertvector(v, f16x4v));
   }
+  __device__ static W pack(V v) { return W{pack_bf2(v.x, v.y), pack_bf2(v.z, v.w)}; }  // bf16
+  __device__ static V lrg(V z, float s) { return lrelu_grad_v4(z, s); }
 };
 template <> struct BfLane<2> {
   using V = f32x2;
@@ -3430,6 +3432,8 @@ template <> struct BfLane<2> {
   __device__ static V ld(const bf16_t* p) { return cvt(raw(p)); }
   __device__ static V rbf(V v) { return V{round_bf(v.x), round_bf(v.y)}; }
   __device__ static void st16(bf16_t* p, V v) { *(uint32_t*)p = pack_h2(v); }
+  __device__ static W pack(V v) { return pack_bf2(v.x, v.y); }  // bf16
+  __device__ static V lrg(V z, float s) { return V{lrelu_grad(z.x, s), lrelu_grad(z.y, s)}; }
 };
 // NSM_F16_TX_CW: 2 (default) or 4 channels per thread in those transforms
 static int f16_tx_cw() {
@@ -3910,7 +3914,7 @@ extern "C" int nsm_wino_dual_f16(const void* dy, int lddy, int B, int H, int W, 
 // deferred form (nsm_wino_dual_bn_f16): each patch element's dY = k1 dz + k2
 // (y - mean) + k3 is rounded to bf16 exactly where nsm_bn_bwd_apply would
 // store it, then transformed as a loaded dY is
-template <int MT>
+template <int MT, int CW>
 __global__ void __launch_bounds__(256) wino_dual_bn_f16_kernel(
     const bf16_t* __restrict__ g, int ldg, const bf16_t* __restrict__ y, int ldy, int H, int W, int C,
     int TH, int TW, long long T, const float* __restrict__ scale, const float* __restrict__ shift,
@@ -3918,19 +3922,21 @@ __global__ void __launch_bounds__(256) wino_dual_bn_f16_kernel(
     const float* __restrict__ coef, bf16_t* __restrict__ V, bf16_t* __restrict__ dM, H2Scale hv,
     H2Scale hd) {
   constexpr int A = MT + 2;
-  const int C4 = C / 4;
+  using L = BfLane<CW>;
+  using LV = typename L::V;
+  const int C4 = C / CW;
   const long long total = T * C4;
   const float sv = exp2i(h2_exp(hv)), sd = exp2i(h2_exp(hd));  // every lane
   const size_t plane = (size_t)T * C;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
-    const int c = (int)(i % C4) * 4;
+    const int c = (int)(i % C4) * CW;
     const long long t = i / C4;
     const int tx = (int)(t % TW);
     const long long r = t / TW;
     const int ty = (int)(r % TH);
     const long long b = r / TH;
-    u32x2 raw[A][A], yr[A][A];
+    typename L::W raw[A][A], yr[A][A];
 #pragma unroll
     for (int a = 0; a < A; ++a)
 #pragma unroll
@@ -3938,63 +3944,61 @@ __global__ void __launch_bounds__(256) wino_dual_bn_f16_kernel(
         const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
         const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
         const size_t p = (size_t)b * H * W + (in ? (size_t)yy * W + xx : 0);
-        raw[a][e] = *(const u32x2*)(g + p * ldg + c);
-        yr[a][e] = *(const u32x2*)(y + p * ldy + c);
+        raw[a][e] = L::raw(g + p * ldg + c);
+        yr[a][e] = L::raw(y + p * ldy + c);
       }
-    const f32x4 sc = *(const f32x4*)(scale + c), sh = *(const f32x4*)(shift + c);
-    const f32x4 mu = *(const f32x4*)(mean + c);
-    const f32x4 k1 = *(const f32x4*)(coef + c), k2 = *(const f32x4*)(coef + C + c),
-                k3 = *(const f32x4*)(coef + 2 * C + c);
-    const f32x4 mk = mask ? *(const f32x4*)(mask + (size_t)b * C + c) : f32x4{1.f, 1.f, 1.f, 1.f};
+    const LV sc = *(const LV*)(scale + c), sh = *(const LV*)(shift + c);
+    const LV mu = *(const LV*)(mean + c);
+    const LV k1 = *(const LV*)(coef + c), k2 = *(const LV*)(coef + C + c),
+                k3 = *(const LV*)(coef + 2 * C + c);
+    const LV mk = mask ? *(const LV*)(mask + (size_t)b * C + c) : LV{} + 1.f;
 #pragma unroll
     for (int a = 0; a < A; ++a)
 #pragma unroll
       for (int e = 0; e < A; ++e) {
         const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
         const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
-        const f32x4 v = bf4_to_f32(yr[a][e]);
-        f32x4 dz = bf4_to_f32(raw[a][e]) * lrelu_grad_v4(v * sc + sh, slope);
+        const LV v = L::cvt(yr[a][e]);
+        LV dz = L::cvt(raw[a][e]) * L::lrg(v * sc + sh, slope);
         if (mask) dz = dz * mk;
-        const f32x4 d = k1 * dz + k2 * (v - mu) + k3;
-        raw[a][e] = in ? u32x2{pack_bf2(d.x, d.y), pack_bf2(d.z, d.w)} : u32x2{0u, 0u};
+        const LV d = k1 * dz + k2 * (v - mu) + k3;
+        raw[a][e] = in ? L::pack(d) : typename L::W{};
       }
     {
-      f32x4 scv[A][A];
+      LV scv[A][A];
 #pragma unroll
       for (int a = 0; a < A; ++a) {
-        f32x4 d[A];
+        LV d[A];
 #pragma unroll
-        for (int e = 0; e < A; ++e) d[e] = bf4_to_f32(raw[a][e]);
+        for (int e = 0; e < A; ++e) d[e] = L::cvt(raw[a][e]);
         wcol_row<CBt<MT>>(scv, d, a);
       }
       bf16_t* out = V + (size_t)t * C + c;
 #pragma unroll
       for (int a = 0; a < A; ++a) {
-        f32x4 v[A];
+        LV v[A];
         wmat<CBt<MT>>(scv[a], v);
 #pragma unroll
         for (int e = 0; e < A; ++e)
-          *(u32x2*)(out + (a * A + e) * plane) =
-              __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * sv, f16x4v));
+          L::st16(out + (a * A + e) * plane, v[e] * sv);
       }
     }
-    f32x4 scm[A][MT];
+    LV scm[A][MT];
 #pragma unroll
     for (int a = 0; a < MT; ++a) {
-      f32x4 d[MT];
+      LV d[MT];
 #pragma unroll
-      for (int e = 0; e < MT; ++e) d[e] = bf4_to_f32(raw[a + 1][e + 1]);
+      for (int e = 0; e < MT; ++e) d[e] = L::cvt(raw[a + 1][e + 1]);
       wcol_row<CA<MT>>(scm, d, a);
     }
     bf16_t* out = dM + (size_t)t * C + c;
 #pragma unroll
     for (int a = 0; a < A; ++a) {
-      f32x4 v[A];
+      LV v[A];
       wmat<CA<MT>>(scm[a], v);
 #pragma unroll
       for (int e = 0; e < A; ++e)
-        *(u32x2*)(out + (a * A + e) * plane) =
-            __builtin_bit_cast(u32x2, __builtin_convertvector(v[e] * sd, f16x4v));
+        L::st16(out + (a * A + e) * plane, v[e] * sd);
     }
   }
 }
@@ -4012,9 +4016,11 @@ extern "C" int nsm_wino_dual_bn_f16(const void* g, int ldg, const void* y, int l
                 "wino_dual_bn_f16: alignment");
   WinoGeom gm;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, gm), "wino_dual_bn_f16: bad shape");
-  hipLaunchKernelGGL(wino_dual_bn_f16_kernel<4>, dim3(grid_1d(gm.T * c_p / 4)), dim3(256), 0,
-                     as_stream(stream), (const bf16_t*)g, ldg, (const bf16_t*)y, ldy, H, W, c_p, gm.TH,
-                     gm.TW, gm.T, scale, shift, slope, mask, mean, coef, (bf16_t*)V, (bf16_t*)dM,
+  const int cw = f16_tx_cw();
+  hipLaunchKernelGGL((cw == 2 ? wino_dual_bn_f16_kernel<4, 2> : wino_dual_bn_f16_kernel<4, 4>),
+                     dim3(grid_1d(gm.T * c_p / cw)), dim3(256), 0, as_stream(stream),
+                     (const bf16_t*)g, ldg, (const bf16_t*)y, ldy, H, W, c_p, gm.TH, gm.TW, gm.T,
+                     scale, shift, slope, mask, mean, coef, (bf16_t*)V, (bf16_t*)dM,
                      H2Scale{bound, wino_beta(4, 0)}, H2Scale{bound, wino_beta(4, 1)});
   NSM_LAUNCH_CHECK("wino_dual_bn_f16");
   return 0;
