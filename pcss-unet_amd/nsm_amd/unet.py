@@ -69,13 +69,13 @@ WGRAD_F16 = os.environ.get("NSM_WGRAD_F16", "1") != "0"
 # wino_input_f16 + wino_dout_f16 instead of from one read of dY1
 # (ops.wino_dual_f16; B=64 step 1581 / 1586 -> 1596 / 1604 frames/s A/B)
 BF16_DUAL = os.environ.get("NSM_BF16_DUAL", "1") != "0"
-# NSM_LAZY_DY1_F16=1: with BF16_DUAL, the bf16 F(4x4) layers' dY1 formed per
-# element inside the dual transform (ops.wino_dual_bn_f16, scale from the
-# finalize's bound) instead of stored by nsm_bn_bwd_apply and read back. Off by
-# default: measured slower (B=64 step, A/B on one box: 1572 / 1568 with it,
-# 1581 / 1580 frames/s without; the per-thread patch form reads dA1 and Y1,
-# 144 patch registers, and loses the occupancy the single read had)
-LAZY_DY1_F16 = os.environ.get("NSM_LAZY_DY1_F16", "0") != "0"
+# NSM_LAZY_DY1_F16 (default 1): with BF16_DUAL, the bf16 F(4x4) layers' dY1
+# formed per element inside the dual transform (ops.wino_dual_bn_f16, scale
+# from the finalize's bound) instead of stored by nsm_bn_bwd_apply and read
+# back. At 4 channels per thread that kernel ran at one wave per SIMD and lost
+# (1572 / 1568 vs 1581 / 1580 frames/s); at 2 (BfLane<2>) it wins: B=64 step
+# 1611.6 / 1628.0 / 1616.8 vs 1605.1 / 1609.2 / 1613.3 frames/s, A/B on one box
+LAZY_DY1_F16 = os.environ.get("NSM_LAZY_DY1_F16", "1") != "0"
 # NSM_EVAL_FUSED=0: eval forward with separate BN-apply passes instead of the
 # BN + LeakyReLU (+ skip) in the conv epilogues (nsm_conv_fwd_act)
 EVAL_FUSED = os.environ.get("NSM_EVAL_FUSED", "1") != "0"
