@@ -699,7 +699,7 @@ int nsm_conv1x1_dgrad_bnbwd(const void* dy2, int lddy2, int B, int H, int W, int
                             uint32_t* amax_out, void* stream);
 /* (amax_out: fp32 mode 2, may be NULL — max|dy| written, the h2 scale source
  * of its Winograd transforms) */
-int nsm_conv1x1_bnbwd_chunks(int B, int H, int W, int cip, int dtype);
+int nsm_conv1x1_bnbwd_chunks(int B, int H, int W, int cip, int cop, int dtype);
 /* rows per BN-partial chunk of nsm_conv_fwd_bf16 (its M tile) */
 /* Eval-mode DoubleConv half in one pass (Unetmodel.py:21-28 with BatchNorm on
  * its running statistics): y = lrelu(round(conv(x) + bias) * act_scale +

@@ -867,7 +867,7 @@ def conv1x1_dgrad_bn_bwd(dY2, B, H, W, w2d, y, st, mask, c_real, dgamma, dbeta, 
     if dY2.dtype != y.dtype or w2d.dtype != y.dtype:
         raise TypeError("conv1x1_dgrad_bn_bwd: dY2, packed weight and Y1 must share a dtype")
     dtc = dt(y)
-    nchunk = int(lib.nsm_conv1x1_bnbwd_chunks(B, H, W, C, dtc))
+    nchunk = int(lib.nsm_conv1x1_bnbwd_chunks(B, H, W, C, cop, dtc))
     partial = empty(nchunk * 2 * C, device=y.device)
     dA1 = None if recompute else like(M, C, y)
     args = (ptr(dY2), dY2.stride(0), B, H, W, cop, ptr(w2d), C, ptr(y), y.stride(0),
