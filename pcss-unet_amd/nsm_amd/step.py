@@ -34,6 +34,12 @@ class GraphedTrainStep:
         if model._grad_allreduce is not None or model._bn_broadcast is not None:
             raise ValueError("GraphedTrainStep: single process only (the data-parallel "
                              "all-reduce and BN broadcast run eagerly)")
+        if not getattr(optimizer, "sanitize", False):
+            # the plain FlatAdamW step passes its step count (AdamW's bias
+            # correction) as a kernel argument, which a graph would freeze; the
+            # reference's tail (sanitize=True) counts on the device
+            raise ValueError("GraphedTrainStep: needs nsm_amd.FlatAdamW(..., sanitize=True), "
+                             "whose device tail keeps the AdamW step count on the device")
         self.model, self.loss_fn, self.opt = model, loss_fn, optimizer
         self.loss_scale = float(loss_scale)
         self.x = x.detach().clone().requires_grad_(x.requires_grad)
