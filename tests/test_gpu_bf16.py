@@ -74,6 +74,57 @@ def test_conv_fwd_bf16(ops, device, B, H, W, ci, co, k):
     torch.testing.assert_close(pb[:, 1], m2, rtol=1e-3, atol=1e-2)
 
 
+# conv3x3_halo_kernel (csrc/nsm_conv_s16_dma.inc): W in {64, 128, 256}, 64 / 128
+# output channels, >= 256 tiles of 512 pixels; (96 / 32 input channels: 3 and 1
+# channel chunks; the dgrads of those two have 96 / 32 outputs and take the
+# im2col GEMMs)
+HALO_SHAPES = [(2, 256, 256, 128, 128), (8, 128, 128, 64, 128), (64, 64, 64, 128, 64),
+               (2, 256, 256, 96, 64), (2, 256, 256, 32, 64)]
+
+
+@pytest.mark.parametrize("B,H,W,ci,co", HALO_SHAPES)
+@pytest.mark.parametrize("fmt", ["bf16", "f16"])
+def test_conv3x3_halo_fwd_and_dgrad(ops, device, B, H, W, ci, co, fmt, monkeypatch):
+    """The halo-tiled direct 3x3 (opt-in: NSM_BF16_HALO, read at each dispatch)
+    in both 16-bit formats: the forward (with its 256-row BN partials) and the
+    input gradient, against fp32 convolutions of the same rounded operands
+    (only the fp32 summation order and the output rounding differ)."""
+    monkeypatch.setenv("NSM_BF16_HALO", "1")
+    f16 = fmt == "f16"
+    sdt = ops.F16S if f16 else BF
+    rnd = (lambda t: t.half().float()) if f16 else r
+    store = (lambda t: t.to(device).half().view(torch.int16)) if f16 else (lambda t: t.to(device, BF))
+    load = (lambda t: t.view(torch.float16).float()) if f16 else (lambda t: t.float())
+    eps = 2.0 ** -11 if f16 else 2.0 ** -8
+    g = torch.Generator().manual_seed(B * 7 + H + ci + co)
+    x = rnd(torch.randn(B, ci, H, W, generator=g))
+    w = rnd(torch.randn(co, ci, 3, 3, generator=g) / (ci * 9) ** 0.5)
+    b = torch.randn(co, generator=g)
+    torch.set_num_threads(16)
+    wp = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_FWD, sdt)
+    y, part = ops.conv_fwd_bn(store(nhwc(x)), B, H, W, wp, b.to(device), co, 3)
+    assert y.dtype == sdt
+    ref = F.conv2d(x, w, b, padding=1)
+    got = nchw(load(y).cpu(), B, H, W)
+    tol = 2.0 * eps * ref.abs().max().item()
+    assert (got - ref).abs().max().item() <= tol
+    yr = load(y).cpu().double()
+    pb = part.buf.view(part.nchunk, 2, co).cpu().double()
+    assert part.nchunk * part.rpc == B * H * W
+    yd = yr.view(part.nchunk, part.rpc, co)
+    torch.testing.assert_close(pb[:, 0], yd.sum(1), rtol=1e-4, atol=1e-2)
+    m2 = ((yd - yd.mean(1, keepdim=True)) ** 2).sum(1)
+    torch.testing.assert_close(pb[:, 1], m2, rtol=1e-3, atol=1e-2)
+    # input gradient: the 3x3 of dy with the flipped, transposed weights
+    dy = rnd(torch.randn(B, co, H, W, generator=g))
+    xr = x.clone().requires_grad_(True)
+    F.conv2d(xr, w, padding=1).backward(dy)
+    wd = ops.pack_conv_weight(w.to(device), co, ci, ops.PACK_DGRAD, sdt)
+    dx = ops.conv_fwd(store(nhwc(dy)), B, H, W, wd, None, ci, 3)
+    got = nchw(load(dx).cpu(), B, H, W)
+    assert (got - xr.grad).abs().max().item() <= 2.0 * eps * xr.grad.abs().max().item()
+
+
 @pytest.mark.parametrize("B,H,W,ci,co", [(2, 6, 7, 32, 64), (2, 16, 16, 128, 64)])
 def test_conv1x1_prologue_bf16(ops, device, B, H, W, ci, co):
     g = torch.Generator().manual_seed(7)
