@@ -123,6 +123,35 @@ BNB_MODE = int(os.environ.get("NSM_BNB", "2"))
 # ops.resize_bwd, ops.up2_resize_bwd with bnred=); NSM_GRAD_BNRED=0 runs the
 # separate nsm_bn_bwd_reduce pass instead
 GRAD_BNRED = os.environ.get("NSM_GRAD_BNRED", "1") != "0"
+# The weight-gradient launches of the Unet backward (GEMM, split reduce,
+# Winograd weight-gradient output) run on a second stream: nothing on the
+# input-gradient path reads them, so they fill its latency-bound launches and
+# kernel tails. Single process only (the data-parallel all-reduce buckets read
+# the gradients in order); NSM_WGRAD_STREAM=0 keeps one stream
+# (also off under NSM_STAGE_MARKS: the per-stage counters attribute kernels by
+# their order between the marker launches)
+WGRAD_STREAM = (os.environ.get("NSM_WGRAD_STREAM", "1") != "0"
+                and os.environ.get("NSM_STAGE_MARKS", "0") == "0")
+_wg_stream = None      # the side stream while a Unet backward runs, else None
+_wg_streams = {}       # one side stream per device
+
+
+def _wgrad(fn, *reads):
+    """Run fn (weight-gradient launches) on the side stream after everything
+    queued so far on the current stream. The tensors it reads are recorded on
+    the side stream, so the allocator keeps their memory from the current
+    stream until the side stream has used it (under graph capture it defers
+    those frees to the end of the capture)."""
+    side = _wg_stream
+    if side is None:
+        fn()
+        return
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        fn()
+    for t in reads:
+        if isinstance(t, torch.Tensor):
+            t.record_stream(side)
 
 
 def bnb_mode(cip, cop, dtype, h2=False):
@@ -684,9 +713,11 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
         am_dy2 = _slot(s.am, AM_DY2B)
         dY2h = ops.bn_bwd(G, s.Y2, s.bn2, HW, None, co, g[bn2m.weight], g[bn2m.bias], g[c4.bias],
                           part=gpart, h2=(_slot(s.am, AM_K1DZ), am_dy2))
-        ops.conv1x1_wgrad_h2(dY2h, s.A1, ci, co, g[c4.weight], amax=(am_dy2, _slot(s.am, AM_A1)),
-                             tag=name + ".conv.4.wgrad")
-        s.A1 = None
+        A1 = s.A1
+        _wgrad(lambda: ops.conv1x1_wgrad_h2(dY2h, A1, ci, co, g[c4.weight],
+                                            amax=(am_dy2, _slot(s.am, AM_A1)),
+                                            tag=name + ".conv.4.wgrad"), dY2h, A1)
+        s.A1 = A1 = None
         # h2 Winograd 3x3: one GEMM pass storing dA1 + the BN-backward partials;
         # the dual transform forms dY1 per element (wino_dual_input_bn_h2), so
         # dY1 is never stored and the GEMM never recomputed, under the bound
@@ -711,12 +742,15 @@ def _block_bwd(blk, s, G, grads, need_dx, name="", gpart=None):
                      part=gpart, amax=_slot(s.am, AM_DY2))
     am_w2d = (_slot(s.am, AM_DY2), s.pw.amax_w2(ops.PACK_DGRAD))
     if s.A1 is not None:
-        ops.conv_wgrad(dY2, s.A1, B, H, W, 1, ci, co, g[c4.weight], tag=name + ".conv.4.wgrad",
-                       amax=(_slot(s.am, AM_DY2), _slot(s.am, AM_A1)))
-        s.A1 = None
+        A1 = s.A1
+        _wgrad(lambda: ops.conv_wgrad(dY2, A1, B, H, W, 1, ci, co, g[c4.weight],
+                                      tag=name + ".conv.4.wgrad",
+                                      amax=(_slot(s.am, AM_DY2), _slot(s.am, AM_A1))), dY2, A1)
+        s.A1 = A1 = None
     else:
-        ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight],
-                       pro=(s.bn1.scale, s.bn1.shift, s.mask), tag=name + ".conv.4.wgrad")
+        pro = (s.bn1.scale, s.bn1.shift, s.mask)
+        _wgrad(lambda: ops.conv_wgrad(dY2, s.Y1, B, H, W, 1, ci, co, g[c4.weight], pro=pro,
+                                      tag=name + ".conv.4.wgrad"), dY2, s.Y1, *pro)
     mode = bnb_mode(s.cip, s.cop, dtype)
     if mode == 2 and _wino_f16(s):
         mode = 1   # dY1 through nsm_bn_bwd_apply, which records max|dY1| (the dgrad's V scale)
@@ -760,10 +794,11 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
             Vd, dM = ops.wino_dual_input_bn_h2(dY1, s.Y1, s.bn1, s.mask, B, H, W, tile, am_dy1)
         else:
             Vd, dM = ops.wino_dual_input_h2(dY1, B, H, W, tile, am_dy1)
-        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=tile,
-                               tag=name + ".conv.0.wgrad", dM=dM,
-                               amax=(am_dy1, _slot(s.am, AM_X)))
-        s.V = None
+        V = s.V
+        _wgrad(lambda: ops.conv3x3_wgrad_wino(dY1, V, B, H, W, s.cip, ci, ci, g[c0.weight],
+                                              tile=tile, tag=name + ".conv.0.wgrad", dM=dM,
+                                              amax=(am_dy1, _slot(s.am, AM_X))), dM, V)
+        s.V = V = None
         if not need_dx:
             return None
         return ops.conv3x3_wino(dY1, B, H, W, s.pw.U1(tile, True), None, s.cip, tile=tile,
@@ -780,14 +815,17 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
                                                 amax=am2)
             else:
                 Vd, dM = ops.wino_dual_input(dY1, B, H, W, tile=tile, amax=am2)
-        ops.conv3x3_wgrad_wino(dY1, s.V, B, H, W, s.cip, ci, ci, g[c0.weight], tile=tile,
-                               tag=name + ".conv.0.wgrad", dM=dM,
-                               amax=(_slot(s.am, AM_DM), _slot(s.am, AM_V)))
-        s.V = None
+        V = s.V
+        _wgrad(lambda: ops.conv3x3_wgrad_wino(dY1, V, B, H, W, s.cip, ci, ci, g[c0.weight],
+                                              tile=tile, tag=name + ".conv.0.wgrad", dM=dM,
+                                              amax=(_slot(s.am, AM_DM), _slot(s.am, AM_V))),
+               dM, V, dY1 if dM is None else None)
+        s.V = V = None
     elif s.X is not None and s.X.dtype == ops.H2:   # direct 3x3 on h2 operands (dY1 from the BN backward)
         assert dY1.dtype == ops.H2
-        ops.conv3x3_wgrad_h2(dY1, s.X, B, H, W, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad",
-                             amax=(am_dy1, _slot(s.am, AM_X)))
+        _wgrad(lambda: ops.conv3x3_wgrad_h2(dY1, s.X, B, H, W, ci, ci, g[c0.weight],
+                                            tag=name + ".conv.0.wgrad",
+                                            amax=(am_dy1, _slot(s.am, AM_X))), dY1, s.X)
         if not need_dx:
             return None
         return ops.conv3x3_h2(dY1, B, H, W, s.pw.w1(ops.PACK_DGRAD), None, s.cip, stats=False,
@@ -800,12 +838,15 @@ def _block_bwd_3x3(blk, s, dY1, grads, need_dx, name, h2, am_dy1):
             Vd, dM = ops.wino_dual_f16(dY1, B, H, W, am_dy1)
         else:
             dM = ops.wino_dout_f16(dY1, B, H, W, am_dy1)
-        ops.conv3x3_wgrad_wino_f16(dM, s.Vf16, B, H, W, s.cip, s.cip, ci, ci, g[c0.weight],
-                                   amax=(am_dy1, _slot(s.am, AM_X)), tag=name + ".conv.0.wgrad")
-        s.Vf16 = None
+        Vf = s.Vf16
+        _wgrad(lambda: ops.conv3x3_wgrad_wino_f16(dM, Vf, B, H, W, s.cip, s.cip, ci, ci,
+                                                  g[c0.weight], amax=(am_dy1, _slot(s.am, AM_X)),
+                                                  tag=name + ".conv.0.wgrad"), dM, Vf)
+        s.Vf16 = Vf = None
     else:
-        ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight], tag=name + ".conv.0.wgrad",
-                       amax=(am_dy1, _slot(s.am, AM_X)))
+        _wgrad(lambda: ops.conv_wgrad(dY1, s.X, B, H, W, 3, ci, ci, g[c0.weight],
+                                      tag=name + ".conv.0.wgrad",
+                                      amax=(am_dy1, _slot(s.am, AM_X))), dY1, s.X)
     if not need_dx:
         return None
     if s.cip >= WINOGRAD_MIN_CHANNELS and dtype == torch.float32:
@@ -1089,6 +1130,24 @@ class _UnetFn(torch.autograd.Function):
             off += p.numel()
         dp = mod._grad_allreduce
         split = offset_of.get(id(mod.conv6.conv[0].weight)) if dp is not None else None
+        global _wg_stream
+        side = None
+        if WGRAD_STREAM and dp is None:
+            side = _wg_streams.get(dev)
+            if side is None:
+                side = _wg_streams[dev] = torch.cuda.Stream(device=dev)
+        _wg_stream = side
+        try:
+            return _UnetFn._backward(ctx, gout, mod, out, params, flat, grads, views, dp, split)
+        finally:
+            _wg_stream = None
+            if side is not None:   # the gradients are complete when backward returns
+                torch.cuda.current_stream().wait_stream(side)
+
+    @staticmethod
+    def _backward(ctx, gout, mod, out, params, flat, grads, views, dp, split):
+        B, C, H, W, orig_hw, Rh, Rw, training = ctx.meta
+        total = flat.numel()
 
         gout = gout.contiguous().to(torch.float32)
         with ops.stage("head.bwd"):
