@@ -126,14 +126,21 @@ GRAD_BNRED = os.environ.get("NSM_GRAD_BNRED", "1") != "0"
 # The weight-gradient launches of the Unet backward (GEMM, split reduce,
 # Winograd weight-gradient output) run on a second stream: nothing on the
 # input-gradient path reads them, so they fill its latency-bound launches and
-# kernel tails. Single process only (the data-parallel all-reduce buckets read
-# the gradients in order); NSM_WGRAD_STREAM=0 keeps one stream
+# kernel tails. Under data parallelism the main stream joins the side stream
+# before each gradient bucket's all-reduce is queued; NSM_WGRAD_STREAM=0 keeps
+# one stream
 # (also off under NSM_STAGE_MARKS: the per-stage counters attribute kernels by
 # their order between the marker launches)
 WGRAD_STREAM = (os.environ.get("NSM_WGRAD_STREAM", "1") != "0"
                 and os.environ.get("NSM_STAGE_MARKS", "0") == "0")
 _wg_stream = None      # the side stream while a Unet backward runs, else None
 _wg_streams = {}       # one side stream per device
+
+
+def _join_wgrad():
+    """The current stream waits for the weight gradients queued so far."""
+    if _wg_stream is not None:
+        torch.cuda.current_stream().wait_stream(_wg_stream)
 
 
 def _wgrad(fn, *reads):
@@ -1132,7 +1139,7 @@ class _UnetFn(torch.autograd.Function):
         split = offset_of.get(id(mod.conv6.conv[0].weight)) if dp is not None else None
         global _wg_stream
         side = None
-        if WGRAD_STREAM and dp is None:
+        if WGRAD_STREAM:
             side = _wg_streams.get(dev)
             if side is None:
                 side = _wg_streams[dev] = torch.cuda.Stream(device=dev)
@@ -1176,6 +1183,7 @@ class _UnetFn(torch.autograd.Function):
                 skip_grad[SKIP_OF[k - 1]] = dprev
             G = dprev
         if split is not None:   # conv6..conv10 grads are final: overlap their all-reduce
+            _join_wgrad()
             optim.allreduce_async(flat, split, total, dp[0])
         # encoder: G is now d c5
         need_x = ctx.needs_input_grad[0]
@@ -1204,6 +1212,7 @@ class _UnetFn(torch.autograd.Function):
                 G = dX
             st.__exit__(None, None, None)
         if split is not None:
+            _join_wgrad()
             optim.allreduce_async(flat, 0, split, dp[0])
         dx = None
         if need_x:
