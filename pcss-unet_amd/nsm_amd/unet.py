@@ -133,6 +133,9 @@ GRAD_BNRED = os.environ.get("NSM_GRAD_BNRED", "1") != "0"
 # their order between the marker launches)
 WGRAD_STREAM = (os.environ.get("NSM_WGRAD_STREAM", "1") != "0"
                 and os.environ.get("NSM_STAGE_MARKS", "0") == "0")
+# NSM_WGRAD_PRIO: the side stream's priority (torch.cuda.Stream priority: lower
+# numbers run first; 0 = the default streams')
+WGRAD_PRIO = int(os.environ.get("NSM_WGRAD_PRIO", "0"))
 _wg_stream = None      # the side stream while a Unet backward runs, else None
 _wg_streams = {}       # one side stream per device
 
@@ -1142,7 +1145,7 @@ class _UnetFn(torch.autograd.Function):
         if WGRAD_STREAM:
             side = _wg_streams.get(dev)
             if side is None:
-                side = _wg_streams[dev] = torch.cuda.Stream(device=dev)
+                side = _wg_streams[dev] = torch.cuda.Stream(device=dev, priority=WGRAD_PRIO)
         _wg_stream = side
         try:
             return _UnetFn._backward(ctx, gout, mod, out, params, flat, grads, views, dp, split)
