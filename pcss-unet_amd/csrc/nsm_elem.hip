@@ -1644,11 +1644,11 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(
     int b = (int)(t / Rh);
     float d[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int di = j >> 1, dj = j & 1;
-      size_t o = ((size_t)b * 2 * Rh + 2 * ry + di) * (2 * Rw) + 2 * rx + dj;
-      float ov = out[o];
-      d[j] = gout[o] * (1.f - ov) * ov;  // ATen sigmoid_backward
+    for (int di = 0; di < 2; ++di) {  // the (dj = 0, 1) pair is adjacent: one 8-B load each
+      size_t o = ((size_t)b * 2 * Rh + 2 * ry + di) * (2 * Rw) + 2 * rx;
+      const f32x2 ov = *(const f32x2*)(out + o), gv = *(const f32x2*)(gout + o);
+      d[2 * di] = gv.x * (1.f - ov.x) * ov.x;  // ATen sigmoid_backward
+      d[2 * di + 1] = gv.y * (1.f - ov.y) * ov.y;
     }
     const T* zr = z + (size_t)p * ldz;
     T* dzr = dz + (size_t)p * ldz;
@@ -1676,8 +1676,22 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(
     for (int j = 0; j < 4; ++j) accw[64 + j] += d[j];
   }
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // dw10 (64 sums): a reduce-scatter butterfly. Each xor step halves the values
+  // a lane holds (it keeps the half its lane bit selects and adds the partner's
+  // copy of it), so after 6 steps lane L holds the wave sum of accw[L]: 63
+  // cross-lane moves instead of 64 full wave reductions (384)
 #pragma unroll
-  for (int k = 0; k < 68; ++k) {
+  for (int o = 32; o >= 1; o >>= 1) {
+    const bool up = (lane & o) != 0;
+#pragma unroll
+    for (int i = 0; i < o; ++i) {
+      const float lo = accw[i], hi = accw[i + o];
+      accw[i] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, o, 64);
+    }
+  }
+  red[wv][lane] = accw[0];
+#pragma unroll
+  for (int k = 64; k < 68; ++k) {
     float s = wave_sum(accw[k]);
     if (lane == 0) red[wv][k] = s;
   }
