@@ -2187,13 +2187,20 @@ extern "C" int nsm_avgpool2_fwd(const void* x, int B, int H, int W, int C, void*
   return 0;
 }
 
+// Blocks of the fused-reduction form: at most one chip-wide pass of 8 waves per
+// SIMD (2048 blocks of 256), so every block folds several pixels into its
+// partial row. At 8192 blocks the conv4-level call (64x64, 512 channels) ran one
+// pixel per thread and wrote 4 KB of partials per block: 33.5 MB, half the size
+// of dx, written and read back by the merge
+static inline int pool_bnred_grid(long long work) { return grid_for(work, 256, 2048); }
+
 static int avgpool2_bwd_add(const void* dy, int B, int H, int W, int C, const void* skip, void* dx,
                             int dtype, const BnRedP* rp, void* stream) {
   NSM_CHECK_ARG(dy && dx && C % 8 == 0, "avgpool2_bwd: bad args");
   long long work = (long long)B * H * W * (C / 8);
   NSM_CHECK_ARG(work < (1ll << 31), "avgpool2_bwd: too large");
   NSM_CHECK_ARG(!rp || 256 % (C / 8) == 0, "avgpool2_bwd: fused BN reduction needs C/8 | 256");
-  dim3 g(grid_for(work));
+  dim3 g(rp ? pool_bnred_grid(work) : grid_for(work));  // rp: the rows nsm_bnred_chunks reports
   const FastDiv f8 = make_fastdiv(C / 8), fw = make_fastdiv(W), fh = make_fastdiv(H);
   const BnRedP r = rp ? *rp : BnRedP{};
   hipStream_t s = as_stream(stream);
@@ -2507,7 +2514,7 @@ extern "C" int nsm_bnred_chunks(int kind, int B, int H, int W, int C) {
   if (B <= 0 || H <= 0 || W <= 0 || C % 8 || 256 % (C / 8)) return 0;
   if (kind == 0) {
     const long long work = (long long)B * H * W * (C / 8);
-    return work < (1ll << 31) ? grid_for(work) : 0;
+    return work < (1ll << 31) ? pool_bnred_grid(work) : 0;
   }
   if (kind == 1 && !rows_resize()) return 0;
   if ((kind == 1 || kind == 2) && W <= U2_MAXW && (long long)B * H < (1ll << 31) &&
