@@ -531,6 +531,8 @@ def _summary(r):
            "roofline": {k: roof.get(k) for k in ("achieved", "frac", "avg_launch_ms", "traffic")}}
     if "dp" in r:
         out["dp"] = r["dp"]
+    if "eager" in r:
+        out["eager"] = {k: r["eager"][k] for k in ("value", "ms_per_step", "steps")}
     if r["config"]["workload"].startswith(("configs[2]", "configs[3]")):
         out["stages"] = r["stages"]
     if "vgg_perceptual" in r:
@@ -638,6 +640,8 @@ def train_measure(args, world, rank, dev):
     # below come from eager steps of the same shapes (HIP events cannot be read
     # from inside a replayed graph). NSM_GRAPH_STEP=0: eager timed steps.
     graphed = None
+    dp_tags = ("dp.bn_broadcast", "dp.allreduce_wait")
+    eager_elapsed, eager_steps = None, max(3, min(args.steps, 10))
     if world == 1 and os.environ.get("NSM_GRAPH_STEP", "1") != "0":
         graphed = nsm_amd.GraphedTrainStep(model, crit, opt, x, y, loss_scale=loss_scale,
                                            warmup=1)
@@ -645,7 +649,20 @@ def train_measure(args, world, rank, dev):
             graphed()
         torch.cuda.synchronize()
         elapsed = timed(graphed, args.steps, world, dev)
+        # the eager step (what an unchanged main.py and every DP rank run),
+        # timed back to back like the replays, no probes
+        eager_elapsed = timed(step, eager_steps, world, dev)
+    else:
+        # eager timed steps (DP ranks): only the DP waits carry HIP events
+        for t in dp_tags:
+            nops.PROBES[t] = []
+        elapsed = timed(step, args.steps, world, dev)
+    dp_ms = {t: mean_ms(nops.PROBES.pop(t, [])) for t in dp_tags}
 
+    # attribution steps (not timed): kernel and stage times from HIP events
+    # with the weight gradients on the main stream, the configuration the
+    # per-stage counters are taken in (tools/stage_pmc.py, NSM_STAGE_MARKS),
+    # so each stage's bytes and time describe the same kernels
     probe_tag = "conv6.conv.0.fwd"
     nops.PROBES[probe_tag] = []
     nops.PROBES[probe_tag + ".gemm"] = []
@@ -655,16 +672,14 @@ def train_measure(args, world, rank, dev):
     nops.PROBES["vgg.fwd"] = []
     nops.PROBES["vgg.30"] = []
     nops.PROBES["vgg.30.gemm"] = []
-    dp_tags = ("dp.bn_broadcast", "dp.allreduce_wait")
-    for t in dp_tags:
-        nops.PROBES[t] = []
-    if graphed is None:
-        elapsed = timed(step, args.steps, world, dev)
-    else:   # eager probe steps (not timed)
+    from nsm_amd import unet as nunet
+    side_prev, nunet.WGRAD_STREAM = nunet.WGRAD_STREAM, False
+    try:
         for _ in range(min(args.steps, 10)):
             step()
         torch.cuda.synchronize()
-    dp_ms = {t: mean_ms(nops.PROBES.pop(t)) for t in dp_tags}
+    finally:
+        nunet.WGRAD_STREAM = side_prev
     evs = nops.PROBES.pop(probe_tag)
     kern_ms = mean_ms(evs)
     gemm_ms = mean_ms(nops.PROBES.pop(probe_tag + ".gemm"))
@@ -731,10 +746,20 @@ def train_measure(args, world, rank, dev):
         "stages": stage_table(work, times, pipe_mult, peak, measured),
         "stage_pmc_source": measured_src,
         "roofline": roof,
-        "step_execution": ("one hipGraph replay per step (nsm_amd.GraphedTrainStep); kernel and "
-                           "stage times from eager steps of the same shapes" if graphed is not None
-                           else "eager"),
+        "step_execution": ("one hipGraph replay per step (nsm_amd.GraphedTrainStep)"
+                           if graphed is not None else
+                           "eager (weight gradients on the side stream)"),
+        "stage_execution": "eager attribution steps after the timed ones, weight gradients on "
+                           "the main stream (NSM_WGRAD_STREAM=0: the configuration of the "
+                           "stage PMC), HIP events per stage",
     }
+    if eager_elapsed is not None:
+        res["eager"] = {"value": round(world * B * eager_steps / eager_elapsed, 3),
+                        "ms_per_step": round(eager_elapsed / eager_steps * 1e3, 3),
+                        "steps": eager_steps,
+                        "what": "the same step run eagerly (an unchanged main.py loop; the "
+                                "per-rank step of data parallelism), back to back, weight "
+                                "gradients on the side stream"}
     if world > 1:
         res["dp"] = {"bn_broadcast_ms": round(dp_ms["dp.bn_broadcast"], 4),
                      "allreduce_wait_ms": round(dp_ms["dp.allreduce_wait"], 4),

@@ -78,11 +78,20 @@ class _RangeCheck:
             raise AssertionError(f"{self.what}: output must be in [0, 1] (sigmoid output), "
                                  "customLoss.py:131")
 
-    def launch(self, o):
-        if self.flag is None or self.flag.device != o.device:
-            self.flag = torch.zeros(1, dtype=torch.int32, device=o.device)
+    def prepare(self, device):
+        """Allocate the flag, its pinned host copy and the event on `device`
+        (outside any graph capture: a capture would record the flag's zeroing
+        into every replay, which would make it non-sticky)."""
+        if self.flag is None or self.flag.device != torch.device(device):
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError(f"{self.what}: the range flag must be allocated before graph "
+                                   "capture (call prepare_capture(device) first)")
+            self.flag = torch.zeros(1, dtype=torch.int32, device=device)
             self.host = torch.zeros(1, dtype=torch.int32).pin_memory()
             self.event = torch.cuda.Event()
+
+    def launch(self, o):
+        self.prepare(o.device)
         if torch.cuda.is_current_stream_capturing():
             # a captured step (GraphedTrainStep): the sticky device flag only —
             # no event, no copy; check() reads the flag itself
@@ -190,6 +199,12 @@ class CustomLoss(nn.Module):
         """Raise now (host sync) if any output seen so far left [0, 1]."""
         self._range.check()
 
+    def prepare_capture(self, device):
+        """Allocate the range assert's device state before a graph capture
+        (GraphedTrainStep calls it)."""
+        if self.check_range:
+            self._range.prepare(device)
+
 
 class PerturbationLoss(nn.Module):
     def __init__(self, perturbation_count=3, alpha=0.9, std_factor=0.01):
@@ -237,6 +252,12 @@ class EnhancedCustomLoss(nn.Module):
         self.base = CustomLoss(device, alpha, vgg=vgg, vgg_weights=vgg_weights)
         self.vgg_loss = getattr(self.base, "vgg_loss", None) or vgg
         self.perturbation_loss = PerturbationLoss()
+
+    def prepare_capture(self, device):
+        self.base._range.prepare(device)
+
+    def check_range_now(self):
+        self.base._range.check()
 
     def forward(self, model, output, target, inputs, noises=None):
         # pert_loss.py:131: the same [0, 1] assertion, as CustomLoss's device flag

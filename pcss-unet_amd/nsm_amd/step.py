@@ -12,8 +12,11 @@ What the graph holds fixed, and how the step stays the reference's:
     (`step(x, y)` does it);
   * Dropout2d masks: drawn from torch's graph-safe CUDA generator inside the
     graph (unet._masks_for -> nsm_dropout_masks_dev), new masks every replay;
-  * the CustomLoss range assert: its sticky device flag only
-    (`loss_fn.check_range_now()` reads it);
+  * the CustomLoss range assert: its sticky device flag only, allocated
+    before the capture (`loss_fn.prepare_capture`); `loss_fn.check_range_now()`
+    reads it, or the step itself every `range_check_every` replays;
+  * version counters: each replay bumps those of the parameters and buffers
+    (the kernels rewrote them), so infer.GraphedUnet refreshes its layouts;
   * hyper-parameters passed as kernel arguments (lr, betas, eps, weight decay,
     max_norm, the loss scale): the step re-captures when one of them changes
     (an epoch's LambdaLR / max_norm schedule costs one capture);
@@ -26,10 +29,12 @@ buffers, so building the step changes no training state. Single process only
 import torch
 
 from ._lib import require_gpu
+from .optim import _bump
 
 
 class GraphedTrainStep:
-    def __init__(self, model, loss_fn, optimizer, x, y, loss_scale=1.0, warmup=3):
+    def __init__(self, model, loss_fn, optimizer, x, y, loss_scale=1.0, warmup=3,
+                 range_check_every=0):
         require_gpu(x, "GraphedTrainStep input")
         if model._grad_allreduce is not None or model._bn_broadcast is not None:
             raise ValueError("GraphedTrainStep: single process only (the data-parallel "
@@ -45,6 +50,11 @@ class GraphedTrainStep:
         self.x = x.detach().clone().requires_grad_(x.requires_grad)
         self.y = y.detach().clone()
         self.warmup = warmup
+        # every N-th replay raises the reference's `assert 0 <= output <= 1`
+        # (customLoss.py:131) from the sticky device flag (a host sync); 0:
+        # only when the caller runs loss_fn.check_range_now()
+        self.range_check_every = int(range_check_every)
+        self.replays = 0
         self.graph = None
         self._capture()
 
@@ -82,6 +92,9 @@ class GraphedTrainStep:
             for _ in range(warmup):   # allocator, weight-layout and mask-descriptor caches
                 self._body()
         torch.cuda.current_stream().wait_stream(side)
+        prep = getattr(self.loss_fn, "prepare_capture", None)
+        if prep is not None:   # the range assert's sticky flag, allocated outside the capture
+            prep(self.x.device)
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):   # recorded, not run
             self.loss = self._body()
@@ -108,4 +121,14 @@ class GraphedTrainStep:
             self.graph = None
             self._capture(warmup=0)   # the caches are warm
         self.graph.replay()
+        # the replay rewrote the parameters and the BN buffers with HIP kernels;
+        # the Python-side version bumps (FlatAdamW's, the forward's BN one) ran
+        # only at capture: bump them here so version-keyed caches
+        # (infer.GraphedUnet's frozen layouts and eval BN vectors) refresh
+        _bump(list(self.model.parameters()) + list(self.model.buffers()))
+        self.replays += 1
+        if self.range_check_every and self.replays % self.range_check_every == 0:
+            check = getattr(self.loss_fn, "check_range_now", None)
+            if check is not None:
+                check()
         return self.loss

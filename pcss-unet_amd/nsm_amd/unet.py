@@ -138,30 +138,56 @@ WGRAD_STREAM = (os.environ.get("NSM_WGRAD_STREAM", "1") != "0"
 WGRAD_PRIO = int(os.environ.get("NSM_WGRAD_PRIO", "0"))
 _wg_stream = None      # the side stream while a Unet backward runs, else None
 _wg_streams = {}       # one side stream per device
+# The tensors the queued side-stream launches read, held (not freed) until the
+# main stream has waited for those launches: [(event recorded on the side
+# stream after them, tensors, bytes)], oldest first. Once the held bytes
+# exceed NSM_WGRAD_HOLD_GB the oldest entries are released, each after the
+# main stream waits for its event (a launch or two behind the side stream's
+# tail, so the wait rarely stalls it).
+#
+# Not record_stream: a block recorded on another stream returns to the
+# allocator only when the allocator, at a later malloc, finds that stream's
+# event complete. An eager loop whose host runs ahead of the GPU then finds
+# none complete and takes fresh device memory every step — the B=64 bf16
+# eager step's reserved memory grew 5.9-9.7 GB per step, and once hipMalloc
+# slowed (2.97 s inside one conv7 backward) the stage averaged 266-278 ms
+# (tools/eager_probe.py --bench; DESIGN.md "The eager-step stall").
+WGRAD_HOLD_BYTES = int(float(os.environ.get("NSM_WGRAD_HOLD_GB", "8")) * (1 << 30))
+_wg_hold = []
 
 
 def _join_wgrad():
-    """The current stream waits for the weight gradients queued so far."""
+    """The current stream waits for the weight gradients queued so far; the
+    tensors they read are released (the allocator reuses their memory on the
+    current stream, now ordered after those reads)."""
     if _wg_stream is not None:
         torch.cuda.current_stream().wait_stream(_wg_stream)
+    _wg_hold.clear()
 
 
 def _wgrad(fn, *reads):
     """Run fn (weight-gradient launches) on the side stream after everything
-    queued so far on the current stream. The tensors it reads are recorded on
-    the side stream, so the allocator keeps their memory from the current
-    stream until the side stream has used it (under graph capture it defers
-    those frees to the end of the capture)."""
+    queued so far on the current stream. The tensors it reads stay referenced
+    until the current stream has waited for it (_wg_hold), so their memory is
+    never handed to a later launch on the current stream before fn's kernels
+    have read it."""
     side = _wg_stream
     if side is None:
         fn()
         return
-    side.wait_stream(torch.cuda.current_stream())
+    cur = torch.cuda.current_stream()
+    side.wait_stream(cur)
     with torch.cuda.stream(side):
         fn()
-    for t in reads:
-        if isinstance(t, torch.Tensor):
-            t.record_stream(side)
+    ev = torch.cuda.Event()
+    ev.record(side)
+    ts = [t for t in reads if isinstance(t, torch.Tensor)]
+    _wg_hold.append((ev, ts, sum(t.untyped_storage().nbytes() for t in ts)))
+    held = sum(h[2] for h in _wg_hold)
+    while held > WGRAD_HOLD_BYTES and len(_wg_hold) > 1:
+        e, _, nb = _wg_hold.pop(0)
+        cur.wait_event(e)
+        held -= nb
 
 
 def bnb_mode(cip, cop, dtype, h2=False):
@@ -1153,6 +1179,7 @@ class _UnetFn(torch.autograd.Function):
             _wg_stream = None
             if side is not None:   # the gradients are complete when backward returns
                 torch.cuda.current_stream().wait_stream(side)
+            _wg_hold.clear()
 
     @staticmethod
     def _backward(ctx, gout, mod, out, params, flat, grads, views, dp, split):

@@ -93,3 +93,69 @@ def test_graphed_step_range_assert(device):
     step = nsm_amd.GraphedTrainStep(m, crit, opt, x, y, warmup=1)
     step()
     crit.check_range_now()   # sigmoid output: in range, nothing raised
+
+
+def test_graphed_unet_follows_graphed_train_step(device):
+    """A GraphedUnet built before training sees the weights and BN running
+    statistics that GraphedTrainStep replays wrote (the replay bumps their
+    version counters): its output equals an eager eval forward afterwards."""
+    import nsm_amd
+    m, opt, crit, x, y = _setup(device, 0.2)
+    step = nsm_amd.GraphedTrainStep(m, crit, opt, x, y, warmup=1)
+    gu = nsm_amd.GraphedUnet(m, x[:1])
+    before = gu(x[:1]).clone()
+    for _ in range(3):
+        step()
+    after = gu(x[:1]).clone()
+    m.eval()
+    with torch.no_grad():
+        ref = m(x[:1])
+    m.train()
+    assert not torch.equal(before, after)
+    torch.testing.assert_close(after, ref, rtol=0, atol=0)
+
+
+def test_graphed_step_recapture_keeps_sticky_flag(device):
+    """A re-capture (warmup=0) with a range check whose flag was never
+    allocated: the flag is allocated before the capture, so a replay does not
+    re-zero it (it stays sticky) and the step's every-2nd-replay check raises
+    after an out-of-range output was seen."""
+    import nsm_amd
+    from nsm_amd import losses
+    m, opt, crit, x, y = _setup(device, 0.0)
+    step = nsm_amd.GraphedTrainStep(m, crit, opt, x, y, warmup=1, range_check_every=2)
+    crit._range = losses._RangeCheck("CustomLoss")   # no flag yet
+    opt.param_groups[0]["lr"] = 5e-4                 # the next call re-captures, warmup=0
+    step()
+    step()                      # replay 2 checks the flag: in range
+    crit._range.flag.fill_(1)   # as if an output had left [0, 1]
+    step()
+    with pytest.raises(AssertionError):
+        step()                  # replay 4 checks: the flag survived replay 3
+
+
+def test_eager_steps_back_to_back_keep_memory_flat(device):
+    """Eager steps queued back to back (the host ahead of the GPU) with the
+    weight gradients on the side stream: after the first steps the caching
+    allocator reserves no new device memory (the tensors the side stream
+    reads are held until the main stream waited for it, not record_stream-ed,
+    whose blocks return only once the allocator sees their events complete)."""
+    import nsm_amd
+    from nsm_amd import unet
+    assert unet.WGRAD_STREAM
+    m, opt, crit, x, y = _setup(device, 0.2, B=8, H=512)
+
+    def step():
+        loss = crit(m(x), y, x)
+        loss.backward()
+        opt.step()
+        opt.zero_grad()
+
+    for _ in range(3):
+        step()
+    torch.cuda.synchronize()
+    r0 = torch.cuda.memory_stats()["num_device_alloc"]
+    for _ in range(12):        # no synchronisation between the steps
+        step()
+    torch.cuda.synchronize()
+    assert torch.cuda.memory_stats()["num_device_alloc"] == r0
