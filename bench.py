@@ -422,6 +422,13 @@ def init_dist(args):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         assert dist.get_world_size() == args.gpus
+    elif getattr(args, "force_dp", False) and not dist.is_initialized():
+        # --force-dp at N=1: the data-parallel step over a world-size-1 RCCL group
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=0, world_size=1,
+                                device_id=torch.device("cuda", local))
     return world, rank, torch.device("cuda", local)
 
 
@@ -502,7 +509,7 @@ def run_train(args):
             res["cpu_baseline"]["sample"] += " (fp32: the reference's CPU path)"
     if rank == 0:
         emit(res, args)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
         dist.destroy_process_group()
 
@@ -598,7 +605,10 @@ def train_measure(args, world, rank, dev):
     # f16: GradScaler's loss scale (main.py:175,281; its initial 2^16, held
     # fixed here), unscaled inside the tail (main.py:361-368)
     loss_scale = 65536.0 if f16 else 1.0
-    if world > 1:  # identical initial weights on every rank (DDP semantics)
+    # data parallel at N > 1, or at N = 1 over a world-size-1 RCCL group
+    # (--force-dp: the per-rank step of configs[3] with its collectives)
+    dp = world > 1 or getattr(args, "force_dp", False)
+    if dp:  # identical initial weights on every rank (DDP semantics)
         with torch.no_grad():
             for p in model.parameters():
                 dist.broadcast(p, 0)
@@ -619,7 +629,7 @@ def train_measure(args, world, rank, dev):
         out = model(x)
         loss = crit(out, y, x)
         (loss * loss_scale if f16 else loss).backward()
-        if world > 1:
+        if dp:
             # the exposed part of the overlapped all-reduce: how long the compute
             # stream waits for RCCL after the backward (HIP events)
             with nops.stage("dp.allreduce_wait"):
@@ -642,7 +652,10 @@ def train_measure(args, world, rank, dev):
     graphed = None
     dp_tags = ("dp.bn_broadcast", "dp.allreduce_wait")
     eager_elapsed, eager_steps = None, max(3, min(args.steps, 10))
-    if world == 1 and os.environ.get("NSM_GRAPH_STEP", "1") != "0":
+    # one process: the step replayed from one graph; N > 1 ranks run eager
+    # steps unless NSM_GRAPH_DP=1 (the captured DP step, collectives inside)
+    if os.environ.get("NSM_GRAPH_STEP", "1") != "0" and (
+            world == 1 or os.environ.get("NSM_GRAPH_DP", "0") == "1"):
         graphed = nsm_amd.GraphedTrainStep(model, crit, opt, x, y, loss_scale=loss_scale,
                                            warmup=1)
         for _ in range(args.warmup):
@@ -650,7 +663,10 @@ def train_measure(args, world, rank, dev):
         torch.cuda.synchronize()
         elapsed = timed(graphed, args.steps, world, dev)
         # the eager step (what an unchanged main.py and every DP rank run),
-        # timed back to back like the replays, no probes
+        # timed back to back like the replays; only the DP waits carry events
+        if dp:
+            for t in dp_tags:
+                nops.PROBES[t] = []
         eager_elapsed = timed(step, eager_steps, world, dev)
     else:
         # eager timed steps (DP ranks): only the DP waits carry HIP events
@@ -739,9 +755,10 @@ def train_measure(args, world, rank, dev):
                                + " + bwd + RCCL grad all-reduce + clip + AdamW)",
                    "global_batch": world * B, "in_ch": C, "res": [H, W],
                    "parallelism": f"dp{world}"},
+        "data_parallel": bool(dp),
         "model_tflops_per_s": round(step_flops * args.steps / elapsed / 1e12 / world, 2),
-        "world_size": dist.get_world_size() if world > 1 else 1,
-        "backend": dist.get_backend() if world > 1 else None,
+        "world_size": dist.get_world_size() if dist.is_initialized() else 1,
+        "backend": dist.get_backend() if dist.is_initialized() else None,
         "stage_cols": STAGE_COLS,
         "stages": stage_table(work, times, pipe_mult, peak, measured),
         "stage_pmc_source": measured_src,
@@ -760,7 +777,7 @@ def train_measure(args, world, rank, dev):
                         "what": "the same step run eagerly (an unchanged main.py loop; the "
                                 "per-rank step of data parallelism), back to back, weight "
                                 "gradients on the side stream"}
-    if world > 1:
+    if dp:
         res["dp"] = {"bn_broadcast_ms": round(dp_ms["dp.bn_broadcast"], 4),
                      "allreduce_wait_ms": round(dp_ms["dp.allreduce_wait"], 4),
                      "grad_bytes": 4 * sum(p.numel() for p in model.parameters()),
@@ -912,6 +929,9 @@ def main():
                     help="train: include CustomLoss's VGG19 perceptual term (customLoss.py:7-90)")
     ap.add_argument("--detail", default=None,
                     help="also write the full record (all stage rows of every config) to this file")
+    ap.add_argument("--force-dp", action="store_true",
+                    help="N=1: run the data-parallel step (BN broadcast, bucketed all-reduce) "
+                         "over a world-size-1 RCCL group, captured and eager")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU/gloo launcher check with a stand-in step (no GPU, not a measurement)")
     args = ap.parse_args()

@@ -24,21 +24,25 @@ What the graph holds fixed, and how the step stays the reference's:
     re-allocation raises.
 The constructor runs `warmup` eager steps on (x, y) to settle the caches,
 then restores parameters, AdamW moments, the tail's counters and the BN
-buffers, so building the step changes no training state. Single process only
-(the data-parallel all-reduce stays eager)."""
+buffers, so building the step changes no training state. Under data
+parallelism (`Unet.data_parallel`) the collectives are captured with the
+rest: the rank-0 BN buffer broadcast at the forward, the two gradient buckets'
+all-reduce the backward issues, and the wait for them before the tail; every
+rank must build and replay its step in lockstep, as with eager collectives."""
 import torch
 
 from ._lib import require_gpu
-from .optim import _bump
+from .optim import _bump, allreduce_grads
 
 
 class GraphedTrainStep:
     def __init__(self, model, loss_fn, optimizer, x, y, loss_scale=1.0, warmup=3,
                  range_check_every=0):
         require_gpu(x, "GraphedTrainStep input")
-        if model._grad_allreduce is not None or model._bn_broadcast is not None:
-            raise ValueError("GraphedTrainStep: single process only (the data-parallel "
-                             "all-reduce and BN broadcast run eagerly)")
+        # data parallel (Unet.data_parallel): the rank-0 BN broadcast, the
+        # bucketed gradient all-reduce the backward issues and the wait for it
+        # are captured too (RCCL kernels recorded into the graph)
+        self.dp = model._grad_allreduce is not None
         if not getattr(optimizer, "sanitize", False):
             # the plain FlatAdamW step passes its step count (AdamW's bias
             # correction) as a kernel argument, which a graph would freeze; the
@@ -69,7 +73,12 @@ class GraphedTrainStep:
     def _body(self):
         out = self.model(self.x)
         loss = self.loss_fn(out, self.y, self.x)
-        (loss * self.loss_scale if self.loss_scale != 1.0 else loss).backward()
+        # d(loss_scale * loss)/d loss seeded from a buffer filled before the
+        # capture: the same gradient as (loss * s).backward(), without the
+        # seed's fill (and the scale's multiply) launched by ATen in the graph
+        loss.backward(self._seed)
+        if self.dp:
+            allreduce_grads(self.model.parameters(), self.model._grad_allreduce[0])
         self.opt.step()
         self.opt.zero_grad(set_to_none=True)
         self.x.grad = None
@@ -85,6 +94,7 @@ class GraphedTrainStep:
 
     def _capture(self, warmup=None):
         warmup = self.warmup if warmup is None else warmup
+        self._seed = torch.full((), self.loss_scale, dtype=torch.float32, device=self.x.device)
         side = torch.cuda.Stream(device=self.x.device)
         side.wait_stream(torch.cuda.current_stream())
         saved = [t.detach().clone() for t in self._state()]
@@ -96,7 +106,10 @@ class GraphedTrainStep:
         if prep is not None:   # the range assert's sticky flag, allocated outside the capture
             prep(self.x.device)
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):   # recorded, not run
+        # thread-local capture: RCCL's watchdog thread queries events while the
+        # capture runs (a global-mode capture would fail those queries)
+        mode = "thread_local" if self.dp else "global"
+        with torch.cuda.graph(self.graph, capture_error_mode=mode):   # recorded, not run
             self.loss = self._body()
         # the warm-up steps leave no trace: the model and optimizer are as
         # they were before the constructor

@@ -220,3 +220,65 @@ def test_data_parallel_steps_match_single_process():
         for r, t in ((0, t0), (1, t1)):
             bd, be = t[s][1], emu[s][1 + r]
             assert np.abs(bd - be).max() <= 1e-4 * (1 + np.abs(be).max()), (s, r)
+
+
+def _captured_dp_worker(port, q):
+    """World-size-1 RCCL group: GraphedTrainStep over a data-parallel model
+    (BN broadcast, bucketed all-reduce and its wait captured in the graph)
+    vs the same steps run eagerly on a second model."""
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "pcss-unet_amd"), os.path.join(ROOT, "tests")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    import nsm_amd
+    from oracle.weights import make_state, synthetic_batch
+    sd0 = {k: torch.from_numpy(v.copy()) for k, v in make_state(7, 42).items()}
+
+    def build():
+        m = nsm_amd.Unet(in_ch=7, dropout_rate=0.0).to(dev).train()
+        m.load_state_dict(sd0)
+        m.data_parallel()
+        opt = nsm_amd.FlatAdamW(m.parameters(), lr=1e-3, weight_decay=1e-3, max_grad_norm=1.0,
+                                world_size=1, sanitize=True, seed=7)
+        return m, opt
+
+    x_np, y_np = synthetic_batch(2, 7, 64, 64)
+    x, y = torch.from_numpy(x_np).to(dev), torch.from_numpy(y_np).to(dev)
+    crit = nsm_amd.CustomLoss(dev, 0.9, vgg_weights=False)
+    m, opt = build()
+    step = nsm_amd.GraphedTrainStep(m, crit, opt, x, y, warmup=1)
+    graphed = [step().item() for _ in range(3)]
+    m2, opt2 = build()
+    eager = []
+    for _ in range(3):
+        opt2.zero_grad()
+        loss = crit(m2(x), y, x)
+        loss.backward()
+        nsm_amd.allreduce_grads(m2.parameters())
+        opt2.step()
+        eager.append(loss.item())
+    torch.cuda.synchronize()
+    same_flat = bool(torch.equal(opt.flat, opt2.flat))
+    same_bufs = all(torch.equal(a, b) for a, b in zip(m.buffers(), m2.buffers()))
+    same_moments = bool(torch.equal(opt.exp_avg_sq, opt2.exp_avg_sq))
+    dist.destroy_process_group()
+    q.put((graphed, eager, same_flat, same_bufs, same_moments))
+
+
+@pytest.mark.timeout(600)
+def test_captured_dp_step_equals_eager_dp_step():
+    """the data-parallel per-rank step captured as one
+    graph with its RCCL collectives (world size 1 on the test box's one GPU)
+    gives the eager DP step's results bitwise: losses, parameters, AdamW
+    moments, BN buffers over three steps."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_captured_dp_worker, args=(_free_port(), q))
+    p.start()
+    graphed, eager, same_flat, same_bufs, same_moments = q.get(timeout=500)
+    p.join(60)
+    assert p.exitcode == 0
+    assert graphed == eager, (graphed, eager)
+    assert same_flat and same_bufs and same_moments
