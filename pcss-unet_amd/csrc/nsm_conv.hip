@@ -4045,6 +4045,37 @@ static WinoWgradPlan plan_wino_wgrad_f16(long long T, int cin_p, int cout_p, int
     p.slab_floats = (size_t)nb * sp * cout_p * cin_p;
     if (sp > 1) p.slab_floats += (size_t)nb * cout_p * cin_p;
   }
+  if (force <= 0 && p.BM == 256 && p.BN == 256 && f16_wg_kt64()) {
+    // K splits by a round model of the 256x256 blocks (one per CU): rounds x
+    // (K / s x a + b) + the split sum's slab traffic c (s + 1) per tile, a, b,
+    // c fitted on the B=64 step's conv5-conv7 weight gradients (kernel traces,
+    // s = 1..8: conv6 1465 / 1299 / 1296 / 1345 us at s = 1..4, split sum
+    // included; conv5 204 at s = 8 vs 136 at s = 3). The h2 planner's ~4
+    // rounds left conv6 unsplit at 2.25 rounds and conv5 at 512-row splits
+    const long long tiles = (long long)(cout_p / 256) * (cin_p / 256) * nb, cus = cu_count();
+    const double a = 26.4e-3, b = 27.5, c = 0.0524;
+    long long best = 1;
+    double bt = 1e30;
+    for (long long s = 1; s <= 8; ++s) {
+      long long kc = (T + s - 1) / s;
+      kc = (kc + BK - 1) / BK * BK;
+      const long long se = (T + kc - 1) / kc;
+      if (se != s) continue;
+      const double t = (double)((tiles * s + cus - 1) / cus) * ((double)kc * a + b) +
+                       (s > 1 ? c * (double)(s + 1) * (double)tiles : 0.0);
+      if (t < bt) {
+        bt = t;
+        best = s;
+      }
+    }
+    long long kc = (T + best - 1) / best;
+    kc = (kc + BK - 1) / BK * BK;
+    const long long sp = (T + kc - 1) / kc;
+    p.splits = (int)sp;
+    p.kchunk = (int)kc;
+    p.slab_floats = (size_t)nb * sp * cout_p * cin_p;
+    if (sp > 1) p.slab_floats += (size_t)nb * cout_p * cin_p;
+  }
   if ((p.BM == 256 && p.BN == 256) || (p.BM == 128 && p.BN == 128)) return p;
   // (the h2 planner's smaller tiles: 128 x 128 with its ~512-block split)
   p.BM = p.BN = 128;
