@@ -1448,13 +1448,23 @@ static int sep_rmax() {
   }();
   return v;
 }
+// NSM_SEP_LDS_KB: the LDS budget of the backward's fp32 row sums per block
+// (64 KiB: two blocks per CU; 16 / 32 measured slower, B=8 fp32 step)
+static size_t sep_lds_budget() {
+  static size_t v = [] {
+    const char* e = getenv("NSM_SEP_LDS_KB");
+    return (size_t)(e ? atoi(e) : 64) * 1024;
+  }();
+  return v;
+}
 static SepPlan sep_bwd_plan(int C, int tw) {
+  const size_t budget = sep_lds_budget();
   for (int R : {4, 2}) {
     if (R > sep_rmax()) continue;
-    const int l = sep_lcb8(C, tw, R, 65536);
+    const int l = sep_lcb8(C, tw, R, budget);
     if (l >= 2 || (l >= 0 && (8 << l) == C)) return SepPlan{R, l};
   }
-  return SepPlan{1, sep_lcb8(C, tw, 1, 65536)};
+  return SepPlan{1, sep_lcb8(C, tw, 1, budget)};
 }
 // dynamic LDS above the default 64 KiB (gfx950: 160 KiB per workgroup)
 template <typename K>
@@ -1499,13 +1509,17 @@ static void dispatch_sep_bwd(const SepPlan& pl, int B, size_t lds, hipStream_t s
 // fp32 only: in bf16 (16-B lanes, half the bytes per pixel) the 2-D gather
 // forms measured faster (B=64: x2 backward 401 vs 675 us, composite forward
 // 366 vs 541 us; 1080p eval 505 vs 457 frames/s)
-static bool sep_resize() {
-  static bool v = [] {
+// (NSM_RESIZE_SEP=2: the separable forms for the 16-bit storage too; measured
+// slower again in round 6: B=64 bf16 x2 backward 516 -> 773 us at conv8)
+static int sep_resize_mode() {
+  static int v = [] {
     const char* e = getenv("NSM_RESIZE_SEP");
-    return !e || atoi(e) != 0;
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
+static bool sep_resize() { return sep_resize_mode() != 0; }
+static bool sep_for(int dtype) { return dtype == NSM_F32 ? sep_resize() : sep_resize_mode() == 2; }
 
 // ---------------------------------------------------------------------------
 // Model boundary: pixel_unshuffle(2) + NCHW->NHWC (+ zero channel pad), and its
@@ -2284,7 +2298,7 @@ static int resize_bwd(const void* dy, int B, int Hi, int Wi, int C, void* dx, in
     const size_t slds = pl.lcb8 < 0 ? 0
                                     : (size_t)pl.R * Wo * (8 << pl.lcb8) * 4 +
                                           (size_t)Wi * (RS_W + 2) * 4;
-    if (sep_resize() && dtype == NSM_F32 && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * Hi < (1ll << 31)) {
+    if (sep_for(dtype) && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * Hi < (1ll << 31)) {
       dispatch_sep_bwd<false>(pl, B, slds, s, dy, Hi, Wi, C, dx, Ho, Wo, sh, sw, 0.f, 0.f, rp,
                               dtype);
     } else if (Wi <= U2_MAXW && (long long)B * Hi < (1ll << 31) && rows_resize()) {
@@ -2376,7 +2390,7 @@ extern "C" int nsm_up2_resize_fwd_act(const void* y2, int B, int h, int w, int C
   const ActSrc act{scale, shift, res, slope};
   const int lcb8 = sep_lcb8(C, w);
   const size_t slds = lcb8 < 0 ? 0 : (size_t)w * (8 << lcb8) * 4 + (size_t)tw * 16;
-  if (sep_resize() && dtype == NSM_F32 && lcb8 >= 0 && slds <= 65536) {
+  if (sep_for(dtype) && lcb8 >= 0 && slds <= 65536) {
     const dim3 gs((unsigned)rows, (unsigned)(C / (8 << lcb8)));
     if (dtype == NSM_BF16)
       hipLaunchKernelGGL((up2_resize_fwd_sep_kernel<bf16_t, true>), gs, dim3(256), slds, s,
@@ -2427,7 +2441,7 @@ extern "C" int nsm_up2_resize_fwd(const void* x, int B, int h, int w, int C, voi
     const dim3 gr((unsigned)rows, (unsigned)segs);
     const int lcb8 = sep_lcb8(C, w);
     const size_t slds = lcb8 < 0 ? 0 : (size_t)w * (8 << lcb8) * 4 + (size_t)tw * 16;
-    if (sep_resize() && dtype == NSM_F32 && lcb8 >= 0 && slds <= 65536) {
+    if (sep_for(dtype) && lcb8 >= 0 && slds <= 65536) {
       const dim3 gs((unsigned)rows, (unsigned)(C / (8 << lcb8)));
 #define A_(T) NSM_CT(T, x), h, w, C, lcb8, NSM_T(T, y), th, tw, a, b, c, d
       if (dtype == NSM_BF16)
@@ -2472,7 +2486,7 @@ static int up2_resize_bwd(const void* dy, int B, int h, int w, int C, void* dx, 
   const size_t slds = pl.lcb8 < 0 ? 0
                                   : (size_t)pl.R * tw * (8 << pl.lcb8) * 4 +
                                         (size_t)w * (RS_W + 2) * 4;
-  if (sep_resize() && dtype == NSM_F32 && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * h < (1ll << 31)) {
+  if (sep_for(dtype) && pl.lcb8 >= 0 && slds <= 96 * 1024 && (long long)B * h < (1ll << 31)) {
     dispatch_sep_bwd<true>(pl, B, slds, s, dy, h, w, C, dx, th, tw, a, b, c, d, rp, dtype);
   } else if (w <= U2_MAXW && (long long)B * h < (1ll << 31)) {
     NSM_CHECK_ARG(!rp || 256 % (C / 8) == 0, "up2_resize_bwd: fused BN reduction needs C/8 | 256");

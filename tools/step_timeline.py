@@ -4,6 +4,7 @@ the AdamW kernel): duration, grid (blocks), short name; then totals per kernel
 family. usage: python tools/step_timeline.py TRACE_CSV|RESULTS_DB [step_index_from_end=1]
 (RESULTS_DB: the rocpd sqlite file rocprofv3 writes without --output-format csv)"""
 import collections
+import os
 import csv
 import re
 import sys
@@ -34,7 +35,7 @@ for r in rows[a:b]:
     n = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "").replace("nsm::", "")
     g = (int(r["Grid_Size_X"]) // int(r["Workgroup_Size_X"]), int(r["Grid_Size_Y"]) //
          int(r["Workgroup_Size_Y"]), int(r["Grid_Size_Z"]) // int(r["Workgroup_Size_Z"]))
-    print(f"{d:8.1f} {str(g):18s} {n[:110]}")
+    print(f"{d:8.1f} {str(g):18s} {n[:int(os.environ.get('STL_NAMELEN', 110))]}")
     fam[re.sub(r"<.*", "", n)] += d
 span = (int(rows[b - 1]["End_Timestamp"]) - int(rows[a]["Start_Timestamp"])) / 1e3
 print(f"\nkernels {tot:.0f} us, span {span:.0f} us, launches {b - a}")
