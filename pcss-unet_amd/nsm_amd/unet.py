@@ -133,6 +133,15 @@ GRAD_BNRED = os.environ.get("NSM_GRAD_BNRED", "1") != "0"
 # their order between the marker launches)
 WGRAD_STREAM = (os.environ.get("NSM_WGRAD_STREAM", "1") != "0"
                 and os.environ.get("NSM_STAGE_MARKS", "0") == "0")
+# NSM_WGRAD_GRAPH_F32 (default 0): the side stream also inside a captured fp32
+# step (GraphedTrainStep). Round 6, interleaved A/B on one box (3 rounds): fp32
+# B=8 graph replay 753.2 / 755.0 / 756.3 frames/s without it vs 741.9 / 743.2 /
+# 745.5 with it (the graph runs the weight-gradient branch concurrently and the
+# co-scheduled kernels slow each other more than they gain), while the eager
+# fp32 step gains from it (742.5-745.8 vs 728.3-733.1: it hides the host's
+# launch gaps) and the bf16 B=64 step gains either way (graph 1627.9-1644.4 vs
+# 1614.1-1629.4)
+GRAPH_SIDE_F32 = int(os.environ.get("NSM_WGRAD_GRAPH_F32", "0"))
 # NSM_WGRAD_PRIO: the side stream's priority (torch.cuda.Stream priority: lower
 # numbers run first; 0 = the default streams')
 WGRAD_PRIO = int(os.environ.get("NSM_WGRAD_PRIO", "0"))
@@ -1168,7 +1177,8 @@ class _UnetFn(torch.autograd.Function):
         split = offset_of.get(id(mod.conv6.conv[0].weight)) if dp is not None else None
         global _wg_stream
         side = None
-        if WGRAD_STREAM:
+        if WGRAD_STREAM and not (GRAPH_SIDE_F32 == 0 and torch.cuda.is_current_stream_capturing()
+                                 and ctx.saved_blocks[2].Y1.dtype == torch.float32):
             side = _wg_streams.get(dev)
             if side is None:
                 side = _wg_streams[dev] = torch.cuda.Stream(device=dev, priority=WGRAD_PRIO)
