@@ -4,7 +4,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 T="tests/test_gpu_configs.py::test_configs2_b64_bf16_small_res_vs_oracle[spread]"
-for v in "X=1" "NSM_BF16_M16=0" "NSM_WGRAD_F16=0" "NSM_LAZY_DY1_F16=0" "NSM_BF16_WINO=0" "NSM_BF16_DUAL=0"; do
+for v in ${DIAG_VARIANTS:-"X=1" "NSM_BF16_M16=0" "NSM_BF16_WINO=0"}; do
   env $v timeout -k 10 300 python -u -m pytest "$T" -m gpu -x -q -s --timeout 250 --timeout-method thread > gpurun_out/diag16.log 2>&1
   rc=$?
   echo "== $v rc=$rc"
