@@ -35,6 +35,18 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "pcss-unet_amd"))
 sys.path.insert(0, ROOT)
+# Eager data-parallel ranks (N > 1 without NSM_GRAPH_DP): 8 hardware queues.
+# HIP binds each stream, at its first launch, to the least used of at most
+# GPU_MAX_HW_QUEUES queues (its default: 4); RCCL's and ProcessGroupNCCL's
+# streams take three, and the Unet backward's weight-gradient side stream then
+# shared the default stream's queue and ran serialised with it (round 6 kernel
+# trace). fp32 B=8 eager DP at world size 1: 694 frames/s at 4 queues, 728-729
+# at 8 (753.9 without DP); bf16 B=64 eager unchanged. Not for the captured
+# step: the bf16 B=64 graph drops from 1639-1641 to 1480-1491 at 8 queues (its
+# weight-gradient branch then truly runs beside the critical path, whose GEMMs
+# are sized for the whole chip). Set before torch initialises HIP.
+if int(os.environ.get("WORLD_SIZE", "1")) > 1 and os.environ.get("NSM_GRAPH_DP", "0") != "1":
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -126,9 +126,9 @@ GRAD_BNRED = os.environ.get("NSM_GRAD_BNRED", "1") != "0"
 # The weight-gradient launches of the Unet backward (GEMM, split reduce,
 # Winograd weight-gradient output) run on a second stream: nothing on the
 # input-gradient path reads them, so they fill its latency-bound launches and
-# kernel tails. Under data parallelism the main stream joins the side stream
-# before each gradient bucket's all-reduce is queued; NSM_WGRAD_STREAM=0 keeps
-# one stream
+# kernel tails. Under data parallelism each gradient bucket's all-reduce is
+# issued from the side stream once it has caught up with the main one
+# (_allreduce_bucket); NSM_WGRAD_STREAM=0 keeps one stream
 # (also off under NSM_STAGE_MARKS: the per-stage counters attribute kernels by
 # their order between the marker launches)
 WGRAD_STREAM = (os.environ.get("NSM_WGRAD_STREAM", "1") != "0"
@@ -165,13 +165,22 @@ WGRAD_HOLD_BYTES = int(float(os.environ.get("NSM_WGRAD_HOLD_GB", "8")) * (1 << 3
 _wg_hold = []
 
 
-def _join_wgrad():
-    """The current stream waits for the weight gradients queued so far; the
-    tensors they read are released (the allocator reuses their memory on the
-    current stream, now ordered after those reads)."""
-    if _wg_stream is not None:
-        torch.cuda.current_stream().wait_stream(_wg_stream)
-    _wg_hold.clear()
+def _allreduce_bucket(flat, lo, hi, group):
+    """Start the bucket's gradient all-reduce once both the current stream's
+    work so far (biases, BN parameters) and the weight gradients queued on the
+    side stream are done, WITHOUT making the current stream wait: the call is
+    issued from the side stream after it has waited for the current one, so
+    RCCL's stream waits on the side stream only and the encoder backward goes
+    on (a join of the current stream here held it until the decoder's weight
+    gradients were done). The eager DP step's remaining gap to the step without
+    DP was the hardware-queue binding, not this (bench.py GPU_MAX_HW_QUEUES)."""
+    side = _wg_stream
+    if side is None:
+        optim.allreduce_async(flat, lo, hi, group)
+        return
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        optim.allreduce_async(flat, lo, hi, group)
 
 
 def _wgrad(fn, *reads):
@@ -1223,8 +1232,7 @@ class _UnetFn(torch.autograd.Function):
                 skip_grad[SKIP_OF[k - 1]] = dprev
             G = dprev
         if split is not None:   # conv6..conv10 grads are final: overlap their all-reduce
-            _join_wgrad()
-            optim.allreduce_async(flat, split, total, dp[0])
+            _allreduce_bucket(flat, split, total, dp[0])
         # encoder: G is now d c5
         need_x = ctx.needs_input_grad[0]
         for k in (5, 4, 3, 2):
@@ -1252,8 +1260,7 @@ class _UnetFn(torch.autograd.Function):
                 G = dX
             st.__exit__(None, None, None)
         if split is not None:
-            _join_wgrad()
-            optim.allreduce_async(flat, 0, split, dp[0])
+            _allreduce_bucket(flat, 0, split, dp[0])
         dx = None
         if need_x:
             dx = ops.input_grad(G, B, C, H, W)
