@@ -637,10 +637,15 @@ def train_measure(args, world, rank, dev):
     x = torch.randn(B, C, H, W, device=dev, generator=g).requires_grad_(True)
     y = (torch.randint(0, 256, (B, 1, H, W), device=dev, generator=g).float() / 255.0)
 
+    # the backward's seed gradient (the f16 loss scale, else 1), allocated once
+    # as GraphedTrainStep does: loss.backward() would fill a fresh ones tensor
+    # with an ATen kernel every step (and f16's loss * scale another)
+    seed = torch.full((), loss_scale, dtype=torch.float32, device=dev)
+
     def step():
         out = model(x)
         loss = crit(out, y, x)
-        (loss * loss_scale if f16 else loss).backward()
+        loss.backward(seed)
         if dp:
             # the exposed part of the overlapped all-reduce: how long the compute
             # stream waits for RCCL after the backward (HIP events)

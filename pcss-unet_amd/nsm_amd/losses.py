@@ -100,8 +100,10 @@ class _RangeCheck:
             return
         if self.event.query():
             self._raise_if_set()
-        call("nsm_range_flag", ptr(o), o.numel(), 0.0, 1.0, ptr(self.flag), stream())
-        self.host.copy_(self.flag, non_blocking=True)
+        # eager: the kernel stores the sticky 1 straight into the pinned host
+        # word (mapped into the device's address space; it only ever writes 1),
+        # so no device-to-host copy is queued; the event orders the host's read
+        call("nsm_range_flag", ptr(o), o.numel(), 0.0, 1.0, ptr(self.host), stream())
         self.event.record()
 
     def check(self):

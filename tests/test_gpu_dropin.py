@@ -3,7 +3,7 @@
   * the `assert output.min() >= 0 and output.max() <= 1` of CustomLoss
     (customLoss.py:131) and EnhancedCustomLoss (pert_loss.py:131): a device flag
     here; an out-of-range or NaN output raises AssertionError at the next call
-    once the flag's copy has landed, and at once via check_range_now();
+    once the flag has landed in host memory, and at once via check_range_now();
   * the VGG19 perceptual loss built from a torchvision-layout checkpoint file
     (customLoss.py:20: `models.vgg19(weights=IMAGENET1K_V1)`; here a local .pth
     loaded with weights_only=True) equals the module built from the same
