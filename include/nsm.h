@@ -366,12 +366,15 @@ int nsm_wino_output(const float* Mb, int B, int H, int W, int cout_p, int tile, 
 /* nsm_wino_output that also emits the BatchNorm batch statistics of y
  * (Unetmodel.py:21-22, the BN after a Winograd 3x3 conv) as counted partials
  * partial[nslot][3][cout_p] = {sum, M2, count}. nslot: a multiple of
- * 256 / gcd(cout_p / (tile == 6 ? 1 : 4), 256); nsm_wino_stat_slots gives the
- * tuned count (0 there: the separate nsm_bn_stats pass is faster). */
+ * nsm_wino_stat_step(cout_p, tile) = 256 / gcd(cout_p / channels per thread,
+ * 256) (4 channels per thread for F(2x2) / F(4x4), 2 for F(6x6); 1 with
+ * NSM_F6_OUT_CW=1); nsm_wino_stat_slots gives the tuned count (0 there: the
+ * separate nsm_bn_stats pass is faster). */
 int nsm_wino_output_stats(const float* Mb, int B, int H, int W, int cout_p, int tile,
                           const float* bias, float* y, int ldy, float* partial, int nslot,
                           void* stream);
 int nsm_wino_stat_slots(int B, int H, int W, int cout_p, int tile);
+int nsm_wino_stat_step(int cout_p, int tile);
 
 /* Winograd weight gradient of the same 3x3 conv: dw[co][ci][3][3] (reference
  * layout, real dims) from dy [pixels][cout_p] and the forward's transformed

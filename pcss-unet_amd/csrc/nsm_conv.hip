@@ -1542,7 +1542,8 @@ struct WinoM16 {
 // BFO (the bf16 path, nsm_wino_output_bf16): y holds bf16; the BN partials are
 // of the bf16-rounded outputs, as the direct bf16 convolution's epilogue
 // CWX: channels per thread (0: WinoVec<MT>::W; 2: the bf16 path's f16-M form
-// at half the accumulator registers, BfLane's reason)
+// at half the accumulator registers, BfLane's reason, or fp32 F(6x6): 8-B
+// loads of M instead of 4-B ones, f6_out_cw)
 template <int MT, bool STATS, bool ACT = false, bool BFO = false, bool M16 = false, int CWX = 0>
 __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restrict__ Mb, int N, int H,
                                                           int W, int TH, int TW, long long T,
@@ -1553,7 +1554,8 @@ __global__ void __launch_bounds__(256) wino_output_kernel(const float* __restric
                                                           WinoM16 m16 = WinoM16{}) {
   constexpr int A = MT + 2, CW = CWX ? CWX : WinoVec<MT>::W;
   using VT = std::conditional_t<CW == 2, f32x2, typename WinoVec<MT>::T>;
-  static_assert(CWX == 0 || (BFO && M16 && (CW == 2 || CW == 4)), "CWX: the f16-M bf16 form");
+  static_assert(CWX == 0 || (BFO && M16 && (CW == 2 || CW == 4)) || (MT == 6 && CWX == 2 && !BFO && !M16),
+                "CWX: the f16-M bf16 form, or fp32 F(6x6) at 2 channels per thread");
   static_assert(!M16 || (BFO && (CW == 4 || CW == 2)), "f16 M: the bf16 path's F(4x4)");
   int ev = 0, eu = 0;  // every lane reads the scale slots (wave reduction) before the loop
   if constexpr (M16) {
@@ -2765,8 +2767,21 @@ extern "C" int nsm_wino_gemm_s(const float* V, const float* U, int B, int H, int
 // wino_stat_step). The policy: ~1024 blocks, and 0 (= separate bn_stats pass)
 // under 2 tiles per thread, where the grid-stride form loses more parallelism
 // than the extra pass costs (measured: conv3-conv5 slower, conv6 even).
+// NSM_F6_OUT_CW: channels per thread of the fp32 F(6x6) output transform. 2
+// (default): 8-B loads of M — a wave's 64 plane reads carry 512 B each instead
+// of 256 B (tools/ubench/plane_read.hip: the 64-plane read of the transform at
+// 3.84 TB/s with 4-B lanes, 5.69 with 8-B ones); 1: one channel per thread
+static int f6_out_cw() {
+  static int v = [] {
+    const char* e = getenv("NSM_F6_OUT_CW");
+    return (e && atoi(e) == 1) ? 1 : 2;
+  }();
+  return v;
+}
+static int wino_out_cw(int tile) { return tile == 6 ? f6_out_cw() : 4; }
+
 static int wino_stat_step(int cout_p, int tile) {
-  int a = cout_p / (tile == 6 ? 1 : 4), b = 256;
+  int a = cout_p / wino_out_cw(tile), b = 256;
   while (b) {
     const int r = a % b;
     a = b;
@@ -2785,7 +2800,9 @@ static int wino_stat_resident(int tile) {
   hipError_t e = hipGetDevice(&dev);
   if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
   if (e == hipSuccess) {
-    const void* k = tile == 6   ? (const void*)wino_output_kernel<6, true>
+    const void* k = tile == 6   ? (f6_out_cw() == 2
+                                       ? (const void*)wino_output_kernel<6, true, false, false, false, 2>
+                                       : (const void*)wino_output_kernel<6, true>)
                     : tile == 4 ? (const void*)wino_output_kernel<4, true>
                                 : (const void*)wino_output_kernel<2, true>;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k, 256, 0);
@@ -2794,10 +2811,11 @@ static int wino_stat_resident(int tile) {
   return cache[tile];
 }
 static long long wino_stat_slots(long long T, int cout_p, int tile) {
-  const int N4 = cout_p / (tile == 6 ? 1 : 4), step = wino_stat_step(cout_p, tile);
+  const int N4 = cout_p / wino_out_cw(tile), step = wino_stat_step(cout_p, tile);
   // the policy (stats form where a thread covers >= 2 tiles) is judged on
-  // ~1024 blocks; the grid itself is one resident round
-  long long ns = (1024ll * 256) / N4;
+  // ~1024 blocks of one channel per thread for F(6x6) (its decisions as
+  // before the 2-channel form); the grid itself is one resident round
+  long long ns = (1024ll * 256) / (cout_p / (tile == 6 ? 1 : 4));
   if (ns < 512) ns = 512;
   ns = ns / step * step;
   if (ns < step) ns = step;
@@ -2808,25 +2826,38 @@ static long long wino_stat_slots(long long T, int cout_p, int tile) {
   return ns;
 }
 
+extern "C" int nsm_wino_stat_step(int cout_p, int tile) {
+  if (cout_p <= 0 || cout_p % 32 != 0 || (tile != 2 && tile != 4 && tile != 6)) return 0;
+  return wino_stat_step(cout_p, tile);
+}
+
 extern "C" int nsm_wino_stat_slots(int B, int H, int W, int cout_p, int tile) {
   WinoGeom g;
   if (!wino_geom(tile, B, H, W, g) || cout_p % 32 != 0) return 0;
   return (int)wino_stat_slots(g.T, cout_p, tile);
 }
 
-template <int MT>
+template <int MT, int CWX = 0>
 static void launch_wino_output(dim3 grid, hipStream_t s, const float* Mb, int cout_p, int H, int W,
                                const WinoGeom& g, const float* bias, float* y, int ldy,
                                float* partial, const WinoAct* act = nullptr) {
   if (act)
-    hipLaunchKernelGGL((wino_output_kernel<MT, false, true>), grid, dim3(256), 0, s, Mb, cout_p, H,
-                       W, g.TH, g.TW, g.T, bias, y, ldy, nullptr, *act);
+    hipLaunchKernelGGL((wino_output_kernel<MT, false, true, false, false, CWX>), grid, dim3(256), 0, s,
+                       Mb, cout_p, H, W, g.TH, g.TW, g.T, bias, y, ldy, nullptr, *act);
   else if (partial)
-    hipLaunchKernelGGL((wino_output_kernel<MT, true>), grid, dim3(256), 0, s, Mb, cout_p, H, W,
-                       g.TH, g.TW, g.T, bias, y, ldy, partial);
+    hipLaunchKernelGGL((wino_output_kernel<MT, true, false, false, false, CWX>), grid, dim3(256), 0, s,
+                       Mb, cout_p, H, W, g.TH, g.TW, g.T, bias, y, ldy, partial);
   else
-    hipLaunchKernelGGL((wino_output_kernel<MT, false>), grid, dim3(256), 0, s, Mb, cout_p, H, W,
-                       g.TH, g.TW, g.T, bias, y, ldy, partial);
+    hipLaunchKernelGGL((wino_output_kernel<MT, false, false, false, false, CWX>), grid, dim3(256), 0, s,
+                       Mb, cout_p, H, W, g.TH, g.TW, g.T, bias, y, ldy, partial);
+}
+static void launch_wino_output6(dim3 grid, hipStream_t s, const float* Mb, int cout_p, int H, int W,
+                                const WinoGeom& g, const float* bias, float* y, int ldy,
+                                float* partial, const WinoAct* act = nullptr) {
+  if (f6_out_cw() == 2)
+    launch_wino_output<6, 2>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial, act);
+  else
+    launch_wino_output<6>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial, act);
 }
 
 extern "C" int nsm_wino_output_stats(const float* Mb, int B, int H, int W, int cout_p, int tile,
@@ -2835,7 +2866,7 @@ extern "C" int nsm_wino_output_stats(const float* Mb, int B, int H, int W, int c
   NSM_CHECK_ARG(Mb && y && cout_p % 32 == 0 && ldy % 4 == 0, "wino_output: bad args");
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output: bad tile or shape");
-  const int N4 = cout_p / (tile == 6 ? 1 : 4);
+  const int N4 = cout_p / wino_out_cw(tile);
   dim3 grid(grid_1d(g.T * N4));
   if (partial) {
     NSM_CHECK_ARG(nslot > 0 && nslot % wino_stat_step(cout_p, tile) == 0 && nslot <= (1 << 20),
@@ -2846,7 +2877,7 @@ extern "C" int nsm_wino_output_stats(const float* Mb, int B, int H, int W, int c
   hipStream_t s = as_stream(stream);
   if (tile == 2) launch_wino_output<2>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
   else if (tile == 4) launch_wino_output<4>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
-  else launch_wino_output<6>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
+  else launch_wino_output6(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial);
   NSM_LAUNCH_CHECK("wino_output");
   return 0;
 }
@@ -2861,11 +2892,11 @@ extern "C" int nsm_wino_output_act(const float* Mb, int B, int H, int W, int cou
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_act: bad tile or shape");
   const WinoAct act{act_scale, act_shift, slope, res, ldres};
-  dim3 grid(grid_1d(g.T * (cout_p / (tile == 6 ? 1 : 4))));
+  dim3 grid(grid_1d(g.T * (cout_p / wino_out_cw(tile))));
   hipStream_t s = as_stream(stream);
   if (tile == 2) launch_wino_output<2>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, nullptr, &act);
   else if (tile == 4) launch_wino_output<4>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, nullptr, &act);
-  else launch_wino_output<6>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, nullptr, &act);
+  else launch_wino_output6(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, nullptr, &act);
   NSM_LAUNCH_CHECK("wino_output_act");
   return 0;
 }

@@ -104,6 +104,7 @@ _SIGS = {
     "nsm_wino_input_resize": (I, [P, I, I, I, I, I, I, I, I, I, P, P, P]),
     "nsm_wino_output_stats": (I, [P, I, I, I, I, I, P, P, I, P, I, P]),
     "nsm_wino_stat_slots": (I, [I, I, I, I, I]),
+    "nsm_wino_stat_step": (I, [I, I]),
     "nsm_conv1x1_bnbwd_chunks": (I, [I, I, I, I, I, I]),
     "nsm_conv1x1_dgrad_bnbwd": (I, [P, I, I, I, I, I, P, I, P, I, P, P, P, P, P, F, I, P, P, P, I,
                                     I, P, P, P, P]),

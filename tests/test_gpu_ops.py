@@ -187,7 +187,8 @@ def test_wino_output_bn_stats(ops, device, B, H, W, ci, co, tile):
     w = torch.randn(co, ci, 3, 3, generator=g) / (ci * 9) ** 0.5
     b = torch.randn(co, generator=g) * 2 + 1  # a large mean, as a pre-BN conv output has
     U = ops.wino_weight(w.to(device), co, ci, flip=False, tile=tile)
-    step = 256 // math.gcd(co // (1 if tile == 6 else 4), 256)
+    step = int(lib.nsm_wino_stat_step(co, tile))   # from the library's channels per thread
+    assert step > 0
     tuned = int(lib.nsm_wino_stat_slots(B, H, W, co, tile))
     if (B, H, W) == (8, 256, 256):
         assert tuned > 1024  # conv8 / conv9 geometry: the stats form with a merge
