@@ -3474,6 +3474,19 @@ static int f16_tx_cw() {
   }();
   return v;
 }
+// NSM_F16_OUT_CW: channels per thread of the training step's f16-M output
+// transform alone (4, default: M read as 8-B words; 2: as 4-B ones).
+// Interleaved A/B (bf16 B=64 kernel traces, two rounds): the step's output
+// transforms 2818 / 2818 -> 2397 / 2401 us, bench 1637.8 / 1619.2 -> 1643.7 /
+// 1632.7 frames/s — the 8-B reads outweigh the halved occupancy here, unlike
+// the input and dual transforms (NSM_F16_TX_CW)
+static int f16_out_cw() {
+  static int v = [] {
+    const char* e = getenv("NSM_F16_OUT_CW");
+    return (e && atoi(e) == 2) ? 2 : 4;
+  }();
+  return v;
+}
 
 // V [alpha^2][T][C] f16 = s B^T d B of the bf16 NHWC input x (zero padding), 4
 // channels per thread, the column pass streamed over the patch rows
@@ -3695,7 +3708,7 @@ extern "C" int nsm_wino_output_bf16m(const void* M16, const int* m16e, int B, in
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_output_bf16m: bad shape");
   // (the partial slots: nslot x N channels whatever the width; the grid's
   // threads, nslot x N / cw, each keep one channel group)
-  const int cw = f16_tx_cw();
+  const int cw = f16_out_cw();
   dim3 grid(grid_1d(g.T * (cout_p / cw)));
   if (partial) {
     NSM_CHECK_ARG(nslot > 0 && nslot % wino_stat_step(cout_p, tile) == 0 && nslot <= (1 << 20),
