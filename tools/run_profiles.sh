@@ -62,4 +62,4 @@ if [ "$WHICH" != f32 ]; then
       "$OUT/rdreq_b64_bf16.csv" "$OUT/fetch_b64_bf16.csv" "$OUT/write_b64_bf16.csv"
 fi
 mkdir -p "$OUT/profiles_copy"
-cp profiles/$R/* "$OUT/profiles_copy/"
+cp -r profiles/$R/* "$OUT/profiles_copy/"
