@@ -3628,6 +3628,114 @@ __global__ void __launch_bounds__(256) wino_input_f16_up_kernel(
   }
 }
 
+// wino_input_f16_up_kernel at 2 channels per thread on 32-bit buffer offsets
+// (host-checked: x under 2 GiB, all of V under 4 GiB, T x C / 2 under 2^31):
+// the source taps' column offsets are formed once per tile, a source row adds
+// one offset, and V is stored through one descriptor, the plane in the scalar
+// offset and the thread's in-plane offset in the vector one — the 64-bit
+// address arithmetic of ~150 global loads and 36 stores per tile (the kernel
+// is VALU-bound: 78 % VALU-busy SIMDs at B=64) is gone. Same values, bits and
+// order as the generic kernel.
+template <int MT>
+__global__ void __launch_bounds__(256) wino_input_f16_up_buf_kernel(
+    const bf16_t* __restrict__ x, int ld, int hi, int wi, float sh, float sw, int H, int W, int C,
+    int TH, int TW, int T, bf16_t* __restrict__ V, H2Scale hsc) {
+  constexpr int A = MT + 2;
+  using L = BfLane<2>;
+  using LV = L::V;
+  const int C4 = C / 2;
+  const int total = T * C4;
+  const float hs = exp2i(h2_exp(hsc));  // every lane (amax_read: a wave reduction)
+  const int nb = T / (TH * TW);
+  const __amdgpu_buffer_rsrc_t xr = make_rsrc_b(x, (long long)nb * hi * wi * ld);
+  // all of V through one descriptor (4 GiB range: host-checked under it), the
+  // plane in the scalar offset
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, -1, 0x00020000);
+  const uint32_t pbytes = (uint32_t)T * (uint32_t)C * 2u;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = (i % C4) * 2;
+    const int t = i / C4;
+    const int tx = t % TW;
+    const int r = t / TW;
+    const int ty = r % TH;
+    const int b = r / TH;
+    uint32_t o0[A], o1[A];  // byte offsets of the taps' source columns (+ channel)
+    float lx0[A], lx1[A];
+#pragma unroll
+    for (int e = 0; e < A; ++e) {
+      int x0, x1;
+      lin_idx(sw, min(max(MT * tx - 1 + e, 0), W - 1), wi, x0, x1, lx0[e], lx1[e]);
+      o0[e] = (uint32_t)(x0 * ld + c) * 2u;
+      o1[e] = (uint32_t)(x1 * ld + c) * 2u;
+    }
+    auto src_row = [&](int y, LV(&h)[A]) {
+      const uint32_t ro = (uint32_t)((b * hi + y) * wi) * (uint32_t)ld * 2u;
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(xr, ro + o0[e], 0, 0);
+        const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(xr, ro + o1[e], 0, 0);
+        h[e] = lx0[e] * L::cvt(w0) + lx1[e] * L::cvt(w1);
+      }
+    };
+    LV h0[A], h1[A];
+    int ya = -1, yb = -1;  // source rows held in h0, h1
+    LV sc[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      const int yy = MT * ty - 1 + a;
+      int y0, y1;
+      float ly0, ly1;
+      lin_idx(sh, min(max(yy, 0), H - 1), hi, y0, y1, ly0, ly1);
+      if (y0 != ya) {
+        if (y0 == yb) {
+#pragma unroll
+          for (int e = 0; e < A; ++e) h0[e] = h1[e];
+        } else {
+          src_row(y0, h0);
+        }
+        ya = y0;
+      }
+      if (y1 != yb) {
+        if (y1 == ya) {
+#pragma unroll
+          for (int e = 0; e < A; ++e) h1[e] = h0[e];
+        } else {
+          src_row(y1, h1);
+        }
+        yb = y1;
+      }
+      const bool rin = (unsigned)yy < (unsigned)H;
+      LV d[A];
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const bool in = rin && (unsigned)(MT * tx - 1 + e) < (unsigned)W;
+        const LV v = ly0 * h0[e] + ly1 * h1[e];
+        d[e] = in ? L::rbf(v) : LV{};
+      }
+      wcol_row<CBt<MT>>(sc, d, a);
+    }
+    const uint32_t vo = (uint32_t)(t * C + c) * 2u;
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      LV v[A];
+      wmat<CBt<MT>>(sc[a], v);
+#pragma unroll
+      for (int e = 0; e < A; ++e)  // plane a A + e at the (uniform) scalar offset
+        __builtin_amdgcn_raw_buffer_store_b32(pack_h2(v[e] * hs), vr, vo,
+                                              (int)((uint32_t)(a * A + e) * pbytes), 0);
+    }
+  }
+}
+
+// NSM_F16_UP_BUF=0: the generic kernel for the bf16 x2-upsample input transform
+static bool f16_up_buf() {
+  static bool v = [] {
+    const char* e = getenv("NSM_F16_UP_BUF");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 extern "C" int nsm_wino_input_f16_resize(const void* x, int ldx, int B, int hi, int wi, int H, int W,
                                          int cin_p, int tile, void* V, const uint32_t* amax_x,
                                          void* stream) {
@@ -3638,6 +3746,15 @@ extern "C" int nsm_wino_input_f16_resize(const void* x, int ldx, int B, int hi, 
   WinoGeom g;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, g), "wino_input_f16_resize: bad shape");
   const int cw = f16_tx_cw();
+  const long long xbytes = (long long)B * hi * wi * ldx * 2, vbytes = 36ll * g.T * cin_p * 2;
+  if (cw == 2 && f16_up_buf() && xbytes < 0x7FFFFFFFll && vbytes < 0xFFFFFFFFll &&
+      g.T * (cin_p / 2) < (1ll << 31)) {
+    hipLaunchKernelGGL(wino_input_f16_up_buf_kernel<4>, dim3(grid_1d(g.T * cin_p / 2)), dim3(256), 0,
+                       as_stream(stream), (const bf16_t*)x, ldx, hi, wi, ac_scale(hi, H), ac_scale(wi, W),
+                       H, W, cin_p, g.TH, g.TW, (int)g.T, (bf16_t*)V, H2Scale{amax_x, wino_beta(4, 0)});
+    NSM_LAUNCH_CHECK("wino_input_f16_resize");
+    return 0;
+  }
   hipLaunchKernelGGL((cw == 2 ? wino_input_f16_up_kernel<4, 2> : wino_input_f16_up_kernel<4, 4>),
                      dim3(grid_1d(g.T * cin_p / cw)), dim3(256), 0, as_stream(stream),
                      (const bf16_t*)x, ldx, hi, wi, ac_scale(hi, H), ac_scale(wi, W), H, W, cin_p,
