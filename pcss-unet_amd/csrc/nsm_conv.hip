@@ -3727,7 +3727,8 @@ __global__ void __launch_bounds__(256) wino_input_f16_up_buf_kernel(
   }
 }
 
-// NSM_F16_UP_BUF=0: the generic kernel for the bf16 x2-upsample input transform
+// NSM_F16_UP_BUF=0: the generic kernels for the bf16 x2-upsample input
+// transform and the lazy dual transform (their buffer-offset forms otherwise)
 static bool f16_up_buf() {
   static bool v = [] {
     const char* e = getenv("NSM_F16_UP_BUF");
@@ -4164,6 +4165,106 @@ __global__ void __launch_bounds__(256) wino_dual_bn_f16_kernel(
   }
 }
 
+// wino_dual_bn_f16_kernel at 2 channels per thread on 32-bit buffer offsets
+// (host-checked: g and y under 2 GiB, V and dM under 4 GiB, T x C / 2 under
+// 2^31): the patch's 72 loads add a per-pixel offset to one descriptor each,
+// the 72 stores put the plane in the scalar offset of one descriptor per
+// output (as wino_input_f16_up_buf_kernel). Same values and bits as the
+// generic kernel.
+template <int MT>
+__global__ void __launch_bounds__(256) wino_dual_bn_f16_buf_kernel(
+    const bf16_t* __restrict__ g, int ldg, const bf16_t* __restrict__ y, int ldy, int H, int W, int C,
+    int TH, int TW, int T, const float* __restrict__ scale, const float* __restrict__ shift,
+    float slope, const float* __restrict__ mask, const float* __restrict__ mean,
+    const float* __restrict__ coef, bf16_t* __restrict__ V, bf16_t* __restrict__ dM, H2Scale hv,
+    H2Scale hd) {
+  constexpr int A = MT + 2;
+  using L = BfLane<2>;
+  using LV = L::V;
+  const int C4 = C / 2;
+  const int total = T * C4;
+  const float sv = exp2i(h2_exp(hv)), sd = exp2i(h2_exp(hd));  // every lane
+  const int nb = T / (TH * TW);
+  const __amdgpu_buffer_rsrc_t gr = make_rsrc_b(g, (long long)nb * H * W * ldg);
+  const __amdgpu_buffer_rsrc_t yr_ = make_rsrc_b(y, (long long)nb * H * W * ldy);
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc((void*)V, (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)dM, (short)0, -1, 0x00020000);
+  const uint32_t pbytes = (uint32_t)T * (uint32_t)C * 2u;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int c = (i % C4) * 2;
+    const int t = i / C4;
+    const int tx = t % TW;
+    const int r = t / TW;
+    const int ty = r % TH;
+    const int b = r / TH;
+    uint32_t raw[A][A], yv[A][A];
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
+        const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const uint32_t p = (uint32_t)(b * H * W + (in ? yy * W + xx : 0));
+        raw[a][e] = __builtin_amdgcn_raw_buffer_load_b32(gr, (p * (uint32_t)ldg + c) * 2u, 0, 0);
+        yv[a][e] = __builtin_amdgcn_raw_buffer_load_b32(yr_, (p * (uint32_t)ldy + c) * 2u, 0, 0);
+      }
+    const LV sc = *(const LV*)(scale + c), sh = *(const LV*)(shift + c);
+    const LV mu = *(const LV*)(mean + c);
+    const LV k1 = *(const LV*)(coef + c), k2 = *(const LV*)(coef + C + c),
+             k3 = *(const LV*)(coef + 2 * C + c);
+    const LV mk = mask ? *(const LV*)(mask + (size_t)b * C + c) : LV{} + 1.f;
+#pragma unroll
+    for (int a = 0; a < A; ++a)
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        const int yy = MT * ty - 1 + a, xx = MT * tx - 1 + e;
+        const bool in = (unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W;
+        const LV v = L::cvt(yv[a][e]);
+        LV dz = L::cvt(raw[a][e]) * L::lrg(v * sc + sh, slope);
+        if (mask) dz = dz * mk;
+        const LV d = k1 * dz + k2 * (v - mu) + k3;
+        raw[a][e] = in ? L::pack(d) : 0u;
+      }
+    const uint32_t vo = (uint32_t)(t * C + c) * 2u;
+    {
+      LV scv[A][A];
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        LV d[A];
+#pragma unroll
+        for (int e = 0; e < A; ++e) d[e] = L::cvt(raw[a][e]);
+        wcol_row<CBt<MT>>(scv, d, a);
+      }
+#pragma unroll
+      for (int a = 0; a < A; ++a) {
+        LV v[A];
+        wmat<CBt<MT>>(scv[a], v);
+#pragma unroll
+        for (int e = 0; e < A; ++e)
+          __builtin_amdgcn_raw_buffer_store_b32(pack_h2(v[e] * sv), vr, vo,
+                                                (int)((uint32_t)(a * A + e) * pbytes), 0);
+      }
+    }
+    LV scm[A][MT];
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      LV d[MT];
+#pragma unroll
+      for (int e = 0; e < MT; ++e) d[e] = L::cvt(raw[a + 1][e + 1]);
+      wcol_row<CA<MT>>(scm, d, a);
+    }
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      LV v[A];
+      wmat<CA<MT>>(scm[a], v);
+#pragma unroll
+      for (int e = 0; e < A; ++e)
+        __builtin_amdgcn_raw_buffer_store_b32(pack_h2(v[e] * sd), mr, vo,
+                                              (int)((uint32_t)(a * A + e) * pbytes), 0);
+    }
+  }
+}
+
 extern "C" int nsm_wino_dual_bn_f16(const void* g, int ldg, const void* y, int ldy, int B, int H, int W,
                                     int c_p, int tile, const float* scale, const float* shift,
                                     float slope, const float* mask, const float* mean,
@@ -4178,6 +4279,17 @@ extern "C" int nsm_wino_dual_bn_f16(const void* g, int ldg, const void* y, int l
   WinoGeom gm;
   NSM_CHECK_ARG(wino_geom(tile, B, H, W, gm), "wino_dual_bn_f16: bad shape");
   const int cw = f16_tx_cw();
+  const long long gbytes = (long long)B * H * W * ldg * 2, ybytes = (long long)B * H * W * ldy * 2,
+                  obytes = 36ll * gm.T * c_p * 2;
+  if (cw == 2 && f16_up_buf() && gbytes < 0x7FFFFFFFll && ybytes < 0x7FFFFFFFll &&
+      obytes < 0xFFFFFFFFll && gm.T * (c_p / 2) < (1ll << 31)) {
+    hipLaunchKernelGGL(wino_dual_bn_f16_buf_kernel<4>, dim3(grid_1d(gm.T * c_p / 2)), dim3(256), 0,
+                       as_stream(stream), (const bf16_t*)g, ldg, (const bf16_t*)y, ldy, H, W, c_p, gm.TH,
+                       gm.TW, (int)gm.T, scale, shift, slope, mask, mean, coef, (bf16_t*)V, (bf16_t*)dM,
+                       H2Scale{bound, wino_beta(4, 0)}, H2Scale{bound, wino_beta(4, 1)});
+    NSM_LAUNCH_CHECK("wino_dual_bn_f16");
+    return 0;
+  }
   hipLaunchKernelGGL((cw == 2 ? wino_dual_bn_f16_kernel<4, 2> : wino_dual_bn_f16_kernel<4, 4>),
                      dim3(grid_1d(gm.T * c_p / cw)), dim3(256), 0, as_stream(stream),
                      (const bf16_t*)g, ldg, (const bf16_t*)y, ldy, H, W, c_p, gm.TH, gm.TW, gm.T,
