@@ -3815,6 +3815,104 @@ extern "C" int nsm_wino_gemm_f16m(const void* V, const void* U, int B, int H, in
 
 // the output transform of nsm_wino_gemm_f16m's f16 M (same scale slots / bounds
 // as the GEMM call, cin_p its K) writing bf16 Y (+ the BN partials)
+// wino_output_kernel<4, STATS, false, true, true, 4> (the training step's
+// f16-M output transform) on 32-bit buffer offsets (host-checked: M under
+// 4 GiB, y under 2 GiB, T x N / 4 under 2^31): M's plane in the scalar offset
+// of one descriptor, y's pixel rows through another. Same arithmetic and
+// order, so the same bits and BN partials.
+template <bool STATS>
+__global__ void __launch_bounds__(256) wino_output_f16m_buf_kernel(
+    const bf16_t* __restrict__ M, int N, int H, int W, int TH, int TW, int T,
+    const float* __restrict__ bias, bf16_t* __restrict__ y, int ldy, float* __restrict__ partial,
+    WinoM16 m16) {
+  constexpr int MT = 4, A = 6, CW = 4;
+  using VT = f32x4;
+  const int ev = h2_exp(m16.sv), eu = h2_exp(m16.su);
+  const int N4 = N / CW;
+  const int total = T * N4;
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = T / (TH * TW);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)M, (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc_b(y, (long long)nb * H * W * ldy);
+  const uint32_t pbytes = (uint32_t)T * (uint32_t)N * 2u;
+  const float ieu = exp2i(-eu);
+  VT s_sum{}, s_mean{}, s_m2{};
+  float s_n = 0.f;
+  for (int i = i0; i < total; i += gridDim.x * blockDim.x) {
+    const int c = (i % N4) * CW;
+    const int t = i / N4;
+    const int tx = t % TW;
+    const int r = t / TW;
+    const int ty = r % TH;
+    const int b = r / TH;
+    const uint32_t mo = (uint32_t)(t * N + c) * 2u;
+    const int* et0 = m16.e + (t / 64) * (N / 64) + c / 64;
+    const int estep = m16.rows * (N / 64);
+    VT sc[MT][A], o[MT][MT];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      VT row[A];
+#pragma unroll
+      for (int e = 0; e < A; ++e) {
+        int x = -et0[(a * A + e) * estep] - ev;
+        x = x < -126 ? -126 : (x > 126 ? 126 : x);
+        const u32x2 h = __builtin_bit_cast(
+            u32x2, __builtin_amdgcn_raw_buffer_load_b64(mr, mo, (int)((uint32_t)(a * A + e) * pbytes), 0));
+        const f32x2 lo = unpack_h2(h.x), hi = unpack_h2(h.y);
+        row[e] = VT{lo.x, lo.y, hi.x, hi.y} * (exp2i(x) * ieu);
+      }
+      wcol_row<CAt<MT>>(sc, row, a);
+    }
+#pragma unroll
+    for (int a = 0; a < MT; ++a) wmat<CAt<MT>>(sc[a], o[a]);
+    const VT bv = bias ? *(const VT*)(bias + c) : VT{};
+    VT ts{};
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      const int yy = MT * ty + a;
+      if (yy >= H) continue;
+      const uint32_t ro = (uint32_t)(((b * H + yy) * W + MT * tx) * ldy + c) * 2u;
+#pragma unroll
+      for (int e = 0; e < MT; ++e)
+        if (MT * tx + e < W) {
+          o[a][e] = o[a][e] + bv;
+          const VT q = o[a][e];
+          o[a][e] = VT{round_bf(q.x), round_bf(q.y), round_bf(q.z), round_bf(q.w)};
+          const u32x2 w = u32x2{pack_bf2(o[a][e].x, o[a][e].y), pack_bf2(o[a][e].z, o[a][e].w)};
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(mr, 0u, 0, 0)), w),
+                                                yr, ro + (uint32_t)(e * ldy) * 2u, 0, 0);
+          if (STATS) ts = ts + o[a][e];
+        }
+    }
+    if (STATS) {
+      const int nv = min(MT, H - MT * ty) * min(MT, W - MT * tx);
+      const VT tmean = ts * (1.f / (float)nv);
+      VT tq{};
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int e = 0; e < MT; ++e)
+          if (MT * ty + a < H && MT * tx + e < W) {
+            const VT d = o[a][e] - tmean;
+            tq = tq + d * d;
+          }
+      const float n2 = s_n + (float)nv;
+      const VT delta = tmean - s_mean;
+      s_mean = s_mean + delta * ((float)nv / n2);
+      s_m2 = s_m2 + tq + delta * delta * (s_n * (float)nv / n2);
+      s_sum = s_sum + ts;
+      s_n = n2;
+    }
+  }
+  if (STATS && i0 < (int)(gridDim.x * blockDim.x)) {
+    const int c = (i0 % N4) * CW;
+    float* pr = partial + (size_t)(i0 / N4) * 3 * N + c;
+    *(VT*)pr = s_sum;
+    *(VT*)(pr + N) = s_m2;
+    *(VT*)(pr + 2 * N) = VT{} + s_n;
+  }
+}
+
 extern "C" int nsm_wino_output_bf16m(const void* M16, const int* m16e, int B, int H, int W, int cin_p,
                                      int cout_p, int tile, const uint32_t* amax_v, float beta_v,
                                      const uint32_t* amax_u, float beta_u, const float* bias,
@@ -3836,6 +3934,18 @@ extern "C" int nsm_wino_output_bf16m(const void* M16, const int* m16e, int B, in
   }
   const WinoM16 m16{H2Scale{amax_v, beta_v}, H2Scale{amax_u, beta_u}, m16e, (int)((g.T + 63) / 64)};
   hipStream_t s = as_stream(stream);
+  const long long mbytes = 36ll * g.T * cout_p * 2, ybytes = (long long)B * H * W * ldy * 2;
+  if (cw == 4 && f16_up_buf() && mbytes < 0xFFFFFFFFll && ybytes < 0x7FFFFFFFll &&
+      g.T * (cout_p / 4) < (1ll << 31)) {
+    if (partial)
+      hipLaunchKernelGGL(wino_output_f16m_buf_kernel<true>, grid, dim3(256), 0, s, (const bf16_t*)M16,
+                         cout_p, H, W, g.TH, g.TW, (int)g.T, bias, (bf16_t*)y, ldy, partial, m16);
+    else
+      hipLaunchKernelGGL(wino_output_f16m_buf_kernel<false>, grid, dim3(256), 0, s, (const bf16_t*)M16,
+                         cout_p, H, W, g.TH, g.TW, (int)g.T, bias, (bf16_t*)y, ldy, nullptr, m16);
+    NSM_LAUNCH_CHECK("wino_output_bf16m");
+    return 0;
+  }
 #define NSM_OUT16(STATS_, CW_)                                                                      \
   hipLaunchKernelGGL((wino_output_kernel<4, STATS_, false, true, true, CW_>), grid, dim3(256), 0, s, \
                      (const float*)M16, cout_p, H, W, g.TH, g.TW, g.T, bias, (float*)y, ldy,        \
