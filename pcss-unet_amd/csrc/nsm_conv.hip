@@ -2851,9 +2851,116 @@ static void launch_wino_output(dim3 grid, hipStream_t s, const float* Mb, int co
     hipLaunchKernelGGL((wino_output_kernel<MT, false, false, false, false, CWX>), grid, dim3(256), 0, s,
                        Mb, cout_p, H, W, g.TH, g.TW, g.T, bias, y, ldy, partial);
 }
+// wino_output_kernel<6, STATS, false, false, false, 2> (the fp32 step's F(6x6)
+// output transform) on 32-bit buffer offsets (host-checked: M under 4 GiB, y
+// under 2 GiB, T x N / 2 under 2^31): M's plane in the scalar offset of one
+// descriptor, y's rows through another. Same arithmetic and order.
+template <bool STATS>
+__global__ void __launch_bounds__(256) wino_output6_buf_kernel(const float* __restrict__ Mb, int N,
+                                                               int H, int W, int TH, int TW, int T,
+                                                               const float* __restrict__ bias,
+                                                               float* __restrict__ y, int ldy,
+                                                               float* __restrict__ partial) {
+  constexpr int MT = 6, A = 8, CW = 2;
+  using VT = f32x2;
+  const int N4 = N / CW;
+  const int total = T * N4;
+  const int i0 = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nb = T / (TH * TW);
+  const __amdgpu_buffer_rsrc_t mr = __builtin_amdgcn_make_buffer_rsrc((void*)Mb, (short)0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t yr = make_rsrc(y, (long long)nb * H * W * ldy);
+  const uint32_t pbytes = (uint32_t)T * (uint32_t)N * 4u;
+  VT s_sum{}, s_mean{}, s_m2{};
+  float s_n = 0.f;
+  for (int i = i0; i < total; i += gridDim.x * blockDim.x) {
+    const int c = (i % N4) * CW;
+    const int t = i / N4;
+    const int tx = t % TW;
+    const int r = t / TW;
+    const int ty = r % TH;
+    const int b = r / TH;
+    const uint32_t mo = (uint32_t)(t * N + c) * 4u;
+    VT sc[MT][A], o[MT][MT];
+#pragma unroll
+    for (int a = 0; a < A; ++a) {
+      VT row[A];
+#pragma unroll
+      for (int e = 0; e < A; ++e)
+        row[e] = __builtin_bit_cast(VT, __builtin_amdgcn_raw_buffer_load_b64(
+                                            mr, mo, (int)((uint32_t)(a * A + e) * pbytes), 0));
+      wcol_row<CAt<MT>>(sc, row, a);
+    }
+#pragma unroll
+    for (int a = 0; a < MT; ++a) wmat<CAt<MT>>(sc[a], o[a]);
+    const VT bv = bias ? *(const VT*)(bias + c) : VT{};
+    VT ts{};
+#pragma unroll
+    for (int a = 0; a < MT; ++a) {
+      const int yy = MT * ty + a;
+      if (yy >= H) continue;
+      const uint32_t ro = (uint32_t)(((b * H + yy) * W + MT * tx) * ldy + c) * 4u;
+#pragma unroll
+      for (int e = 0; e < MT; ++e)
+        if (MT * tx + e < W) {
+          o[a][e] = o[a][e] + bv;
+          __builtin_amdgcn_raw_buffer_store_b64(
+              __builtin_bit_cast(decltype(__builtin_amdgcn_raw_buffer_load_b64(mr, 0u, 0, 0)), o[a][e]),
+              yr, ro + (uint32_t)(e * ldy) * 4u, 0, 0);
+          if (STATS) ts = ts + o[a][e];
+        }
+    }
+    if (STATS) {
+      const int nv = min(MT, H - MT * ty) * min(MT, W - MT * tx);
+      const VT tmean = ts * (1.f / (float)nv);
+      VT tq{};
+#pragma unroll
+      for (int a = 0; a < MT; ++a)
+#pragma unroll
+        for (int e = 0; e < MT; ++e)
+          if (MT * ty + a < H && MT * tx + e < W) {
+            const VT d = o[a][e] - tmean;
+            tq = tq + d * d;
+          }
+      const float n2 = s_n + (float)nv;
+      const VT delta = tmean - s_mean;
+      s_mean = s_mean + delta * ((float)nv / n2);
+      s_m2 = s_m2 + tq + delta * delta * (s_n * (float)nv / n2);
+      s_sum = s_sum + ts;
+      s_n = n2;
+    }
+  }
+  if (STATS && i0 < (int)(gridDim.x * blockDim.x)) {
+    const int c = (i0 % N4) * CW;
+    float* pr = partial + (size_t)(i0 / N4) * 3 * N + c;
+    *(VT*)pr = s_sum;
+    *(VT*)(pr + N) = s_m2;
+    *(VT*)(pr + 2 * N) = VT{} + s_n;
+  }
+}
+
+// NSM_F6_OUT_BUF=0: the generic kernel for the fp32 F(6x6) output transform
+static bool f6_out_buf() {
+  static bool v = [] {
+    const char* e = getenv("NSM_F6_OUT_BUF");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 static void launch_wino_output6(dim3 grid, hipStream_t s, const float* Mb, int cout_p, int H, int W,
                                 const WinoGeom& g, const float* bias, float* y, int ldy,
                                 float* partial, const WinoAct* act = nullptr) {
+  const long long B = g.T / ((long long)g.TH * g.TW);
+  if (f6_out_cw() == 2 && !act && f6_out_buf() && 64ll * g.T * cout_p * 4 < 0xFFFFFFFFll &&
+      B * H * W * ldy * 4 < 0x7FFFFFFFll && g.T * (cout_p / 2) < (1ll << 31)) {
+    if (partial)
+      hipLaunchKernelGGL(wino_output6_buf_kernel<true>, grid, dim3(256), 0, s, Mb, cout_p, H, W, g.TH,
+                         g.TW, (int)g.T, bias, y, ldy, partial);
+    else
+      hipLaunchKernelGGL(wino_output6_buf_kernel<false>, grid, dim3(256), 0, s, Mb, cout_p, H, W, g.TH,
+                         g.TW, (int)g.T, bias, y, ldy, nullptr);
+    return;
+  }
   if (f6_out_cw() == 2)
     launch_wino_output<6, 2>(grid, s, Mb, cout_p, H, W, g, bias, y, ldy, partial, act);
   else
