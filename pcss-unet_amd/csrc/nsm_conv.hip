@@ -2810,6 +2810,18 @@ static int wino_stat_resident(int tile) {
   cache[tile] = (e == hipSuccess && per > 0 && cus > 0) ? per * cus : 1024;
   return cache[tile];
 }
+// NSM_WINO_STAT_SMALL=0: layers with fewer tiles than the policy's slot count
+// (conv3-conv6 of the fp32 step) write Y without statistics and a separate
+// bn_stats pass re-reads it; default: the statistics form at one slot per
+// tile (the plain form's grid), capped at one resident round as below.
+// Interleaved A/B, fp32 B=8 step: conv6 71.8 + 46 (bn_stats) -> 77.9 us
+static bool wino_stat_small() {
+  static bool v = [] {
+    const char* e = getenv("NSM_WINO_STAT_SMALL");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
 static long long wino_stat_slots(long long T, int cout_p, int tile) {
   const int N4 = cout_p / wino_out_cw(tile), step = wino_stat_step(cout_p, tile);
   // the policy (stats form where a thread covers >= 2 tiles) is judged on
@@ -2819,7 +2831,11 @@ static long long wino_stat_slots(long long T, int cout_p, int tile) {
   if (ns < 512) ns = 512;
   ns = ns / step * step;
   if (ns < step) ns = step;
-  if (T < 2 * ns) return 0;
+  if (T < 2 * ns) {
+    if (!wino_stat_small()) return 0;
+    ns = T / step * step;
+    if (ns < step) return 0;
+  }
   long long nr = ((long long)wino_stat_resident(tile) * 256) / N4;
   nr = nr / step * step;
   if (nr >= step && nr < ns) ns = nr;
