@@ -550,8 +550,9 @@ def _summary(r):
            "roofline": {k: roof.get(k) for k in ("achieved", "frac", "avg_launch_ms", "traffic")}}
     if "dp" in r:
         out["dp"] = r["dp"]
-    if "eager" in r:
-        out["eager"] = {k: r["eager"][k] for k in ("value", "ms_per_step", "steps")}
+    for k2 in ("eager", "graph"):
+        if k2 in r:
+            out[k2] = {k: r[k2][k] for k in ("value", "ms_per_step", "steps")}
     if r["config"]["workload"].startswith(("configs[2]", "configs[3]")):
         out["stages"] = r["stages"]
     if "vgg_perceptual" in r:
@@ -661,36 +662,50 @@ def train_measure(args, world, rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # one process: the whole step (forward, loss, backward, the device tail)
-    # replayed from one HIP graph (nsm_amd.GraphedTrainStep: dropout masks from
-    # the graph-safe generator, new every replay); the kernel / stage timings
-    # below come from eager steps of the same shapes (HIP events cannot be read
-    # from inside a replayed graph). NSM_GRAPH_STEP=0: eager timed steps.
-    graphed = None
+    # The headline times the eager step: what an unchanged main.py loop and
+    # every DP rank run, with the weight gradients on the side stream. At N = 1
+    # the same step replayed from one HIP graph (nsm_amd.GraphedTrainStep:
+    # dropout masks from the graph-safe generator, new every replay) is timed
+    # after it and reported beside it ("graph"). Interleaved A/B, fp32 B=8, one
+    # box: eager 797.8 / 798.5 / 798.3 frames/s vs replay 771.7 / 769.0 / 769.0
+    # (a replay runs its nodes in order, so the side stream's overlap is lost).
+    # NSM_BENCH_STEP=graph: the replay is the headline (the eager step beside it).
+    # The kernel / stage timings below come from eager steps of the same shapes.
+    head_graph = os.environ.get("NSM_BENCH_STEP", "eager") == "graph"
+    graphed, dp_ms = None, None
     dp_tags = ("dp.bn_broadcast", "dp.allreduce_wait")
-    eager_elapsed, eager_steps = None, max(3, min(args.steps, 10))
-    # one process: the step replayed from one graph; N > 1 ranks run eager
-    # steps unless NSM_GRAPH_DP=1 (the captured DP step, collectives inside)
-    if os.environ.get("NSM_GRAPH_STEP", "1") != "0" and (
-            world == 1 or os.environ.get("NSM_GRAPH_DP", "0") == "1"):
+    side_elapsed, side_steps = None, max(3, min(args.steps, 20))
+    # one process: the graph too; N > 1 ranks run eager steps only unless
+    # NSM_GRAPH_DP=1 (the captured DP step, collectives inside)
+    want_graph = os.environ.get("NSM_GRAPH_STEP", "1") != "0" and (
+        world == 1 or os.environ.get("NSM_GRAPH_DP", "0") == "1")
+    if want_graph and head_graph:
         graphed = nsm_amd.GraphedTrainStep(model, crit, opt, x, y, loss_scale=loss_scale,
                                            warmup=1)
         for _ in range(args.warmup):
             graphed()
         torch.cuda.synchronize()
         elapsed = timed(graphed, args.steps, world, dev)
-        # the eager step (what an unchanged main.py and every DP rank run),
-        # timed back to back like the replays; only the DP waits carry events
+        # the eager step beside it; only the DP waits carry events
         if dp:
             for t in dp_tags:
                 nops.PROBES[t] = []
-        eager_elapsed = timed(step, eager_steps, world, dev)
+        side_elapsed = timed(step, side_steps, world, dev)
     else:
-        # eager timed steps (DP ranks): only the DP waits carry HIP events
+        # eager timed steps: only the DP waits carry HIP events
         for t in dp_tags:
             nops.PROBES[t] = []
         elapsed = timed(step, args.steps, world, dev)
-    dp_ms = {t: mean_ms(nops.PROBES.pop(t, [])) for t in dp_tags}
+        dp_ms = {t: mean_ms(nops.PROBES.pop(t, [])) for t in dp_tags}
+        if want_graph:
+            graphed = nsm_amd.GraphedTrainStep(model, crit, opt, x, y, loss_scale=loss_scale,
+                                               warmup=1)
+            for _ in range(args.warmup):
+                graphed()
+            torch.cuda.synchronize()
+            side_elapsed = timed(graphed, side_steps, world, dev)
+    if dp_ms is None:
+        dp_ms = {t: mean_ms(nops.PROBES.pop(t, [])) for t in dp_tags}
 
     # attribution steps (not timed): kernel and stage times from HIP events
     # with the weight gradients on the main stream, the configuration the
@@ -781,19 +796,26 @@ def train_measure(args, world, rank, dev):
         "stage_pmc_source": measured_src,
         "roofline": roof,
         "step_execution": ("one hipGraph replay per step (nsm_amd.GraphedTrainStep)"
-                           if graphed is not None else
-                           "eager (weight gradients on the side stream)"),
+                           if head_graph and graphed is not None else
+                           "eager, back to back (an unchanged main.py loop; the per-rank step "
+                           "of data parallelism), weight gradients on the side stream"),
         "stage_execution": "eager attribution steps after the timed ones, weight gradients on "
                            "the main stream (NSM_WGRAD_STREAM=0: the configuration of the "
                            "stage PMC), HIP events per stage",
     }
-    if eager_elapsed is not None:
-        res["eager"] = {"value": round(world * B * eager_steps / eager_elapsed, 3),
-                        "ms_per_step": round(eager_elapsed / eager_steps * 1e3, 3),
-                        "steps": eager_steps,
-                        "what": "the same step run eagerly (an unchanged main.py loop; the "
-                                "per-rank step of data parallelism), back to back, weight "
-                                "gradients on the side stream"}
+    if side_elapsed is not None:
+        side = {"value": round(world * B * side_steps / side_elapsed, 3),
+                "ms_per_step": round(side_elapsed / side_steps * 1e3, 3),
+                "steps": side_steps}
+        if head_graph:
+            side["what"] = ("the same step run eagerly (an unchanged main.py loop; the per-rank "
+                            "step of data parallelism), back to back, weight gradients on the "
+                            "side stream")
+            res["eager"] = side
+        else:
+            side["what"] = ("the same step replayed from one hipGraph (nsm_amd.GraphedTrainStep), "
+                            "timed after the headline's eager steps")
+            res["graph"] = side
     if dp:
         res["dp"] = {"bn_broadcast_ms": round(dp_ms["dp.bn_broadcast"], 4),
                      "allreduce_wait_ms": round(dp_ms["dp.allreduce_wait"], 4),
