@@ -18,6 +18,10 @@ resident in HBM and requiring grad like the reference's batches
 Step = forward + 0.9*L1 + backward + RCCL grad all-reduce (N > 1, overlapped
 with the backward) + the reference's whole step tail on the device
 (main.py:287-423: sanitise, per-parameter clips, clip_grad_norm_, AdamW).
+The timed steps run eagerly, back to back, as an unchanged main.py loop runs
+them (weight gradients on the side stream); at N = 1 the same step replayed
+from one HIP graph is timed after them and reported beside the headline
+("graph"; NSM_BENCH_STEP=graph swaps the two).
 
 Rank 0 prints ONE JSON line with the metric, a roofline object for the
 dominant convolution (conv6.conv.0 forward, 3x3 1024->1024: Winograd input
