@@ -1,5 +1,7 @@
 """GPU: each libnsm kernel family against the PyTorch-CPU fp32 op it replaces
 (same seeded inputs), through the C ABI (nsm_amd.ops -> ctypes -> libnsm.so)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -192,6 +194,11 @@ def test_wino_output_bn_stats(ops, device, B, H, W, ci, co, tile):
     tuned = int(lib.nsm_wino_stat_slots(B, H, W, co, tile))
     if (B, H, W) == (8, 256, 256):
         assert tuned > 1024  # conv8 / conv9 geometry: the stats form with a merge
+    T = B * -(-H // tile) * -(-W // tile)
+    if T >= step and os.environ.get("NSM_WINO_STAT_SMALL", "1") != "0":
+        # every layer with a slot's worth of tiles takes the statistics form
+        # (below the policy's slot count: one slot per tile, no bn_stats pass)
+        assert tuned > 0 and tuned % step == 0, (T, step, tuned)
     for ns in sorted({tuned, step, step * -(-1100 // step)} - {0}):
         y, _, part = ops.conv3x3_wino(nhwc(x).to(device), B, H, W, U, b.to(device), co, tile=tile,
                                       stats=True, nslot=ns)
