@@ -48,8 +48,10 @@ sys.path.insert(0, ROOT)
 # at 8 (753.9 without DP); bf16 B=64 eager unchanged. Not for the captured
 # step: the bf16 B=64 graph drops from 1639-1641 to 1480-1491 at 8 queues (its
 # weight-gradient branch then truly runs beside the critical path, whose GEMMs
-# are sized for the whole chip). Set before torch initialises HIP.
-if int(os.environ.get("WORLD_SIZE", "1")) > 1 and os.environ.get("NSM_GRAPH_DP", "0") != "1":
+# are sized for the whole chip). Set before torch initialises HIP. --force-dp
+# (the per-rank DP step at N = 1, eager in the headline) takes them too.
+if ((int(os.environ.get("WORLD_SIZE", "1")) > 1 or "--force-dp" in sys.argv)
+        and os.environ.get("NSM_GRAPH_DP", "0") != "1"):
     os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 import numpy as np  # noqa: E402
