@@ -18,10 +18,10 @@ resident in HBM and requiring grad like the reference's batches
 Step = forward + 0.9*L1 + backward + RCCL grad all-reduce (N > 1, overlapped
 with the backward) + the reference's whole step tail on the device
 (main.py:287-423: sanitise, per-parameter clips, clip_grad_norm_, AdamW).
-The timed steps run eagerly, back to back, as an unchanged main.py loop runs
-them (weight gradients on the side stream); at N = 1 the same step replayed
-from one HIP graph is timed after them and reported beside the headline
-("graph"; NSM_BENCH_STEP=graph swaps the two).
+The step is timed eagerly, back to back, as an unchanged main.py loop runs it
+(weight gradients on the side stream), and at N = 1 also replayed from one HIP
+graph; both over K steps, the faster is the headline and the other is reported
+beside it ("graph" or "eager"; NSM_BENCH_STEP=eager|graph fixes the headline).
 
 Rank 0 prints ONE JSON line with the metric, a roofline object for the
 dominant convolution (conv6.conv.0 forward, 3x3 1024->1024: Winograd input
@@ -436,15 +436,19 @@ def init_dist(args):
         if world > 1:
             dist.init_process_group("gloo")
         return world, rank, torch.device("cpu")
-    if world > 1:
+    if world > 1 or (getattr(args, "force_dp", False) and not dist.is_initialized()):
+        import nsm_amd
         torch.cuda.set_device(local)
+        # the weight-gradient side stream on a hardware queue of its own,
+        # before RCCL's streams take the free ones (nsm_amd.reserve_side_stream)
+        nsm_amd.reserve_side_stream(torch.device("cuda", local))
+    if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         assert dist.get_world_size() == args.gpus
     elif getattr(args, "force_dp", False) and not dist.is_initialized():
         # --force-dp at N=1: the data-parallel step over a world-size-1 RCCL group
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
-        torch.cuda.set_device(local)
         dist.init_process_group("nccl", rank=0, world_size=1,
                                 device_id=torch.device("cuda", local))
     return world, rank, torch.device("cuda", local)
@@ -559,6 +563,7 @@ def _summary(r):
     for k2 in ("eager", "graph"):
         if k2 in r:
             out[k2] = {k: r[k2][k] for k in ("value", "ms_per_step", "steps")}
+            out["execution"] = "graph" if k2 == "eager" else "eager"   # the headline's
     if r["config"]["workload"].startswith(("configs[2]", "configs[3]")):
         out["stages"] = r["stages"]
     if "vgg_perceptual" in r:
@@ -668,16 +673,19 @@ def train_measure(args, world, rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # The headline times the eager step: what an unchanged main.py loop and
-    # every DP rank run, with the weight gradients on the side stream. At N = 1
-    # the same step replayed from one HIP graph (nsm_amd.GraphedTrainStep:
-    # dropout masks from the graph-safe generator, new every replay) is timed
-    # after it and reported beside it ("graph"). Interleaved A/B, fp32 B=8, one
-    # box: eager 797.8 / 798.5 / 798.3 frames/s vs replay 771.7 / 769.0 / 769.0
-    # (a replay runs its nodes in order, so the side stream's overlap is lost).
-    # NSM_BENCH_STEP=graph: the replay is the headline (the eager step beside it).
-    # The kernel / stage timings below come from eager steps of the same shapes.
-    head_graph = os.environ.get("NSM_BENCH_STEP", "eager") == "graph"
+    # Two executions of the same step: eager (what an unchanged main.py loop and
+    # every DP rank run, the weight gradients on the side stream) and, at N = 1,
+    # the replay of one HIP graph (nsm_amd.GraphedTrainStep: dropout masks from
+    # the graph-safe generator, new every replay). NSM_BENCH_STEP=auto (default)
+    # times both over K steps and reports the faster as the headline, the other
+    # beside it: the eager step wins where the host keeps ahead of the GPU (its
+    # side-stream overlap; interleaved A/B on one box: eager 797.8 / 798.5 /
+    # 798.3 frames/s vs replay 771.7 / 769.0 / 769.0), the replay where the host
+    # is slow. eager / graph: that mode is the headline, the other timed over
+    # min(K, 20) steps beside it. The kernel / stage timings below come from
+    # eager steps of the same shapes.
+    mode = os.environ.get("NSM_BENCH_STEP", "auto")
+    head_graph = mode == "graph"
     graphed, dp_ms = None, None
     dp_tags = ("dp.bn_broadcast", "dp.allreduce_wait")
     side_elapsed, side_steps = None, max(3, min(args.steps, 20))
@@ -709,7 +717,13 @@ def train_measure(args, world, rank, dev):
             for _ in range(args.warmup):
                 graphed()
             torch.cuda.synchronize()
-            side_elapsed = timed(graphed, side_steps, world, dev)
+            g_steps = args.steps if mode == "auto" else side_steps
+            g_elapsed = timed(graphed, g_steps, world, dev)
+            if mode == "auto" and g_elapsed < elapsed:
+                # the replay is the faster execution on this machine
+                side_elapsed, side_steps, elapsed, head_graph = elapsed, args.steps, g_elapsed, True
+            else:
+                side_elapsed, side_steps = g_elapsed, g_steps
     if dp_ms is None:
         dp_ms = {t: mean_ms(nops.PROBES.pop(t, [])) for t in dp_tags}
 
@@ -813,6 +827,9 @@ def train_measure(args, world, rank, dev):
         side = {"value": round(world * B * side_steps / side_elapsed, 3),
                 "ms_per_step": round(side_elapsed / side_steps * 1e3, 3),
                 "steps": side_steps}
+        side["headline_choice"] = ("NSM_BENCH_STEP=%s: %s" % (
+            mode, "the faster of the two executions, each timed over K steps" if mode == "auto"
+            else "fixed"))
         if head_graph:
             side["what"] = ("the same step run eagerly (an unchanged main.py loop; the per-rank "
                             "step of data parallelism), back to back, weight gradients on the "
@@ -820,7 +837,7 @@ def train_measure(args, world, rank, dev):
             res["eager"] = side
         else:
             side["what"] = ("the same step replayed from one hipGraph (nsm_amd.GraphedTrainStep), "
-                            "timed after the headline's eager steps")
+                            "timed after the eager steps")
             res["graph"] = side
     if dp:
         res["dp"] = {"bn_broadcast_ms": round(dp_ms["dp.bn_broadcast"], 4),

@@ -5,7 +5,7 @@ HIP kernels (libnsm.so), behind the reference's Python surface.
 Importing this package loads libnsm.so and fails loudly if it is missing.
 """
 from ._lib import LIB_PATH, NsmError, lib  # noqa: F401  (loads the HIP library)
-from .unet import DoubleConv, Unet  # noqa: F401
+from .unet import DoubleConv, Unet, reserve_side_stream  # noqa: F401
 from .losses import (CustomLoss, EnhancedCustomLoss, L1Loss, PerturbationLoss,  # noqa: F401
                      l1_loss, measure_temporal_instability)
 from .optim import FlatAdamW, allreduce_grads, flat_grad  # noqa: F401

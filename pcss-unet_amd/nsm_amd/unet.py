@@ -165,6 +165,28 @@ WGRAD_HOLD_BYTES = int(float(os.environ.get("NSM_WGRAD_HOLD_GB", "8")) * (1 << 3
 _wg_hold = []
 
 
+def reserve_side_stream(device=None):
+    """Create the weight-gradient side stream of `device` and bind it, and the
+    current stream, to hardware queues now (one small launch on each). HIP binds
+    a stream at its first launch to the least used of GPU_MAX_HW_QUEUES queues;
+    RCCL's and ProcessGroupNCCL's streams, created by init_process_group, would
+    otherwise take the free queues first and leave the side stream on the
+    current stream's queue, serialised with it (the eager DP step at world size
+    1: side and main kernels on one queue even at 8 queues, round-6 trace). Call
+    it before torch.distributed.init_process_group."""
+    dev = (torch.device(device) if device is not None
+           else torch.device("cuda", torch.cuda.current_device()))
+    s = _wg_streams.get(dev)
+    if s is None:
+        s = _wg_streams[dev] = torch.cuda.Stream(device=dev, priority=WGRAD_PRIO)
+    buf = torch.empty(64, dtype=torch.int32, device=dev)
+    call("nsm_zero_u32", ptr(buf), buf.numel(), stream())
+    with torch.cuda.stream(s):
+        call("nsm_zero_u32", ptr(buf), buf.numel(), stream())
+    torch.cuda.synchronize(dev)
+    return s
+
+
 def _allreduce_bucket(flat, lo, hi, group):
     """Start the bucket's gradient all-reduce once both the current stream's
     work so far (biases, BN parameters) and the weight gradients queued on the
