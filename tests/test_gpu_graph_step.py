@@ -159,3 +159,14 @@ def test_eager_steps_back_to_back_keep_memory_flat(device):
         step()
     torch.cuda.synchronize()
     assert torch.cuda.memory_stats()["num_device_alloc"] == r0
+
+
+def test_reserve_side_stream_is_the_backward_side_stream(device):
+    """nsm_amd.reserve_side_stream (called before init_process_group by DP
+    ranks, bench.py) creates and binds the very stream the Unet backward then
+    runs its weight gradients on, once per device."""
+    import nsm_amd
+    from nsm_amd import unet
+    s = nsm_amd.reserve_side_stream(device)
+    assert unet._wg_streams[torch.device(device)] is s
+    assert nsm_amd.reserve_side_stream(device) is s
